@@ -1,0 +1,192 @@
+// bsm_internal.hpp -- shared internals of libbsm_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/bsm.h"
+
+namespace bsm {
+
+// ---------------------------------------------------------------------------
+// errors: thread-local message + status codes
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+#define BSM_HIP_TRY(expr)                                                                   \
+    do {                                                                                    \
+        hipError_t bsm_e_ = (expr);                                                         \
+        if (bsm_e_ != hipSuccess) {                                                         \
+            ::bsm::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(bsm_e_),     \
+                             __FILE__, __LINE__);                                           \
+            return bsm_e_ == hipErrorOutOfMemory ? BSM_ERR_OOM : BSM_ERR_HIP;               \
+        }                                                                                   \
+    } while (0)
+
+#define BSM_TRY(expr)                 \
+    do {                              \
+        int bsm_rc_ = (expr);         \
+        if (bsm_rc_ != BSM_OK) return bsm_rc_; \
+    } while (0)
+
+#define BSM_REQUIRE(cond, code, ...)           \
+    do {                                       \
+        if (!(cond)) {                         \
+            ::bsm::set_error(__VA_ARGS__);     \
+            return (code);                     \
+        }                                      \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// arithmetic with the reference's semantics: IEEE, no contraction, integers
+// wrap (Cargo.toml:18). Signed integers are computed in the same-width
+// unsigned type so device code never hits C++ signed-overflow UB.
+// ---------------------------------------------------------------------------
+template <typename T> struct Arith;
+template <> struct Arith<double> {
+    __device__ __forceinline__ static double add(double a, double b) { return __dadd_rn(a, b); }
+    __device__ __forceinline__ static double sub(double a, double b) { return __dsub_rn(a, b); }
+    __device__ __forceinline__ static double mul(double a, double b) { return __dmul_rn(a, b); }
+    __device__ __forceinline__ static bool nz(double v) { return !(v == 0.0); }
+    __device__ __forceinline__ static double zero() { return 0.0; }
+    __device__ __forceinline__ static double neg_zero() { return -0.0; }
+};
+template <> struct Arith<float> {
+    __device__ __forceinline__ static float add(float a, float b) { return __fadd_rn(a, b); }
+    __device__ __forceinline__ static float sub(float a, float b) { return __fsub_rn(a, b); }
+    __device__ __forceinline__ static float mul(float a, float b) { return __fmul_rn(a, b); }
+    __device__ __forceinline__ static bool nz(float v) { return !(v == 0.0f); }
+    __device__ __forceinline__ static float zero() { return 0.0f; }
+    __device__ __forceinline__ static float neg_zero() { return -0.0f; }
+};
+template <typename T, typename U> struct ArithInt {
+    __device__ __forceinline__ static T add(T a, T b) { return (T)((U)a + (U)b); }
+    __device__ __forceinline__ static T sub(T a, T b) { return (T)((U)a - (U)b); }
+    __device__ __forceinline__ static T mul(T a, T b) { return (T)((U)a * (U)b); }
+    __device__ __forceinline__ static bool nz(T v) { return v != 0; }
+    __device__ __forceinline__ static T zero() { return 0; }
+    __device__ __forceinline__ static T neg_zero() { return 0; }
+};
+template <> struct Arith<int32_t> : ArithInt<int32_t, uint32_t> {};
+template <> struct Arith<uint32_t> : ArithInt<uint32_t, uint32_t> {};
+template <> struct Arith<int64_t> : ArithInt<int64_t, uint64_t> {};
+template <> struct Arith<uint64_t> : ArithInt<uint64_t, uint64_t> {};
+
+template <typename T> struct IsFloat { static constexpr bool value = false; };
+template <> struct IsFloat<double> { static constexpr bool value = true; };
+template <> struct IsFloat<float> { static constexpr bool value = true; };
+
+inline size_t dtype_size(int dt) {
+    switch (dt) {
+        case BSM_F64: case BSM_I64: case BSM_U64: return 8;
+        case BSM_F32: case BSM_I32: case BSM_U32: return 4;
+        default: return 0;
+    }
+}
+
+// Invoke F.template operator()<T>() for the runtime dtype.
+template <typename F> int dispatch_dtype(int dt, F&& f) {
+    switch (dt) {
+        case BSM_F64: return f.template operator()<double>();
+        case BSM_F32: return f.template operator()<float>();
+        case BSM_I32: return f.template operator()<int32_t>();
+        case BSM_U32: return f.template operator()<uint32_t>();
+        case BSM_I64: return f.template operator()<int64_t>();
+        case BSM_U64: return f.template operator()<uint64_t>();
+        default: set_error("unknown dtype %d", dt); return BSM_ERR_INVALID;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// device context: one non-blocking stream per device, created lazily.
+// ---------------------------------------------------------------------------
+int current_device(int* dev);
+int ctx_stream(hipStream_t* s);  // stream of the calling thread's device
+
+// RAII device buffer for host-path temporaries.
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int alloc(size_t n) {
+        reset();
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e != hipSuccess) {
+            p = nullptr;
+            set_error("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? BSM_ERR_OOM : BSM_ERR_HIP;
+        }
+        bytes = n;
+        return BSM_OK;
+    }
+    void* release() {
+        void* q = p;
+        p = nullptr;
+        bytes = 0;
+        return q;
+    }
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace bsm
+
+// Device-resident finalised Csr<T>.
+struct bsm_csr {
+    int dtype = BSM_F64;
+    int device = 0;
+    uint64_t rows = 0, cols = 0, nnz = 0;
+    int64_t* row_ptr = nullptr;  // rows+1
+    int32_t* col = nullptr;      // nnz
+    void* vals = nullptr;        // nnz * sizeof(T)
+    // lazily computed analysis (see bsm_analyse)
+    bool analysed = false;
+    bool rows_sorted = true;  // col non-decreasing inside every row
+    uint64_t max_row_len = 0;
+};
+
+namespace bsm {
+int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz);
+int csr_analyse(bsm_csr* m, hipStream_t s);
+
+// kernels (kernels_*.hip), all async on stream s
+uint64_t scan_workspace_bytes(uint64_t n);
+int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void* ws,
+                              uint64_t ws_bytes, hipStream_t s);  // out has n+1 entries
+int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
+                  const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
+                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s);
+int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
+                     int32_t* out_col, void* out_vals, hipStream_t s);
+int pack_cols_to_rowmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor, void* rowmajor,
+                          hipStream_t s);
+int unpack_rowmajor_to_cols(int dtype, uint64_t n, uint64_t k, const void* rowmajor,
+                            void* colmajor, hipStream_t s);
+int transpose_dispatch(const bsm_csr* a, bsm_csr** out, hipStream_t s);
+int analyse_dispatch(const int64_t* rp, const int32_t* col, uint64_t rows, uint64_t cols,
+                     uint64_t* d_out3, hipStream_t s);
+int gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols, int kind,
+                uint32_t a, uint32_t b, int64_t* rp, void* ws, uint64_t ws_bytes, hipStream_t s);
+int gen_entries(int dtype, uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols,
+                int value_kind, const int64_t* rp, int32_t* col, void* vals, hipStream_t s);
+int gen_dense(int dtype, uint64_t seed, uint64_t row0, uint64_t n, uint64_t k, int value_kind,
+              void* x, hipStream_t s);
+int solve_dispatch_cholesky(const bsm_csr* a, bsm_csr** out, hipStream_t s);
+int solve_dispatch_trsv(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, const void* b_dev,
+                        void* x_dev, hipStream_t s);
+int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev,
+                        hipStream_t s);
+}  // namespace bsm

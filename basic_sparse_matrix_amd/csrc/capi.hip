@@ -1,0 +1,458 @@
+// capi.hip -- extern "C" boundary of libbsm_hip.so (declared in include/bsm.h).
+//
+// Host-buffer entry points mirror the reference crate's hot-path methods
+// (src/sparse.rs, src/lib.rs); each is synchronous and owns no caller memory.
+#include <cstdarg>
+#include <mutex>
+#include <vector>
+
+#include "bsm_internal.hpp"
+
+namespace bsm {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+const char* last_error() { return g_err.c_str(); }
+
+namespace {
+std::mutex g_stream_mu;
+hipStream_t g_streams[64] = {};
+}  // namespace
+
+int current_device(int* dev) {
+    BSM_HIP_TRY(hipGetDevice(dev));
+    return BSM_OK;
+}
+
+int ctx_stream(hipStream_t* s) {
+    int dev = 0;
+    BSM_TRY(current_device(&dev));
+    BSM_REQUIRE(dev >= 0 && dev < 64, BSM_ERR_INVALID, "device ordinal %d out of range", dev);
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if (!g_streams[dev]) BSM_HIP_TRY(hipStreamCreateWithFlags(&g_streams[dev], hipStreamNonBlocking));
+    *s = g_streams[dev];
+    return BSM_OK;
+}
+
+int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz) {
+    const size_t es = dtype_size(dtype);
+    BSM_REQUIRE(es != 0, BSM_ERR_INVALID, "unknown dtype %d", dtype);
+    BSM_REQUIRE(cols <= 0x7fffffffull, BSM_ERR_UNSUPPORTED,
+                "cols = %llu: device CSR stores int32 column indices", (unsigned long long)cols);
+    auto* m = new bsm_csr();
+    m->dtype = dtype;
+    m->rows = rows;
+    m->cols = cols;
+    m->nnz = nnz;
+    int dev = 0;
+    int rc = current_device(&dev);
+    m->device = dev;
+    DBuf rp, col, val;
+    if (rc == BSM_OK) rc = rp.alloc((rows + 1) * sizeof(int64_t));
+    if (rc == BSM_OK) rc = col.alloc(nnz * sizeof(int32_t));
+    if (rc == BSM_OK) rc = val.alloc(nnz * es);
+    if (rc != BSM_OK) {
+        delete m;
+        return rc;
+    }
+    m->row_ptr = static_cast<int64_t*>(rp.release());
+    m->col = static_cast<int32_t*>(col.release());
+    m->vals = val.release();
+    *out = m;
+    return BSM_OK;
+}
+
+int csr_analyse(bsm_csr* m, hipStream_t s) {
+    if (m->analysed) return BSM_OK;
+    DBuf out;
+    BSM_TRY(out.alloc(3 * sizeof(uint64_t)));
+    BSM_TRY(analyse_dispatch(m->row_ptr, m->col, m->rows, m->cols, out.as<uint64_t>(), s));
+    uint64_t h[3] = {0, 0, 0};
+    BSM_HIP_TRY(hipMemcpyAsync(h, out.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    BSM_REQUIRE(h[2] == 0, BSM_ERR_PANIC, "column index out of bounds in %llu row(s)",
+                (unsigned long long)h[2]);
+    m->max_row_len = h[0];
+    m->rows_sorted = (h[1] == 0);
+    m->analysed = true;
+    return BSM_OK;
+}
+
+// Upload k host columns (each n values) into a device ROW-major n x k array.
+static int upload_columns(int dtype, uint64_t n, uint64_t k, const void* const* cols, DBuf& out,
+                          hipStream_t s) {
+    const size_t es = dtype_size(dtype);
+    BSM_TRY(out.alloc(n * k * es));
+    if (n == 0 || k == 0) return BSM_OK;
+    if (k == 1) {
+        BSM_REQUIRE(cols[0] != nullptr, BSM_ERR_INVALID, "null column pointer");
+        BSM_HIP_TRY(hipMemcpyAsync(out.p, cols[0], n * es, hipMemcpyHostToDevice, s));
+        return BSM_OK;
+    }
+    DBuf staging;
+    BSM_TRY(staging.alloc(n * k * es));
+    for (uint64_t j = 0; j < k; ++j) {
+        BSM_REQUIRE(cols[j] != nullptr, BSM_ERR_INVALID, "null column pointer %llu",
+                    (unsigned long long)j);
+        BSM_HIP_TRY(hipMemcpyAsync(static_cast<char*>(staging.p) + j * n * es, cols[j], n * es,
+                                   hipMemcpyHostToDevice, s));
+    }
+    BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, staging.p, out.p, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));  // staging dies here
+    return BSM_OK;
+}
+
+// Download a device ROW-major n x k array into k host columns.
+static int download_columns(int dtype, uint64_t n, uint64_t k, const void* dev, void* const* cols,
+                            hipStream_t s) {
+    const size_t es = dtype_size(dtype);
+    if (n == 0 || k == 0) return BSM_OK;
+    if (k == 1) {
+        BSM_HIP_TRY(hipMemcpyAsync(cols[0], dev, n * es, hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        return BSM_OK;
+    }
+    DBuf staging;
+    BSM_TRY(staging.alloc(n * k * es));
+    BSM_TRY(unpack_rowmajor_to_cols(dtype, n, k, dev, staging.p, s));
+    for (uint64_t j = 0; j < k; ++j)
+        BSM_HIP_TRY(hipMemcpyAsync(cols[j], static_cast<const char*>(staging.p) + j * n * es, n * es,
+                                   hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    return BSM_OK;
+}
+
+// mul_dense core on device operands: Y = A X, then compaction into a Csr.
+static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm_csr** out,
+                            hipStream_t s) {
+    const size_t es = dtype_size(a->dtype);
+    const uint64_t rows = a->rows;
+    DBuf y, row_nnz, ws;
+    BSM_TRY(y.alloc(rows * k * es));
+    BSM_TRY(row_nnz.alloc(rows * sizeof(int32_t)));
+    BSM_TRY(ws.alloc(scan_workspace_bytes(rows)));
+    bsm_csr* r = nullptr;
+    // out row_ptr is allocated first (nnz unknown until the scan completes)
+    DBuf out_rp;
+    BSM_TRY(out_rp.alloc((rows + 1) * sizeof(int64_t)));
+    if (k == 0) {
+        BSM_HIP_TRY(hipMemsetAsync(row_nnz.p, 0, rows * sizeof(int32_t), s));
+    } else {
+        BSM_TRY(spmm_dispatch(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
+                              y.p, row_nnz.as<int32_t>(), false, s));
+    }
+    BSM_TRY(exclusive_scan_i32_to_i64(row_nnz.as<int32_t>(), out_rp.as<int64_t>(), rows, ws.p,
+                                      ws.bytes, s));
+    int64_t out_nnz = 0;
+    BSM_HIP_TRY(hipMemcpyAsync(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t),
+                               hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    r = new bsm_csr();
+    r->dtype = a->dtype;
+    r->device = a->device;
+    r->rows = rows;
+    r->cols = k;
+    r->nnz = (uint64_t)out_nnz;
+    DBuf oc, ov;
+    int rc = oc.alloc((uint64_t)out_nnz * sizeof(int32_t));
+    if (rc == BSM_OK) rc = ov.alloc((uint64_t)out_nnz * es);
+    if (rc != BSM_OK) {
+        delete r;
+        return rc;
+    }
+    r->row_ptr = static_cast<int64_t*>(out_rp.release());
+    r->col = static_cast<int32_t*>(oc.release());
+    r->vals = ov.release();
+    r->analysed = true;
+    r->rows_sorted = true;
+    rc = compact_dispatch(a->dtype, rows, k, y.p, r->row_ptr, r->col, r->vals, s);
+    if (rc == BSM_OK) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
+            rc = BSM_ERR_HIP;
+        }
+    }
+    if (rc != BSM_OK) {
+        bsm_csr_free(r);
+        return rc;
+    }
+    *out = r;
+    return BSM_OK;
+}
+
+}  // namespace bsm
+
+using namespace bsm;
+
+extern "C" {
+
+int bsm_api_version(void) { return BSM_API_VERSION; }
+
+const char* bsm_last_error(void) { return bsm::last_error(); }
+
+int bsm_device_count(int* n) {
+    BSM_REQUIRE(n, BSM_ERR_INVALID, "null argument");
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) {
+        *n = 0;
+        set_error("hipGetDeviceCount: %s", hipGetErrorString(e));
+        return BSM_ERR_NO_DEVICE;
+    }
+    return BSM_OK;
+}
+
+int bsm_set_device(int ordinal) {
+    BSM_HIP_TRY(hipSetDevice(ordinal));
+    return BSM_OK;
+}
+
+int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz, const uint64_t* row_ptr,
+                   const uint64_t* col_idx, const void* vals, bsm_csr** out) {
+    BSM_REQUIRE(out && row_ptr && (nnz == 0 || (col_idx && vals)), BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(row_ptr[0] == 0 && row_ptr[rows] == nnz, BSM_ERR_INVALID,
+                "row_ptr must start at 0 and end at nnz");
+    for (uint64_t r = 0; r < rows; ++r)
+        BSM_REQUIRE(row_ptr[r] <= row_ptr[r + 1], BSM_ERR_PANIC, "row_ptr not monotone at row %llu",
+                    (unsigned long long)r);
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    bsm_csr* m = nullptr;
+    BSM_TRY(csr_alloc(&m, dtype, rows, cols, nnz));
+    std::vector<int64_t> rp64(rows + 1);
+    for (uint64_t r = 0; r <= rows; ++r) rp64[r] = (int64_t)row_ptr[r];
+    std::vector<int32_t> c32(nnz);
+    for (uint64_t e = 0; e < nnz; ++e) {
+        if (col_idx[e] >= cols) {
+            bsm_csr_free(m);
+            set_error("column index %llu >= cols %llu at entry %llu", (unsigned long long)col_idx[e],
+                      (unsigned long long)cols, (unsigned long long)e);
+            return BSM_ERR_PANIC;
+        }
+        c32[e] = (int32_t)col_idx[e];
+    }
+    int rc = BSM_OK;
+    auto cp = [&](void* d, const void* h, size_t b) {
+        if (rc == BSM_OK && b) {
+            hipError_t e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) {
+                set_error("hipMemcpyAsync: %s", hipGetErrorString(e));
+                rc = BSM_ERR_HIP;
+            }
+        }
+    };
+    cp(m->row_ptr, rp64.data(), (rows + 1) * sizeof(int64_t));
+    cp(m->col, c32.data(), nnz * sizeof(int32_t));
+    cp(m->vals, vals, nnz * dtype_size(dtype));
+    if (rc == BSM_OK) rc = csr_analyse(m, s);  // syncs: host vectors may die after this
+    if (rc != BSM_OK) {
+        bsm_csr_free(m);
+        return rc;
+    }
+    *out = m;
+    return BSM_OK;
+}
+
+int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz, int* dtype) {
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    if (rows) *rows = m->rows;
+    if (cols) *cols = m->cols;
+    if (nnz) *nnz = m->nnz;
+    if (dtype) *dtype = m->dtype;
+    return BSM_OK;
+}
+
+int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, void* vals) {
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    std::vector<int64_t> rp64(m->rows + 1);
+    std::vector<int32_t> c32(m->nnz);
+    BSM_HIP_TRY(hipMemcpyAsync(rp64.data(), m->row_ptr, (m->rows + 1) * sizeof(int64_t),
+                               hipMemcpyDeviceToHost, s));
+    if (m->nnz) {
+        BSM_HIP_TRY(hipMemcpyAsync(c32.data(), m->col, m->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (vals)
+            BSM_HIP_TRY(hipMemcpyAsync(vals, m->vals, m->nnz * dtype_size(m->dtype),
+                                       hipMemcpyDeviceToHost, s));
+    }
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    if (row_ptr)
+        for (uint64_t r = 0; r <= m->rows; ++r) row_ptr[r] = (uint64_t)rp64[r];
+    if (col_idx)
+        for (uint64_t e = 0; e < m->nnz; ++e) col_idx[e] = (uint64_t)c32[e];
+    return BSM_OK;
+}
+
+void bsm_csr_free(bsm_csr* m) {
+    if (!m) return;
+    if (m->row_ptr) (void)hipFree(m->row_ptr);
+    if (m->col) (void)hipFree(m->col);
+    if (m->vals) (void)hipFree(m->vals);
+    delete m;
+}
+
+int bsm_csr_mul_dense(const bsm_csr* a, uint64_t k, uint64_t x_rows, const void* const* x_cols,
+                      bsm_csr** out) {
+    BSM_REQUIRE(a && out && (k == 0 || x_cols), BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(a->cols == x_rows, BSM_ERR_DIMENSIONS, "IncorrectDimensions: cols %llu != rhs rows %llu",
+                (unsigned long long)a->cols, (unsigned long long)x_rows);
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf x;
+    BSM_TRY(upload_columns(a->dtype, x_rows, k, x_cols, x, s));
+    return mul_dense_device(a, k, x.p, out, s);
+}
+
+int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void* out,
+                       uint64_t out_len) {
+    BSM_REQUIRE(a, BSM_ERR_INVALID, "null handle");
+    BSM_REQUIRE(a->cols == rhs_len && a->rows == out_len, BSM_ERR_DIMENSIONS, "IncorrectDimensions");
+    BSM_REQUIRE((rhs || rhs_len == 0) && (out || out_len == 0), BSM_ERR_INVALID, "null argument");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    const size_t es = dtype_size(a->dtype);
+    // The reference sums in ascending source-column order (it walks the
+    // transpose, sparse.rs:474-479). For row-sorted matrices that is the
+    // storage order; otherwise sort each row stably first: (A^T)^T.
+    const bsm_csr* src = a;
+    bsm_csr* sorted = nullptr;
+    if (!a->rows_sorted) {
+        bsm_csr* t = nullptr;
+        BSM_TRY(transpose_dispatch(a, &t, s));
+        int rc = transpose_dispatch(t, &sorted, s);
+        bsm_csr_free(t);
+        if (rc != BSM_OK) return rc;
+        src = sorted;
+    }
+    DBuf x, y;
+    int rc = x.alloc(rhs_len * es);
+    if (rc == BSM_OK) rc = y.alloc(out_len * es);
+    if (rc == BSM_OK && rhs_len) {
+        hipError_t e = hipMemcpyAsync(x.p, rhs, rhs_len * es, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { set_error("H2D: %s", hipGetErrorString(e)); rc = BSM_ERR_HIP; }
+    }
+    if (rc == BSM_OK)
+        rc = spmm_dispatch(src->dtype, src->rows, src->cols, src->nnz, src->row_ptr, src->col,
+                           src->vals, 1, x.p, y.p, nullptr, true, s);
+    if (rc == BSM_OK && out_len) {
+        hipError_t e = hipMemcpyAsync(out, y.p, out_len * es, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) { set_error("D2H: %s", hipGetErrorString(e)); rc = BSM_ERR_HIP; }
+    }
+    if (rc == BSM_OK) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { set_error("sync: %s", hipGetErrorString(e)); rc = BSM_ERR_HIP; }
+    }
+    bsm_csr_free(sorted);
+    return rc;
+}
+
+int bsm_csr_transpose(const bsm_csr* a, bsm_csr** out) {
+    BSM_REQUIRE(a && out, BSM_ERR_INVALID, "null argument");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    return transpose_dispatch(a, out, s);
+}
+
+int bsm_csr_cholesky(const bsm_csr* a, bsm_csr** out) {
+    BSM_REQUIRE(a && out, BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(a->rows == a->cols, BSM_ERR_NON_SQUARE, "NonSquareMatrix");
+    BSM_REQUIRE(a->dtype == BSM_F32 || a->dtype == BSM_F64, BSM_ERR_INVALID,
+                "cholesky_decomp is defined for f32 (reference) and f64 only");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    return solve_dispatch_cholesky(a, out, s);
+}
+
+static int trsv_host(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, const void* const* b_cols,
+                     void* const* x_cols) {
+    BSM_REQUIRE(m && (k == 0 || (b_cols && x_cols)), BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(m->dtype == BSM_F32 || m->dtype == BSM_F64, BSM_ERR_INVALID, "f32/f64 only");
+    BSM_REQUIRE(m->rows >= n, BSM_ERR_PANIC, "matrix has fewer rows than the RHS (index out of bounds)");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf b, x;
+    BSM_TRY(upload_columns(m->dtype, n, k, b_cols, b, s));
+    BSM_TRY(x.alloc(n * k * dtype_size(m->dtype)));
+    BSM_TRY(solve_dispatch_trsv(m, lower, k, n, b.p, x.p, s));
+    return download_columns(m->dtype, n, k, x.p, x_cols, s);
+}
+
+int bsm_forward_substitution(const bsm_csr* l, uint64_t k, uint64_t n, const void* const* b_cols,
+                             void* const* y_cols) {
+    return trsv_host(l, true, k, n, b_cols, y_cols);
+}
+
+int bsm_backward_substitution(const bsm_csr* u, uint64_t k, uint64_t n, const void* const* y_cols,
+                              void* const* x_cols) {
+    return trsv_host(u, false, k, n, y_cols, x_cols);
+}
+
+int bsm_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols, void* const* x_cols) {
+    BSM_REQUIRE(a && (k == 0 || (b_cols && x_cols)), BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(a->rows == a->cols, BSM_ERR_PANIC,
+                "solve: cholesky_decomp().unwrap() on a non-square matrix panics (lib.rs:20)");
+    BSM_REQUIRE(a->dtype == BSM_F32 || a->dtype == BSM_F64, BSM_ERR_INVALID, "f32/f64 only");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf b, x;
+    BSM_TRY(upload_columns(a->dtype, n, k, b_cols, b, s));
+    BSM_TRY(x.alloc(n * k * dtype_size(a->dtype)));
+    BSM_TRY(solve_dispatch_full(a, k, n, b.p, x.p, s));
+    return download_columns(a->dtype, n, k, x.p, x_cols, s);
+}
+
+// ---- device-level entry points --------------------------------------------
+uint64_t bsm_dev_scan_workspace_bytes(uint64_t n) {
+    return ((n * sizeof(int32_t) + 255) / 256) * 256 + scan_workspace_bytes(n);
+}
+
+int bsm_dev_gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols, int rowlen_kind,
+                        uint32_t a, uint32_t b, int64_t* row_ptr, void* workspace,
+                        uint64_t workspace_bytes, void* stream) {
+    BSM_REQUIRE(row_ptr, BSM_ERR_INVALID, "null argument");
+    return gen_row_ptr(seed, row0, rows, n_cols, rowlen_kind, a, b, row_ptr, workspace, workspace_bytes,
+                       static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_gen_entries(int dtype, uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols,
+                        int value_kind, const int64_t* row_ptr, int32_t* col, void* vals, void* stream) {
+    BSM_REQUIRE(row_ptr && col && vals, BSM_ERR_INVALID, "null argument");
+    return gen_entries(dtype, seed, row0, rows, n_cols, value_kind, row_ptr, col, vals,
+                       static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_gen_dense(int dtype, uint64_t seed, uint64_t row0, uint64_t n, uint64_t k, int value_kind,
+                      void* x, void* stream) {
+    BSM_REQUIRE(x || n * k == 0, BSM_ERR_INVALID, "null argument");
+    return gen_dense(dtype, seed, row0, n, k, value_kind, x, static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_spmm(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* row_ptr,
+                 const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
+                 int32_t* row_nnz, void* stream) {
+    BSM_REQUIRE(row_ptr && (nnz == 0 || (col && vals)) && (k == 0 || (x && y)), BSM_ERR_INVALID,
+                "null argument");
+    if (k == 0) return BSM_OK;
+    return spmm_dispatch(dtype, rows, n_cols, nnz, row_ptr, col, vals, k, x, y, row_nnz, false,
+                         static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y, const int32_t* row_nnz,
+                    int64_t* out_row_ptr, int32_t* out_col, void* out_vals, void* workspace,
+                    uint64_t workspace_bytes, void* stream) {
+    BSM_REQUIRE(row_nnz && out_row_ptr, BSM_ERR_INVALID, "null argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    BSM_TRY(exclusive_scan_i32_to_i64(row_nnz, out_row_ptr, rows, workspace, workspace_bytes, s));
+    return compact_dispatch(dtype, rows, k, y, out_row_ptr, out_col, out_vals, s);
+}
+
+}  // extern "C"

@@ -1,0 +1,598 @@
+// kernels_spmm.hip -- gfx950 kernels of Csr::mul_dense / mul_vector
+// (reference: src/sparse.rs:426-482) and their compaction into the
+// reference's output Csr, plus the device-wide scan they share.
+//
+// Summation order. The reference sums each output element sequentially in
+// the row's storage order starting from T::default() (sparse.rs:434-440) and
+// never fuses multiply-add. Every kernel here keeps exactly that order per
+// output element (lanes own output columns; products of one column are
+// combined in entry order), so f32/f64 results are bit-identical to the
+// reference, not merely within tolerance. See DESIGN.md "SpMM kernels".
+#include "bsm_internal.hpp"
+#include "bsm_synth.h"
+
+namespace bsm {
+namespace {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) {
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// first r in [0, n) with rp[r] >= v, else n
+__device__ __forceinline__ int64_t lower_bound_rp(const int64_t* rp, int64_t n, int64_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (rp[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------
+// Exclusive scan int32 -> int64 (n+1 outputs; out[n] = total).
+// Three launches: per-tile sums, scan of tile sums (one workgroup), apply.
+// ---------------------------------------------------------------------------
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* smem, int64_t* total) {
+    // smem: SCAN_BLOCK entries. Hillis-Steele over 256 threads.
+    const int t = threadIdx.x;
+    smem[t] = v;
+    __syncthreads();
+    for (int off = 1; off < SCAN_BLOCK; off <<= 1) {
+        int64_t add = (t >= off) ? smem[t - off] : 0;
+        __syncthreads();
+        smem[t] += add;
+        __syncthreads();
+    }
+    int64_t incl = smem[t];
+    *total = smem[SCAN_BLOCK - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_tile_sums(const int32_t* in, uint64_t n,
+                                                             int64_t* tile_sums) {
+    __shared__ int64_t red[SCAN_BLOCK];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    int64_t acc = 0;
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        uint64_t idx = base + (uint64_t)i * SCAN_BLOCK + threadIdx.x;
+        if (idx < n) acc += in[idx];
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = SCAN_BLOCK / 2; off > 0; off >>= 1) {
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_tile_prefix(int64_t* tile_sums, uint64_t n_tiles) {
+    __shared__ int64_t smem[SCAN_BLOCK];
+    int64_t carry = 0;
+    for (uint64_t base = 0; base < n_tiles; base += SCAN_BLOCK) {
+        uint64_t idx = base + threadIdx.x;
+        int64_t v = idx < n_tiles ? tile_sums[idx] : 0;
+        int64_t total;
+        int64_t ex = block_exclusive_scan(v, smem, &total);
+        if (idx < n_tiles) tile_sums[idx] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) tile_sums[n_tiles] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_apply(const int32_t* in, uint64_t n,
+                                                         const int64_t* tile_prefix, int64_t* out) {
+    __shared__ int64_t smem[SCAN_BLOCK];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    // each thread owns SCAN_ITEMS consecutive elements
+    int32_t v[SCAN_ITEMS];
+    int64_t local = 0;
+    const uint64_t my0 = base + (uint64_t)threadIdx.x * SCAN_ITEMS;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        uint64_t idx = my0 + i;
+        v[i] = idx < n ? in[idx] : 0;
+        local += v[i];
+    }
+    int64_t total;
+    int64_t ex = block_exclusive_scan(local, smem, &total) + tile_prefix[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        uint64_t idx = my0 + i;
+        if (idx < n) out[idx] = ex;
+        ex += v[i];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = tile_prefix[gridDim.x];
+}
+
+__global__ void write_zero_i64(int64_t* p) { *p = 0; }
+
+// ---------------------------------------------------------------------------
+// SpMM, lanes own output columns ("row-wave"): one wavefront per CSR row.
+// KL = lanes per entry group (power of two >= min(k,64)); S = 64/KL entries
+// are gathered per wave instruction, U groups are kept in flight. Lane
+// (s, c) multiplies entry e0+u*S+s by X[col][cb+c]; the S products of a
+// column are then added to that column's accumulator in entry order via
+// cross-lane reads, so every lane of column c holds the same, in-order sum.
+// For k = 32 f64 one wave instruction gathers two 256-B X rows.
+// ---------------------------------------------------------------------------
+template <typename T, int KL, int U>
+__global__ __launch_bounds__(256) void spmm_rowwave(int64_t rows, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col,
+                                                    const T* __restrict__ val, int k,
+                                                    const T* __restrict__ X, T* __restrict__ Y,
+                                                    int32_t* __restrict__ row_nnz) {
+    using A = Arith<T>;
+    constexpr int S = WAVE / KL;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+    if (row >= rows) return;  // wave-uniform
+    const int s = lane / KL;
+    const int c = lane % KL;
+    const int64_t start = rp[row], end = rp[row + 1];
+    int nz_count = 0;
+    for (int cb = 0; cb < k; cb += KL) {
+        const int jc = cb + c;
+        const bool cval = jc < k;
+        T acc = A::zero();
+        for (int64_t e0 = start; e0 < end; e0 += (int64_t)S * U) {
+            T p[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = e0 + (int64_t)u * S + s;
+                T pr = A::zero();
+                if (e < end && cval) {
+                    const int64_t cc = col[e];
+                    pr = A::mul(val[e], X[cc * k + jc]);
+                }
+                p[u] = pr;
+            }
+            // number of real entries in this step (wave-uniform); padding
+            // products are +0 and only ever trail the real ones, and the
+            // accumulator is never -0, so they cannot change the sum.
+            const int64_t left = end - e0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (S == 1) {
+                    acc = A::add(acc, p[u]);
+                } else {
+                    int nv = (int)min<int64_t>(S, left - (int64_t)u * S);
+                    for (int t = 0; t < nv; ++t) acc = A::add(acc, __shfl(p[u], t * KL + c, WAVE));
+                }
+            }
+        }
+        if (s == 0 && cval) Y[row * (int64_t)k + jc] = acc;
+        const uint64_t m = __ballot(s == 0 && cval && A::nz(acc));
+        nz_count += __popcll(m);
+    }
+    if (lane == 0 && row_nnz) row_nnz[row] = nz_count;
+}
+
+// ---------------------------------------------------------------------------
+// SpMV (k = 1), CSR-stream with in-order row sums. Workgroup b owns the rows
+// whose first entry lies in [b*CHUNK, (b+1)*CHUNK); their products are
+// computed with coalesced col/val loads into LDS, then one thread per row
+// adds its row's products in storage order (bit-exact). A workgroup whose
+// entry range exceeds LDS (it holds a row longer than CHUNK) falls back to
+// thread-per-row sums for short rows and a workgroup-wide pass per long row.
+// init = +0 for mul_dense (T::default()), -0 for mul_vector (float Sum).
+// ---------------------------------------------------------------------------
+constexpr int SPMV_CHUNK = 1024;
+constexpr int SPMV_CAP = 2048;
+
+template <typename T>
+__global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
+                                                   const int64_t* __restrict__ rp,
+                                                   const int32_t* __restrict__ col,
+                                                   const T* __restrict__ val,
+                                                   const T* __restrict__ x, T* __restrict__ y,
+                                                   int32_t* __restrict__ row_nnz, bool neg_init) {
+    using A = Arith<T>;
+    __shared__ T prod[SPMV_CAP];
+    __shared__ int64_t s_r[2];
+    const int64_t lo = (int64_t)blockIdx.x * SPMV_CHUNK;
+    const int64_t hi = lo + SPMV_CHUNK;
+    if (threadIdx.x == 0) {
+        s_r[0] = lower_bound_rp(rp, rows, lo);
+        s_r[1] = hi > nnz ? rows : lower_bound_rp(rp, rows, hi);
+    }
+    __syncthreads();
+    const int64_t r0 = s_r[0], r1 = s_r[1];
+    if (r0 >= r1) return;
+    const T init = neg_init ? A::neg_zero() : A::zero();
+    const int64_t e0 = rp[r0], e1 = rp[r1];
+    if (e1 - e0 <= SPMV_CAP) {
+        for (int64_t i = threadIdx.x; i < e1 - e0; i += blockDim.x) {
+            const int64_t e = e0 + i;
+            prod[i] = A::mul(val[e], x[col[e]]);
+        }
+        __syncthreads();
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+            const int64_t a = rp[r] - e0, b = rp[r + 1] - e0;
+            T acc = init;
+            for (int64_t i = a; i < b; ++i) acc = A::add(acc, prod[i]);
+            y[r] = acc;
+            if (row_nnz) row_nnz[r] = A::nz(acc) ? 1 : 0;
+        }
+        return;
+    }
+    // fallback: block contains a row longer than SPMV_CHUNK
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+        const int64_t a = rp[r], b = rp[r + 1];
+        if (b - a > SPMV_CHUNK) continue;
+        T acc = init;
+        for (int64_t e = a; e < b; ++e) acc = A::add(acc, A::mul(val[e], x[col[e]]));
+        y[r] = acc;
+        if (row_nnz) row_nnz[r] = A::nz(acc) ? 1 : 0;
+    }
+    for (int64_t r = r0; r < r1; ++r) {  // uniform loop over long rows
+        const int64_t a = rp[r], b = rp[r + 1];
+        if (b - a <= SPMV_CHUNK) continue;
+        T acc = init;
+        for (int64_t cs = a; cs < b; cs += SPMV_CAP) {
+            const int64_t n = min<int64_t>(SPMV_CAP, b - cs);
+            __syncthreads();
+            for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const int64_t e = cs + i;
+                prod[i] = A::mul(val[e], x[col[e]]);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (int64_t i = 0; i < n; ++i) acc = A::add(acc, prod[i]);
+        }
+        if (threadIdx.x == 0) {
+            y[r] = acc;
+            if (row_nnz) row_nnz[r] = A::nz(acc) ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Compaction of dense Y (rows x k, row-major) into the output Csr: entry
+// (r, j) is kept iff Y[r][j] != 0 (insert's zero skip, sparse.rs:229), in
+// ascending j, at out_rp[r] + (kept entries of row r before j).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void compact_wave(int64_t rows, int k, const T* __restrict__ Y,
+                                                    const int64_t* __restrict__ out_rp,
+                                                    int32_t* __restrict__ out_col,
+                                                    T* __restrict__ out_val) {
+    using A = Arith<T>;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+    if (row >= rows) return;
+    int64_t pos = out_rp[row];
+    for (int cb = 0; cb < k; cb += WAVE) {
+        const int j = cb + lane;
+        T v = j < k ? Y[row * (int64_t)k + j] : A::zero();
+        const bool keep = j < k && A::nz(v);
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const int64_t p = pos + __popcll(m & lanemask_lt(lane));
+            out_col[p] = j;
+            out_val[p] = v;
+        }
+        pos += __popcll(m);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void compact_k1(int64_t rows, const T* __restrict__ y,
+                                                  const int64_t* __restrict__ out_rp,
+                                                  int32_t* __restrict__ out_col,
+                                                  T* __restrict__ out_val) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int64_t p = out_rp[r];
+    if (out_rp[r + 1] != p) {
+        out_col[p] = 0;
+        out_val[p] = y[r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Dense operand layout conversion: host Dense is column-major (one Vec per
+// column); the kernels want row-major so that an entry gathers k
+// contiguous values. 64x64 LDS tiles.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_tiles(const T* __restrict__ in, T* __restrict__ out,
+                                                       int64_t in_rows, int64_t in_cols,
+                                                       int64_t tiles_c) {
+    // in: in_rows x in_cols row-major; out: in_cols x in_rows row-major.
+    // 1-D grid over 64x64 tiles (one of the two extents is large).
+    __shared__ T tile[64][65];
+    const int64_t t = blockIdx.x;
+    const int64_t br = (t / tiles_c) * 64, bc = (t % tiles_c) * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = br + i, c = bc + tx;
+        if (r < in_rows && c < in_cols) tile[i][tx] = in[r * in_cols + c];
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = bc + i, c = br + tx;  // out row = in col
+        if (r < in_cols && c < in_rows) out[r * in_rows + c] = tile[tx][i];
+    }
+}
+
+template <typename T>
+int launch_transpose_tiles(const T* in, T* out, uint64_t in_rows, uint64_t in_cols, hipStream_t s) {
+    const uint64_t tr = (in_rows + 63) / 64, tc = (in_cols + 63) / 64;
+    BSM_REQUIRE(tr * tc < (1ull << 31), BSM_ERR_UNSUPPORTED, "dense operand too large");
+    transpose_tiles<T><<<(unsigned)(tr * tc), 256, 0, s>>>(in, out, (int64_t)in_rows,
+                                                           (int64_t)in_cols, (int64_t)tc);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Analysis: max row length and whether every row's columns are
+// non-decreasing (then storage order == ascending-column order, which is
+// what mul_vector's transpose-based sum uses, sparse.rs:474-479).
+// out3 = {max_row_len, unsorted_rows, bad_col (col >= cols or < 0)}.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void analyse_rows(const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col, int64_t rows,
+                                                    int64_t cols, unsigned long long* out3) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+    if (row >= rows) return;
+    const int64_t a = rp[row], b = rp[row + 1];
+    bool unsorted = false, bad = false;
+    for (int64_t e = a + lane; e < b; e += WAVE) {
+        const int32_t c = col[e];
+        if (c < 0 || c >= cols) bad = true;
+        if (e > a && col[e - 1] > c) unsorted = true;
+    }
+    const bool any_uns = __any(unsorted), any_bad = __any(bad);
+    if (lane == 0) {
+        atomicMax(&out3[0], (unsigned long long)(b - a));
+        if (any_uns) atomicAdd(&out3[1], 1ull);
+        if (any_bad) atomicAdd(&out3[2], 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic generator (bsm_synth.h). Row lengths, then one workgroup per row
+// draws its columns, bitonic-sorts them in LDS and applies the bump passes
+// (forward prefix-max, backward suffix-min) sequentially in one lane, which
+// matches the host restatement integer for integer.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gen_rowlen(uint64_t seed, uint64_t row0, int64_t rows,
+                                                  uint32_t n_cols, int kind, uint32_t a, uint32_t b,
+                                                  int32_t* len) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    uint32_t l = bsm_rowlen(seed, row0 + r, kind, a, b);
+    if (l > n_cols) l = n_cols;
+    len[r] = (int32_t)l;
+}
+
+constexpr int GEN_MAX = 4096;
+
+template <typename T>
+__global__ __launch_bounds__(256) void gen_row_entries(uint64_t seed, uint64_t row0, int64_t rows,
+                                                       uint32_t n_cols, int value_kind,
+                                                       const int64_t* __restrict__ rp,
+                                                       int32_t* __restrict__ col,
+                                                       T* __restrict__ vals) {
+    __shared__ uint32_t key[GEN_MAX];
+    const int64_t r = blockIdx.x;
+    if (r >= rows) return;
+    const int64_t s = rp[r];
+    const int len = (int)(rp[r + 1] - s);
+    int P = 1;
+    while (P < len) P <<= 1;
+    const uint64_t grow = row0 + r;
+    for (int j = threadIdx.x; j < P; j += blockDim.x)
+        key[j] = j < len ? bsm_col_draw(seed, grow, j, n_cols) : 0xffffffffu;
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < P / 2; i += blockDim.x) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const uint32_t x = key[lo], y = key[hi];
+                if ((x > y) == asc) { key[lo] = y; key[hi] = x; }
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0 && len > 0) {
+        for (int j = 1; j < len; ++j)
+            if (key[j] <= key[j - 1]) key[j] = key[j - 1] + 1;
+        if (key[len - 1] > n_cols - 1) key[len - 1] = n_cols - 1;
+        for (int j = len - 2; j >= 0; --j)
+            if (key[j] >= key[j + 1]) key[j] = key[j + 1] - 1;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < len; j += blockDim.x) {
+        col[s + j] = (int32_t)key[j];
+        vals[s + j] = (T)bsm_a_value(seed, grow, j, value_kind);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gen_dense_rowmajor(uint64_t seed, uint64_t row0, int64_t n,
+                                                          int64_t k, int value_kind, T* __restrict__ x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * k) return;
+    const int64_t r = i / k, j = i % k;
+    x[i] = (T)bsm_x_value(seed, row0 + r, j, value_kind);
+}
+
+inline unsigned grid1d(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// ===========================================================================
+// host-side launchers
+// ===========================================================================
+uint64_t scan_workspace_bytes(uint64_t n) {
+    const uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    return (tiles + 1) * sizeof(int64_t) + 256;
+}
+
+int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void* ws,
+                              uint64_t ws_bytes, hipStream_t s) {
+    if (n == 0) {
+        write_zero_i64<<<1, 1, 0, s>>>(out);
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    }
+    const uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    BSM_REQUIRE(ws && ws_bytes >= scan_workspace_bytes(n), BSM_ERR_INVALID,
+                "scan workspace too small (%llu < %llu)", (unsigned long long)ws_bytes,
+                (unsigned long long)scan_workspace_bytes(n));
+    BSM_REQUIRE(tiles < (1ull << 31), BSM_ERR_UNSUPPORTED, "scan too large");
+    int64_t* tile_sums = static_cast<int64_t*>(ws);
+    scan_tile_sums<<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, tile_sums);
+    scan_tile_prefix<<<1, SCAN_BLOCK, 0, s>>>(tile_sums, tiles);
+    scan_apply<<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, tile_sums, out);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
+namespace {
+template <typename T>
+int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                const T* vals, uint64_t k, const T* x, T* y, int32_t* row_nnz, bool neg_init,
+                hipStream_t s) {
+    if (rows == 0) return BSM_OK;
+    if (k == 1) {
+        const uint64_t blocks = nnz / SPMV_CHUNK + 1;
+        BSM_REQUIRE(blocks < (1ull << 31), BSM_ERR_UNSUPPORTED, "nnz too large for one launch");
+        spmv_stream<T><<<(unsigned)blocks, 256, 0, s>>>((int64_t)rows, (int64_t)nnz, rp, col, vals,
+                                                        x, y, row_nnz, neg_init);
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    }
+    BSM_REQUIRE(!neg_init, BSM_ERR_INVALID, "-0 init only for k = 1");
+    BSM_REQUIRE(k < (1ull << 30), BSM_ERR_UNSUPPORTED, "k too large");
+    const uint64_t blocks = (rows + 3) / 4;
+    BSM_REQUIRE(blocks < (1ull << 32), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
+    const int ki = (int)k;
+    const dim3 g((unsigned)blocks), b(256);
+    if (k <= 2) spmm_rowwave<T, 2, 4><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    else if (k <= 4) spmm_rowwave<T, 4, 4><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    else if (k <= 8) spmm_rowwave<T, 8, 4><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    else if (k <= 16) spmm_rowwave<T, 16, 8><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    else if (k <= 32) spmm_rowwave<T, 32, 8><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    else spmm_rowwave<T, 64, 8><<<g, b, 0, s>>>(rows, rp, col, vals, ki, x, y, row_nnz);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+}  // namespace
+
+int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
+                  const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
+                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s) {
+    (void)n_cols;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        return launch_spmm<T>(rows, nnz, rp, col, static_cast<const T*>(vals), k,
+                              static_cast<const T*>(x), static_cast<T*>(y), row_nnz,
+                              neg_zero_init, s);
+    });
+}
+
+int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
+                     int32_t* out_col, void* out_vals, hipStream_t s) {
+    if (rows == 0 || k == 0) return BSM_OK;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        if (k == 1) {
+            compact_k1<T><<<grid1d(rows, 256), 256, 0, s>>>((int64_t)rows, static_cast<const T*>(y),
+                                                           out_rp, out_col, static_cast<T*>(out_vals));
+        } else {
+            compact_wave<T><<<grid1d(rows, 4), 256, 0, s>>>((int64_t)rows, (int)k,
+                                                           static_cast<const T*>(y), out_rp, out_col,
+                                                           static_cast<T*>(out_vals));
+        }
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    });
+}
+
+int pack_cols_to_rowmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor, void* rowmajor,
+                          hipStream_t s) {
+    if (n == 0 || k == 0) return BSM_OK;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        // colmajor = k x n row-major; rowmajor = n x k
+        return launch_transpose_tiles<T>(static_cast<const T*>(colmajor), static_cast<T*>(rowmajor),
+                                         k, n, s);
+    });
+}
+
+int unpack_rowmajor_to_cols(int dtype, uint64_t n, uint64_t k, const void* rowmajor, void* colmajor,
+                            hipStream_t s) {
+    if (n == 0 || k == 0) return BSM_OK;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        return launch_transpose_tiles<T>(static_cast<const T*>(rowmajor), static_cast<T*>(colmajor),
+                                         n, k, s);
+    });
+}
+
+int analyse_dispatch(const int64_t* rp, const int32_t* col, uint64_t rows, uint64_t cols,
+                     uint64_t* d_out3, hipStream_t s) {
+    BSM_HIP_TRY(hipMemsetAsync(d_out3, 0, 3 * sizeof(uint64_t), s));
+    if (rows == 0) return BSM_OK;
+    analyse_rows<<<grid1d(rows, 4), 256, 0, s>>>(rp, col, (int64_t)rows, (int64_t)cols,
+                                                 reinterpret_cast<unsigned long long*>(d_out3));
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
+int gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols, int kind, uint32_t a,
+                uint32_t b, int64_t* rp, void* ws, uint64_t ws_bytes, hipStream_t s) {
+    BSM_REQUIRE(kind == BSM_ROWLEN_CONST || kind == BSM_ROWLEN_UNIFORM, BSM_ERR_UNSUPPORTED,
+                "device generator supports CONST/UNIFORM row lengths only");
+    BSM_REQUIRE(b <= GEN_MAX && a <= GEN_MAX, BSM_ERR_UNSUPPORTED, "row length > %d", GEN_MAX);
+    // workspace: [len int32 rows][scan ws]
+    const uint64_t len_bytes = ((rows * sizeof(int32_t)) + 255) / 256 * 256;
+    BSM_REQUIRE(ws && ws_bytes >= len_bytes + scan_workspace_bytes(rows), BSM_ERR_INVALID,
+                "generator workspace too small");
+    int32_t* len = static_cast<int32_t*>(ws);
+    if (rows) {
+        gen_rowlen<<<grid1d(rows, 256), 256, 0, s>>>(seed, row0, (int64_t)rows, n_cols, kind, a, b, len);
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    return exclusive_scan_i32_to_i64(len, rp, rows, static_cast<char*>(ws) + len_bytes,
+                                     ws_bytes - len_bytes, s);
+}
+
+int gen_entries(int dtype, uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols,
+                int value_kind, const int64_t* rp, int32_t* col, void* vals, hipStream_t s) {
+    if (rows == 0) return BSM_OK;
+    BSM_REQUIRE(rows < (1ull << 31), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
+    BSM_REQUIRE(value_kind == BSM_VAL_SMALLINT || dtype == BSM_F64 || dtype == BSM_F32,
+                BSM_ERR_INVALID, "integer dtypes need value_kind SMALLINT (UNIFORM would give zeros)");
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        gen_row_entries<T><<<(unsigned)rows, 256, 0, s>>>(seed, row0, (int64_t)rows, n_cols,
+                                                          value_kind, rp, col, static_cast<T*>(vals));
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    });
+}
+
+int gen_dense(int dtype, uint64_t seed, uint64_t row0, uint64_t n, uint64_t k, int value_kind,
+              void* x, hipStream_t s) {
+    if (n == 0 || k == 0) return BSM_OK;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        const uint64_t total = n * k;
+        BSM_REQUIRE(total / 256 < (1ull << 31), BSM_ERR_UNSUPPORTED, "dense too large");
+        gen_dense_rowmajor<T><<<grid1d(total, 256), 256, 0, s>>>(seed, row0, (int64_t)n, (int64_t)k,
+                                                                value_kind, static_cast<T*>(x));
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    });
+}
+
+}  // namespace bsm

@@ -1,0 +1,111 @@
+"""Device-level (HBM-resident) entry points for benchmarks and multi-GPU runs.
+
+Thin wrappers over the ``bsm_dev_*`` functions of include/bsm.h. PyTorch is
+used only as plumbing: it allocates HBM buffers (``torch.empty(...,
+device="cuda")``), supplies the HIP stream (``torch.cuda.current_stream()``)
+and, in bench.py, ``torch.distributed`` (RCCL). All compute is the HIP
+kernels of libbsm_hip.so.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+TORCH_DT = {
+    np.dtype(np.float64): torch.float64,
+    np.dtype(np.float32): torch.float32,
+    np.dtype(np.int32): torch.int32,
+    np.dtype(np.uint32): torch.uint32,
+    np.dtype(np.int64): torch.int64,
+    np.dtype(np.uint64): torch.uint64,
+}
+
+
+def _stream(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _p(t: torch.Tensor) -> int:
+    return t.data_ptr() if t.numel() else 0
+
+
+@dataclass
+class DeviceCsrBlock:
+    """A CSR row block resident in HBM: rows [row0, row0+rows) of a matrix
+    with n_cols columns. row_ptr is local (starts at 0)."""
+
+    row0: int
+    rows: int
+    n_cols: int
+    row_ptr: torch.Tensor  # int64 [rows+1]
+    col: torch.Tensor  # int32 [nnz]
+    vals: torch.Tensor  # T [nnz]
+    dtype: np.dtype
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+    @classmethod
+    def generate(cls, seed, row0, rows, n_cols, rowlen_kind=_lib.ROWLEN_CONST, a=10, b=10,
+                 value_kind=_lib.VAL_UNIFORM, dtype=np.float64, device="cuda") -> "DeviceCsrBlock":
+        """Synthetic CSR rows (bsm_synth.h recipe) generated on the device."""
+        lib = _lib.require_device()
+        dt = np.dtype(dtype)
+        rp = torch.empty(rows + 1, dtype=torch.int64, device=device)
+        wsb = lib.bsm_dev_scan_workspace_bytes(rows)
+        ws = torch.empty(max(16, wsb), dtype=torch.uint8, device=device)
+        s = _stream()
+        _lib.check(lib.bsm_dev_gen_row_ptr(seed, row0, rows, n_cols, rowlen_kind, a, b, _p(rp), _p(ws), wsb, s))
+        nnz = int(rp[rows].item()) if rows else 0
+        col = torch.empty(nnz, dtype=torch.int32, device=device)
+        vals = torch.empty(nnz, dtype=TORCH_DT[dt], device=device)
+        _lib.check(lib.bsm_dev_gen_entries(_lib.DTYPE_CODES[dt], seed, row0, rows, n_cols, value_kind, _p(rp),
+                                           _p(col), _p(vals), s))
+        return cls(row0, rows, n_cols, rp, col, vals, dt)
+
+    def spmm(self, x: torch.Tensor, y: torch.Tensor, row_nnz: torch.Tensor | None = None, stream=None) -> None:
+        """Y = A X (x: n_cols x k row-major, y: rows x k row-major), async."""
+        lib = _lib.load()
+        k = x.shape[1] if x.dim() == 2 else 1
+        _lib.check(lib.bsm_dev_spmm(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz, _p(self.row_ptr),
+                                    _p(self.col), _p(self.vals), k, _p(x), _p(y),
+                                    _p(row_nnz) if row_nnz is not None else 0, _stream(stream)))
+
+
+def gen_dense(seed, row0, n, k, value_kind=_lib.VAL_UNIFORM, dtype=np.float64, device="cuda") -> torch.Tensor:
+    """Row-major n x k dense operand X[r][j] = bsm_x_value(seed, row0+r, j)."""
+    lib = _lib.require_device()
+    dt = np.dtype(dtype)
+    x = torch.empty((n, k), dtype=TORCH_DT[dt], device=device)
+    _lib.check(lib.bsm_dev_gen_dense(_lib.DTYPE_CODES[dt], seed, row0, n, k, value_kind, _p(x), _stream()))
+    return x
+
+
+class Compactor:
+    """Dense Y -> output Csr (the zero-dropping insert of sparse.rs:229) with
+    preallocated worst-case buffers, so a timed step allocates nothing."""
+
+    def __init__(self, rows: int, k: int, dtype, device="cuda"):
+        lib = _lib.load()
+        self.rows, self.k, self.dtype = rows, k, np.dtype(dtype)
+        self.row_ptr = torch.empty(rows + 1, dtype=torch.int64, device=device)
+        self.col = torch.empty(max(1, rows * k), dtype=torch.int32, device=device)
+        self.vals = torch.empty(max(1, rows * k), dtype=TORCH_DT[self.dtype], device=device)
+        self.ws_bytes = lib.bsm_dev_scan_workspace_bytes(rows)
+        self.ws = torch.empty(max(16, self.ws_bytes), dtype=torch.uint8, device=device)
+
+    def __call__(self, y: torch.Tensor, row_nnz: torch.Tensor, stream=None) -> None:
+        lib = _lib.load()
+        _lib.check(lib.bsm_dev_compact(_lib.DTYPE_CODES[self.dtype], self.rows, self.k, _p(y), _p(row_nnz),
+                                       _p(self.row_ptr), _p(self.col), _p(self.vals), _p(self.ws), self.ws_bytes,
+                                       _stream(stream)))
+
+    def nnz(self) -> int:
+        return int(self.row_ptr[self.rows].item())

@@ -1,0 +1,56 @@
+"""Linear solver of the reference crate (src/lib.rs:11-65), on the GPU.
+
+``solve(a, b)`` = cholesky_decomp -> transpose -> forward_substitution ->
+backward_substitution, with the reference's exact operation order
+(DESIGN.md "Solver"). The reference is ``f32``-only; ``f64`` is accepted as
+this build's addition.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .dense import Dense
+from .sparse import Csr, _raise_for
+from .util import Panic
+
+_FLOATS = (np.dtype(np.float32), np.dtype(np.float64))
+
+
+def _check_types(m: Csr, d: Dense, what: str):
+    if m.dtype not in _FLOATS or d.dtype != m.dtype:
+        raise TypeError(f"{what}: needs Csr<f32>/Dense<f32> (or f64), got {m.dtype}/{d.dtype}")
+
+
+def _run(fn_name: str, m: Csr, rhs: Dense) -> Dense:
+    dims = rhs.get_dims()
+    n, k = dims.rows, dims.cols
+    if m.dims.rows < n:
+        raise Panic("index out of bounds: matrix has fewer rows than the right-hand side")
+    dev = m._device()
+    lib = _lib.require_device()
+    b_cols = [np.ascontiguousarray(rhs.get_col(j)) for j in range(k)]
+    out = Dense.new_default_with_dims(k, n, dtype=m.dtype)
+    _raise_for(getattr(lib, fn_name)(dev.handle, k, n, _lib.ptr_array(b_cols), _lib.ptr_array(out.data)))
+    return out
+
+
+def forward_substitution(l: Csr, b: Dense) -> Dense:
+    """lib.rs:28-46: solve L y = b (diagonal = LAST stored entry of each row)."""
+    _check_types(l, b, "forward_substitution")
+    return _run("bsm_forward_substitution", l, b)
+
+
+def backward_substitution(l_star: Csr, y: Dense) -> Dense:
+    """lib.rs:49-65: solve L* x = y (diagonal = FIRST stored entry of each row)."""
+    _check_types(l_star, y, "backward_substitution")
+    return _run("bsm_backward_substitution", l_star, y)
+
+
+def solve(a: Csr, b: Dense) -> Dense:
+    """lib.rs:11-24. Non-square ``a`` panics (``cholesky_decomp().unwrap()``)."""
+    _check_types(a, b, "solve")
+    if a.dims.rows != a.dims.cols:
+        raise Panic("called `Result::unwrap()` on an `Err` value: NonSquareMatrix")
+    return _run("bsm_solve", a, b)

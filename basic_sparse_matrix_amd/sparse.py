@@ -1,0 +1,423 @@
+"""Csr<T> -- host-side mirror of the reference's sparse core (src/sparse.rs).
+
+Construction and accessors are host logic with the reference's exact
+semantics (zero-skipping ``insert``, running-max row assignment in
+``insert_unchecked``, ``finalise`` padding, ``get_row_compact`` /
+``get_row_complete`` edge cases). The hot-path methods -- ``mul_dense``,
+``mul_dense_s``, ``mul_vector``, ``transpose`` and ``cholesky_decomp`` --
+check dimensions exactly where the reference does and then run on the GPU
+through the C-ABI (include/bsm.h). There is no CPU fallback.
+
+A finalised Csr is immutable (``insert`` returns Err(MatrixFinalised),
+sparse.rs:223-225), so its device copy is uploaded once and cached; the
+cache is not part of equality (the reference's derived PartialEq compares
+the seven fields of sparse.rs:68-78).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import numpy as np
+
+from . import _lib
+from .dense import Dense, _infer_dtype
+from .dense_static import DenseS
+from .util import GetDims, MatDim, MatErr, MatErrKind, Panic
+
+GPU_DTYPES = tuple(_lib.DTYPE_CODES.keys())
+
+
+@dataclass
+class CsrEntry:
+    """sparse.rs:80-91 (``v`` is the value, not a reference)."""
+
+    v: Any
+    col_index: int
+    row_index: int
+
+    @staticmethod
+    def of(t) -> "CsrEntry":
+        """``From<(T, usize, usize)>``: (v, row, col) (sparse.rs:87-91)."""
+        v, row, col = t
+        return CsrEntry(v=v, col_index=int(col), row_index=int(row))
+
+    def __eq__(self, other):
+        return (
+            isinstance(other, CsrEntry)
+            and self.v == other.v
+            and self.col_index == other.col_index
+            and self.row_index == other.row_index
+        )
+
+
+def _raise_for(code: int) -> None:
+    if code == _lib.BSM_OK:
+        return
+    msg = _lib.last_error()
+    if code == _lib.BSM_ERR_DIMENSIONS:
+        raise MatErr(MatErrKind.IncorrectDimensions)
+    if code == _lib.BSM_ERR_NON_SQUARE:
+        raise MatErr(MatErrKind.NonSquareMatrix)
+    if code == _lib.BSM_ERR_PANIC:
+        raise Panic(msg)
+    raise _lib.BsmError(code, msg)
+
+
+class Csr(GetDims):
+    __slots__ = ("dims", "dtype", "v", "col_index", "row_index", "is_finalised", "iter_v_index",
+                 "iter_row_index", "_dev")
+
+    # ------------------------------------------------------------------ ctor
+    def __init__(self, dims, dtype=np.int32, capacity: int = 0):
+        """``Csr::new_with_capacity`` (sparse.rs:121-132)."""
+        self.dims = MatDim.of(dims)
+        self.dtype = np.dtype(dtype)
+        self.v: Any = []
+        self.col_index: Any = []
+        self.row_index: Any = [0]
+        self.is_finalised = False
+        self.iter_v_index = 0
+        self.iter_row_index = 0
+        self._dev = None
+
+    @classmethod
+    def new(cls, dims, dtype=np.int32) -> "Csr":
+        """sparse.rs:117-119."""
+        return cls(dims, dtype)
+
+    @classmethod
+    def new_with_capacity(cls, dims, capacity: int, dtype=np.int32) -> "Csr":
+        return cls(dims, dtype, capacity)
+
+    @classmethod
+    def eye(cls, dims, value, dtype=None) -> "Csr":
+        """sparse.rs:134-152 (insert_unchecked: a zero value IS stored)."""
+        dims = MatDim.of(dims)
+        if dims.cols != dims.rows:
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        m = cls(dims, _infer_dtype([value], dtype))
+        for n in range(dims.cols):
+            m._insert_unchecked(value, n, n)
+        return m.finalise()
+
+    @classmethod
+    def create_diagonal(cls, contents, dtype=None) -> "Csr":
+        """sparse.rs:154-160."""
+        n = len(contents)
+        m = cls((n, n), _infer_dtype(list(contents) or [0], dtype))
+        for i, v in enumerate(contents):
+            m.insert(v, i, i)
+        return m.finalise()
+
+    @classmethod
+    def from_data(cls, data, dtype=None) -> "Csr":
+        """sparse.rs:193-203: ``data`` is a list of ROWS; zeros are skipped."""
+        rows = len(data)
+        cols = len(data[0])
+        m = cls((rows, cols), _infer_dtype([x for row in data for x in row] or [0], dtype))
+        arr = np.asarray(data, dtype=m.dtype) if rows else np.zeros((0, cols), m.dtype)
+        # vectorised equivalent of the insert loop: rows ascend, cols ascend
+        nzr, nzc = np.nonzero(arr != 0) if arr.dtype.kind != "f" else np.nonzero(~(arr == 0))
+        m.v = arr[nzr, nzc].copy()
+        m.col_index = nzc.astype(np.uint64)
+        counts = np.bincount(nzr, minlength=rows) if rows else np.zeros(0, dtype=np.int64)
+        # insert_unchecked registers a row only when its first entry arrives;
+        # rows after the last nonempty row are added by finalise, so the
+        # result is the standard row_ptr once finalised.
+        m.row_index = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+        m.is_finalised = True
+        return m
+
+    @classmethod
+    def from_csr_arrays(cls, dims, row_index, col_index, v, dtype=None) -> "Csr":
+        """Bulk constructor (this build's addition, not in the reference):
+        adopt an already finalised CSR (row_index of length rows+1)."""
+        m = cls(dims, v.dtype if dtype is None else dtype)
+        m.v = np.ascontiguousarray(v, dtype=m.dtype)
+        m.col_index = np.ascontiguousarray(col_index, dtype=np.uint64)
+        m.row_index = np.ascontiguousarray(row_index, dtype=np.uint64)
+        if m.row_index.shape != (m.dims.rows + 1,):
+            raise ValueError("row_index must have rows+1 entries")
+        m.is_finalised = True
+        return m
+
+    # ------------------------------------------------------------ building
+    def finalise(self) -> "Csr":
+        """sparse.rs:206-219: pad row_index to rows+1 with nnz."""
+        if not self.is_finalised:
+            self.is_finalised = True
+            ri = list(self.row_index)
+            if self.dims.rows < len(ri):
+                raise Panic("big eek")
+            nnz = len(self.v)
+            ri.extend([nnz] * (self.dims.rows - len(ri)))
+            ri.append(nnz)
+            self.row_index = np.asarray(ri, dtype=np.uint64)
+            self.col_index = np.asarray(self.col_index, dtype=np.uint64)
+            self.v = np.asarray(self.v, dtype=self.dtype)
+        return self
+
+    def insert(self, value, row: int, col: int) -> None:
+        """sparse.rs:222-233. Raises MatErr(MatrixFinalised) after finalise;
+        silently ignores values equal to T::default()."""
+        if self.is_finalised:
+            raise MatErr(MatErrKind.MatrixFinalised)
+        value = self.dtype.type(value)
+        if value != 0:
+            self._insert_unchecked(value, row, col)
+
+    def _insert_unchecked(self, value, row: int, col: int) -> None:
+        """sparse.rs:237-250: the row is recorded only when it exceeds the
+        running maximum; an entry for an earlier row is appended to the
+        current last row."""
+        self.v.append(self.dtype.type(value))
+        self.col_index.append(int(col))
+        ri = self.row_index
+        if row > len(ri) - 1:
+            if row > len(ri):
+                ri.append(len(self.v) - 1)
+                last = ri[-1]
+                ri.extend([last] * (row + 1 - len(ri)))
+            else:
+                ri.append(len(self.v) - 1)
+
+    insert_unchecked = _insert_unchecked
+
+    # ------------------------------------------------------------ accessors
+    def get_dims(self) -> MatDim:
+        return self.dims
+
+    def get_nnz(self) -> int:
+        """sparse.rs:162-164: last row_index entry."""
+        return int(self.row_index[-1]) if len(self.row_index) else 0
+
+    def get_density(self) -> float:
+        return np.float32(len(self.v)) / np.float32(self.dims.rows * self.dims.cols)
+
+    def _row_bounds(self, index: int):
+        ri = self.row_index
+        if index >= len(ri):
+            raise Panic(f"index out of bounds: the len is {len(ri)} but the index is {index}")
+        start = int(ri[index])
+        end = len(self.v) if index == len(ri) - 1 else int(ri[index + 1])
+        if start > end or end > len(self.v):
+            raise Panic("slice index starts after end")
+        return start, end
+
+    def get_row_compact(self, index: int) -> List[CsrEntry]:
+        """sparse.rs:252-265."""
+        s, e = self._row_bounds(index)
+        return [CsrEntry(v=self.v[i], col_index=int(self.col_index[i]), row_index=index) for i in range(s, e)]
+
+    def get_row_complete(self, index: int) -> Optional[list]:
+        """sparse.rs:267-294 (literal expansion, including its behaviour on
+        unsorted/duplicate columns)."""
+        ri = self.row_index
+        if len(ri) == 0 or index >= len(ri):
+            return None
+        start = int(ri[index])
+        end = len(self.v) if len(ri) == index + 1 else int(ri[index + 1])
+        zero = self.dtype.type(0)
+        out = []
+        prev = 0
+        for i in range(start, end):
+            c = int(self.col_index[i])
+            if c != 0:
+                out.extend([zero] * max(0, c - prev))
+            prev = c + 1
+            out.append(self.v[i])
+        out.extend([zero] * max(0, self.dims.cols - prev))
+        return out
+
+    def get_val_at(self, at):
+        """sparse.rs:170-180."""
+        at = MatDim.of(at)
+        s, e = int(self.row_index[at.rows]), int(self.row_index[at.rows + 1])
+        for i in range(s, e):
+            if int(self.col_index[i]) == at.cols:
+                return self.v[i]
+        return None
+
+    def reset_iter(self) -> None:
+        self.iter_row_index = 0
+        self.iter_v_index = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> CsrEntry:
+        """``Iterator for Csr`` (sparse.rs:93-114)."""
+        if self.iter_v_index == len(self.v):
+            raise StopIteration
+        while int(self.row_index[self.iter_row_index]) == self.iter_v_index:
+            self.iter_row_index += 1
+        e = CsrEntry(v=self.v[self.iter_v_index], col_index=int(self.col_index[self.iter_v_index]),
+                     row_index=self.iter_row_index - 1)
+        self.iter_v_index += 1
+        return e
+
+    # ------------------------------------------------------- device operand
+    def _csr_arrays(self):
+        """(row_ptr[rows+1], col_index, v) as the reference's row loop sees
+        them: an unfinalised matrix whose row_index covers every row is
+        usable (its last recorded row extends to nnz, sparse.rs:256-260);
+        a shorter one makes ``row_index[row]`` panic."""
+        rows = self.dims.rows
+        ri = np.asarray(self.row_index, dtype=np.uint64)
+        nnz = len(self.v)
+        if len(ri) >= rows + 1:
+            rp = ri[: rows + 1].copy()
+            if len(ri) == rows + 1 and not self.is_finalised:
+                rp[rows] = nnz
+        elif len(ri) == rows:
+            rp = np.concatenate([ri, np.asarray([nnz], dtype=np.uint64)])
+        else:
+            raise Panic(f"index out of bounds: the len is {len(ri)} but the index is {len(ri)}")
+        used = int(rp[rows]) if rows else 0
+        if np.any(rp[1:] < rp[:-1]) or used > nnz:
+            raise Panic("slice index starts after end")
+        ci = np.asarray(self.col_index, dtype=np.uint64)[:used]
+        v = np.asarray(self.v, dtype=self.dtype)[:used]
+        return rp, ci, v
+
+    def _device(self) -> "_lib.DeviceCsr":
+        if self._dev is not None:
+            return self._dev
+        if self.dtype not in GPU_DTYPES:
+            raise TypeError(f"Csr<{self.dtype}> has no GPU path (supported: f64 f32 i32 u32 i64 u64)")
+        rp, ci, v = self._csr_arrays()
+        if ci.size and int(ci.max()) >= self.dims.cols:
+            raise Panic(f"index out of bounds: column {int(ci.max())} >= {self.dims.cols}")
+        dev = _lib.DeviceCsr.upload(self.dims.rows, self.dims.cols, rp, ci, v)
+        if self.is_finalised:
+            self._dev = dev
+        return dev
+
+    @classmethod
+    def _from_device(cls, dev: "_lib.DeviceCsr") -> "Csr":
+        rp, ci, v = dev.download()
+        m = cls((dev.rows, dev.cols), dev.dtype)
+        m.row_index, m.col_index, m.v = rp, ci, v
+        m.is_finalised = True
+        m._dev = dev
+        return m
+
+    # ------------------------------------------------------------ hot path
+    def mul_dense(self, rhs: Dense) -> "Csr":
+        """sparse.rs:426-446: ``self * rhs`` as a new finalised Csr of dims
+        (rows, rhs.cols) with zero results dropped. GPU: spmm_rowwave /
+        spmv_stream + compaction (kernels_spmm.hip)."""
+        if self.dims.cols != rhs.get_dims().rows:
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        k = rhs.get_dims().cols
+        cols = [rhs.get_col(j) for j in range(k)]
+        return self._mul_dense_cols(cols, rhs.get_dims().rows)
+
+    def mul_dense_s(self, rhs: DenseS) -> "Csr":
+        """sparse.rs:448-466 (dimension check against ROWS, :449)."""
+        if self.dims.cols != rhs.ROWS:
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        k = rhs.get_dims().cols
+        cols = [rhs.get_col(j) for j in range(k)]
+        return self._mul_dense_cols(cols, rhs.ROWS)
+
+    def _mul_dense_cols(self, cols, x_rows: int) -> "Csr":
+        for c in cols:
+            if c.dtype != self.dtype:
+                raise TypeError(f"mul_dense: Csr<{self.dtype}> x Dense<{c.dtype}>")
+        dev = self._device()
+        lib = _lib.require_device()
+        arrs = [np.ascontiguousarray(c) for c in cols]
+        out = ctypes.c_void_p()
+        _raise_for(lib.bsm_csr_mul_dense(dev.handle, len(arrs), x_rows, _lib.ptr_array(arrs), ctypes.byref(out)))
+        return Csr._from_device(_lib.DeviceCsr(out.value))
+
+    def mul_vector(self, rhs, out: np.ndarray) -> None:
+        """sparse.rs:468-482: writes ``out`` in place (Rust ``&mut [T]``)."""
+        if self.dims.cols != len(rhs) or self.dims.rows != len(out):
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        if not isinstance(out, np.ndarray) or out.dtype != self.dtype or not out.flags.c_contiguous:
+            raise TypeError(f"out must be a contiguous numpy array of {self.dtype}")
+        x = np.ascontiguousarray(rhs, dtype=self.dtype)
+        dev = self._device()
+        lib = _lib.require_device()
+        _raise_for(lib.bsm_csr_mul_vector(dev.handle, _lib.ptr(x), len(x), _lib.ptr(out), len(out)))
+
+    def transpose(self) -> "Csr":
+        """sparse.rs:296-318 (stable CSR->CSC on the GPU)."""
+        if not self.is_finalised and len(self.v):
+            # the reference's row search reads row_index[row+1] past the end
+            # for the last recorded row of an unfinalised matrix
+            raise Panic("index out of bounds (transpose of an unfinalised matrix)")
+        dev = self._device()
+        lib = _lib.require_device()
+        out = ctypes.c_void_p()
+        _raise_for(lib.bsm_csr_transpose(dev.handle, ctypes.byref(out)))
+        return Csr._from_device(_lib.DeviceCsr(out.value))
+
+    def pair_with_tranpose(self):
+        """sparse.rs:320-323."""
+        return self, self.transpose()
+
+    def cholesky_decomp(self) -> "Csr":
+        """``impl Csr<f32>::cholesky_decomp`` (sparse.rs:682-714); f64 is this
+        build's addition."""
+        if self.dtype not in (np.dtype(np.float32), np.dtype(np.float64)):
+            raise TypeError("cholesky_decomp is defined for Csr<f32> (and Csr<f64> here)")
+        if self.dims.rows != self.dims.cols:
+            raise MatErr(MatErrKind.NonSquareMatrix)
+        dev = self._device()
+        lib = _lib.require_device()
+        out = ctypes.c_void_p()
+        _raise_for(lib.bsm_csr_cholesky(dev.handle, ctypes.byref(out)))
+        return Csr._from_device(_lib.DeviceCsr(out.value))
+
+    # ---------------------------------------------------------- comparisons
+    def __eq__(self, other) -> bool:
+        """Derived PartialEq over the seven fields of sparse.rs:68-78."""
+        if not isinstance(other, Csr):
+            return NotImplemented
+
+        def same(a, b):
+            a, b = np.asarray(a), np.asarray(b)
+            return a.shape == b.shape and bool(np.all(a == b))
+
+        return (
+            self.dims == other.dims
+            and same(self.v, other.v)
+            and same(np.asarray(self.col_index, dtype=np.uint64), np.asarray(other.col_index, dtype=np.uint64))
+            and same(np.asarray(self.row_index, dtype=np.uint64), np.asarray(other.row_index, dtype=np.uint64))
+            and self.is_finalised == other.is_finalised
+            and self.iter_v_index == other.iter_v_index
+            and self.iter_row_index == other.iter_row_index
+        )
+
+    def clone(self) -> "Csr":
+        m = Csr(self.dims, self.dtype)
+        for f in ("v", "col_index", "row_index"):
+            val = getattr(self, f)
+            setattr(m, f, val.copy() if isinstance(val, np.ndarray) else list(val))
+        m.is_finalised = self.is_finalised
+        m.iter_v_index, m.iter_row_index = self.iter_v_index, self.iter_row_index
+        m._dev = self._dev
+        return m
+
+    def __repr__(self) -> str:  # Debug (sparse.rs:797-805)
+        return (
+            f"dims:      {self.dims}\n"
+            f"v:         {list(np.asarray(self.v).tolist())}\n"
+            f"col_index: {[int(c) for c in self.col_index]}\n"
+            f"row_index: {[int(r) for r in self.row_index]}\n"
+        )
+
+    def __str__(self) -> str:  # Display (sparse.rs:777-795)
+        out = []
+        for r in range(self.dims.rows):
+            row = self.get_row_complete(r)
+            if row is None:
+                row = [self.dtype.type(0)] * self.dims.cols
+            out.append("|" + "".join(f"{x!s:>5} " for x in row) + "|")
+        return "\n".join(out) + ("\n" if out else "")

@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py -- CSR x dense SpMM throughput on MI355X (BASELINE.json metric:
+"CSR x dense SpMM effective GB/s (% HBM3E peak) at 1/2/4/8 GPUs; nnz/s").
+
+Workload (BASELINE.json north_star target / configs[3]): A = 10M x 10M
+synthetic random CSR, 1000 nnz per row (0.01 % density, nnz = 1e10), f64,
+times a dense 10M x 32 f64 RHS. It fits one MI355X (A 120 GB + X/Y 5 GB of
+288 GB HBM), so N=1 runs the whole matrix on one GPU. For N > 1 the rows are
+split into N contiguous, equal-nnz blocks (one process per GPU); X is
+replicated (every rank generates the same X from its seed -- no transfer) and
+the dense result Y is assembled on every rank with an RCCL all-gather over
+xGMI, as north_star specifies. Total work is fixed as N grows ("strong").
+
+One step = the hot path of Csr::mul_dense (src/sparse.rs:426-446) over the
+whole matrix: SpMM kernel (Y block) -> [all-gather of Y blocks] ->
+compaction of Y into the output Csr (zero-dropping insert, sparse.rs:229).
+Inputs are resident in HBM before timing starts.
+
+value = B_alg / step time (whole job), with the canonical algorithmic bytes
+of SURVEY.md §8d: B_alg = 8(N+1) + 12 nnz + 8 n_cols k + 8 N k.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before the HIP library: one runtime)
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (rows, n_cols, nnz_per_row, k)
+    "c4": (10_000_000, 10_000_000, 1000, 32),
+    "c3": (1_000_000, 1_000_000, 10, 32),
+    "c2": (1_000_000, 1_000_000, 10, 1),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED_A, SEED_X = 1000, 1001
+
+
+def b_alg(rows, n_cols, nnz, k):
+    return 8 * (rows + 1) + 12 * nnz + 8 * n_cols * k + 8 * rows * k
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg_name, sample_rows):
+    """The oracle's restatement of Csr::mul_dense (oracle/, single thread)
+    timed on the first `sample_rows` rows of the same workload, extrapolated
+    linearly to the full row count (rows are statistically identical)."""
+    from oracle import pyoracle as orc
+
+    rows, n_cols, nnz_r, k = CONFIGS[cfg_name]
+    rp = np.arange(sample_rows + 1, dtype=np.uint64) * nnz_r
+    ci, v = orc.gen_entries(SEED_A, rp, n_cols)
+    t0 = time.perf_counter()
+    x_cols = orc.gen_x_cols(SEED_X, n_cols, k)
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc.mul_dense(sample_rows, n_cols, rp, ci, v, x_cols)
+    t = time.perf_counter() - t0
+    t_full = t * rows / sample_rows
+    nnz = rows * nnz_r
+    return {
+        "value": round(b_alg(rows, n_cols, nnz, k) / t_full / 1e9, 4),
+        "unit": "GB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle mul_dense (C restatement of sparse.rs:426-446, -O2, 1 thread) on the first "
+                  f"{sample_rows} of {rows} rows ({sample_rows * nnz_r} nnz x {k} RHS) in {t:.2f} s, "
+                  f"extrapolated x{rows // sample_rows} to {t_full:.1f} s per full SpMM (X generation "
+                  f"{t_gen:.1f} s untimed)",
+        "nnz_per_s": round(sample_rows * nnz_r / t, 1),
+        "host_cpus": os.cpu_count(),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=5000)
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from basic_sparse_matrix_amd import _lib
+    from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
+
+    rows, n_cols, nnz_r, k = CONFIGS[args.config]
+    # contiguous row blocks, equal rows (= equal nnz: constant row length);
+    # padded to a common size for the equal-count all-gather
+    per = (rows + world - 1) // world
+    row0 = min(rows, rank * per)
+    my_rows = max(0, min(rows, row0 + per) - row0)
+
+    t0 = time.perf_counter()
+    blk = DeviceCsrBlock.generate(SEED_A, row0, my_rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r,
+                                  _lib.VAL_UNIFORM, np.float64, device=dev)
+    x = gen_dense(SEED_X, 0, n_cols, k, device=dev)
+    y_local = torch.empty((per, k), dtype=torch.float64, device=dev)
+    nnz_local = torch.zeros(per, dtype=torch.int32, device=dev)
+    if world > 1:
+        y_full = torch.empty((per * world, k), dtype=torch.float64, device=dev)
+        nnz_full = torch.empty(per * world, dtype=torch.int32, device=dev)
+    else:
+        y_full, nnz_full = y_local, nnz_local
+    comp = Compactor(rows, k, np.float64, device=dev)
+    torch.cuda.synchronize()
+    log(f"rank {rank}: rows [{row0},{row0 + my_rows}) nnz {blk.nnz:,} generated in {time.perf_counter() - t0:.1f} s")
+
+    ev_k0 = torch.cuda.Event(enable_timing=True)
+    ev_k1 = torch.cuda.Event(enable_timing=True)
+    ev_c0 = torch.cuda.Event(enable_timing=True)
+    ev_c1 = torch.cuda.Event(enable_timing=True)
+    kern_ms, comm_ms, comp_ms = [], [], []
+
+    def step(timed):
+        if timed:
+            ev_k0.record()
+        blk.spmm(x, y_local[:my_rows], nnz_local[:my_rows])
+        if timed:
+            ev_k1.record()
+        if world > 1:
+            dist.all_gather_into_tensor(y_full, y_local)
+            dist.all_gather_into_tensor(nnz_full, nnz_local)
+        if timed:
+            ev_c0.record()
+        comp(y_full[:rows], nnz_full[:rows])
+        if timed:
+            ev_c1.record()
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        torch.cuda.synchronize()  # events of this step are complete
+        kern_ms.append(ev_k0.elapsed_time(ev_k1))
+        comm_ms.append(ev_k1.elapsed_time(ev_c0))
+        comp_ms.append(ev_c0.elapsed_time(ev_c1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kmax = float(t[0]), float(t[1])
+    else:
+        kmax = float(np.mean(kern_ms))
+
+    out_nnz = comp.nnz()
+    nnz_total = rows * nnz_r
+    ms_per_step = elapsed / args.steps * 1e3
+    value = b_alg(rows, n_cols, nnz_total, k) / (elapsed / args.steps) / 1e9
+    # roofline of the dominant kernel (spmm_rowwave): per-launch algorithmic
+    # bytes of THIS rank's launch over its measured average duration
+    b_launch = b_alg(my_rows, n_cols, blk.nnz, k)
+    achieved = b_launch / (float(np.mean(kern_ms)) / 1e3) / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            log("timing cpu baseline ...")
+            cpu = cpu_baseline(args.config, args.cpu_sample_rows)
+        traffic = args.traffic_bytes
+        line = {
+            "metric": "CSR x dense SpMM effective GB/s (B_alg / step time); nnz/s",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SplitMix64 random CSR, sorted distinct uniform columns, values U[0.5,1.5); "
+                    "generated on device from seeds 1000/1001)",
+            "config": {
+                "workload": f"{args.config}: {rows:,} x {n_cols:,} CSR, {nnz_r} nnz/row "
+                            f"({100.0 * nnz_r / n_cols:g} % density, nnz {nnz_total:,}) x {k}-column dense RHS, "
+                            f"f64; step = SpMM + {'RCCL all-gather of Y + ' if world > 1 else ''}compaction "
+                            f"to Csr",
+                "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
+                "parallelism": f"row-block x{world}" + (" + all-gather" if world > 1 else ""),
+            },
+            "nnz_per_s": round(nnz_total / (elapsed / args.steps), 1),
+            "hbm_frac_of_peak": round(value / (world * HBM_PEAK_GBS), 5),
+            "breakdown_ms": {
+                "spmm_kernel_mean": round(float(np.mean(kern_ms)), 3),
+                "spmm_kernel_max_over_ranks": round(kmax, 3),
+                "allgather_mean": round(float(np.mean(comm_ms)), 3),
+                "compaction_mean": round(float(np.mean(comp_ms)), 3),
+            },
+            "output_nnz": out_nnz,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "spmm_rowwave<double,32,8>",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "bytes_per_launch_alg": b_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

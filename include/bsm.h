@@ -1,0 +1,153 @@
+/*
+ * bsm.h -- C-ABI of the MI355X-native sparse-matrix hot path
+ * (libbsm_hip.so, built from basic_sparse_matrix_amd/csrc/).
+ *
+ * This is the drop-in boundary for the reference crate
+ * jamieapps101/Basic_Sparse_Matrix (pure Rust). The reference has no FFI of
+ * its own; these are the entry points its hot-path methods would bind
+ * through `extern "C"` (see INTEGRATION.md for the Rust-side binding). Every
+ * function below names the reference item it replaces.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; indices are uint64_t like Rust's usize.
+ *  - Host-buffer entry points (bsm_csr_*, bsm_solve, ...) are synchronous:
+ *    when they return, device work is complete and output host buffers are
+ *    filled. The library NEVER takes ownership of caller memory; device
+ *    memory is owned by opaque handles released with bsm_csr_free.
+ *  - Device entry points (bsm_dev_*) take device (HBM) pointers and a
+ *    hipStream_t passed as void*; they enqueue work and return immediately.
+ *  - Return value: BSM_OK (0) or a bsm_status; bsm_last_error() gives a
+ *    thread-local message. Dimension checks that the reference answers with
+ *    Err(MatErr::...) are repeated here (BSM_ERR_DIMENSIONS /
+ *    BSM_ERR_NON_SQUARE) but callers are expected to check first, as the
+ *    reference does, so that Err values stay identical.
+ *  - Arithmetic: floating point is IEEE with no FMA contraction and the
+ *    reference's summation order (bit-exact); integers wrap
+ *    (reference bench profile overflow-checks=false, Cargo.toml:18).
+ *  - Device CSR layout: row_ptr int64[rows+1], col int32[nnz] (so cols must
+ *    be < 2^31), values T[nnz]. Dense operands on device are ROW-major
+ *    (n x k, element (r,j) at r*k + j) so one CSR entry gathers k contiguous
+ *    values; host Dense operands are the reference's column list
+ *    (Vec<Vec<T>>, dense.rs:8) passed as an array of k column pointers.
+ */
+#ifndef BSM_H
+#define BSM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSM_API_VERSION 1
+
+/* Scalar types of the reference's generic T that run on the GPU. */
+typedef enum bsm_dtype {
+    BSM_F64 = 0,
+    BSM_F32 = 1,
+    BSM_I32 = 2,
+    BSM_U32 = 3,
+    BSM_I64 = 4,
+    BSM_U64 = 5
+} bsm_dtype;
+
+typedef enum bsm_status {
+    BSM_OK = 0,
+    BSM_ERR_INVALID = 1,     /* bad argument (null pointer, unknown dtype, ...) */
+    BSM_ERR_DIMENSIONS = 2,  /* MatErr::IncorrectDimensions (util.rs:51) */
+    BSM_ERR_NON_SQUARE = 3,  /* MatErr::NonSquareMatrix (util.rs:50) */
+    BSM_ERR_PANIC = 4,       /* input on which the reference panics (OOB index, empty row) */
+    BSM_ERR_HIP = 5,         /* HIP runtime error */
+    BSM_ERR_OOM = 6,         /* device allocation failed */
+    BSM_ERR_UNSUPPORTED = 7, /* valid input outside what this build implements */
+    BSM_ERR_NO_DEVICE = 8    /* no usable gfx950 device */
+} bsm_status;
+
+/* Opaque device-resident CSR matrix (a finalised Csr<T>, sparse.rs:68-78). */
+typedef struct bsm_csr bsm_csr;
+
+/* ---- library ------------------------------------------------------------ */
+int bsm_api_version(void);
+/* Thread-local description of the last failure on this thread. */
+const char* bsm_last_error(void);
+int bsm_device_count(int* n);
+/* Select the device used by subsequent calls on this thread. */
+int bsm_set_device(int ordinal);
+
+/* ---- device-resident CSR handles ---------------------------------------- */
+/* Upload a finalised Csr<T> (sparse.rs:68-78: row_index = row_ptr of length
+ * rows+1, col_index, v). Replaces nothing in the reference: it is the
+ * marshalling step a Rust `mul_dense` performs before the kernel call (the
+ * handle can be cached by the caller because a finalised Csr is immutable:
+ * insert returns Err(MatrixFinalised), sparse.rs:223-225). */
+int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz,
+                   const uint64_t* row_ptr, const uint64_t* col_idx, const void* vals,
+                   bsm_csr** out);
+int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz,
+                  int* dtype);
+/* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz). */
+int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, void* vals);
+void bsm_csr_free(bsm_csr* m);
+
+/* ---- hot path (host buffers in/out, synchronous) ------------------------- */
+/* Csr::mul_dense (sparse.rs:426-446) and Csr::mul_dense_s (sparse.rs:448-466):
+ * out = a * X as a new finalised Csr with dims (rows, k), zero results
+ * dropped (sparse.rs:229). X is k columns of x_rows values each
+ * (Dense::get_col, dense.rs:31-33). x_rows != cols -> BSM_ERR_DIMENSIONS. */
+int bsm_csr_mul_dense(const bsm_csr* a, uint64_t k, uint64_t x_rows, const void* const* x_cols,
+                      bsm_csr** out);
+/* Csr::mul_vector (sparse.rs:468-482): out[i] = sum over row i of
+ * v * rhs[col] in ascending column order, dense output, no zero skip. */
+int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void* out,
+                       uint64_t out_len);
+/* Csr::transpose (sparse.rs:296-318): stable CSR -> CSC. */
+int bsm_csr_transpose(const bsm_csr* a, bsm_csr** out);
+/* impl Csr<f32>::cholesky_decomp (sparse.rs:682-714); F64 is this build's
+ * addition. Square check -> BSM_ERR_NON_SQUARE. */
+int bsm_csr_cholesky(const bsm_csr* a, bsm_csr** out);
+/* forward_substitution (lib.rs:28-46): solve L y = b for k RHS columns of n. */
+int bsm_forward_substitution(const bsm_csr* l, uint64_t k, uint64_t n,
+                             const void* const* b_cols, void* const* y_cols);
+/* backward_substitution (lib.rs:49-65): solve U x = y, U = L^T as a Csr. */
+int bsm_backward_substitution(const bsm_csr* u, uint64_t k, uint64_t n,
+                              const void* const* y_cols, void* const* x_cols);
+/* solve (lib.rs:11-24): x = A^-1 b via cholesky_decomp + transpose +
+ * forward/backward substitution, all on the device. */
+int bsm_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
+              void* const* x_cols);
+
+/* ---- device-level entry points (HBM pointers, async on `stream`) --------- */
+/* Synthetic CSR generator (bsm_synth.h recipe): rows [row0, row0+rows) of a
+ * matrix with n_cols columns, rowlen_kind CONST/UNIFORM (a, b), value_kind
+ * UNIFORM/SMALLINT. Writes row_ptr (rows+1, local, starting at 0), col, vals.
+ * bsm_dev_gen_row_ptr must run first; its nnz is row_ptr[rows]. Rows longer
+ * than 4096 are not supported by the device generator. */
+int bsm_dev_gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols,
+                        int rowlen_kind, uint32_t a, uint32_t b, int64_t* row_ptr,
+                        void* workspace, uint64_t workspace_bytes, void* stream);
+int bsm_dev_gen_entries(int dtype, uint64_t seed, uint64_t row0, uint64_t rows,
+                        uint32_t n_cols, int value_kind, const int64_t* row_ptr,
+                        int32_t* col, void* vals, void* stream);
+/* Dense ROW-major n x k operand: X[r][j] = bsm_x_value(seed, row0 + r, j). */
+int bsm_dev_gen_dense(int dtype, uint64_t seed, uint64_t row0, uint64_t n, uint64_t k,
+                      int value_kind, void* x, void* stream);
+/* Workspace bytes needed by the scans of bsm_dev_gen_row_ptr / bsm_dev_spmm_csr. */
+uint64_t bsm_dev_scan_workspace_bytes(uint64_t n);
+/* Y = A X (dense ROW-major Y, rows x k), the kernel of mul_dense. row_nnz
+ * (int32[rows], may be NULL) receives the count of nonzero results per row
+ * for compaction. */
+int bsm_dev_spmm(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz,
+                 const int64_t* row_ptr, const int32_t* col, const void* vals, uint64_t k,
+                 const void* x, void* y, int32_t* row_nnz, void* stream);
+/* Compaction of a dense result into the reference's output Csr (insert's
+ * zero skip, sparse.rs:229): out_row_ptr (rows+1), out_col/out_vals with
+ * capacity rows*k. */
+int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y,
+                    const int32_t* row_nnz, int64_t* out_row_ptr, int32_t* out_col,
+                    void* out_vals, void* workspace, uint64_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BSM_H */

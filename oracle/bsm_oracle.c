@@ -1,0 +1,150 @@
+/*
+ * bsm_oracle.c -- CPU ORACLE (test infrastructure only; see bsm_oracle.h).
+ * Compile with -O2 -ffp-contract=off (no FMA: Rust never contracts).
+ */
+#include "bsm_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../basic_sparse_matrix_amd/csrc/bsm_synth.h"
+
+#define T double
+#define SUF f64
+#define UT uint64_t
+#define ISF 1
+#define SQRT sqrt
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+#undef SQRT
+
+#define T float
+#define SUF f32
+#define UT uint32_t
+#define ISF 1
+#define SQRT sqrtf
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+#undef SQRT
+
+#define T int32_t
+#define SUF i32
+#define UT uint32_t
+#define ISF 0
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+
+#define T uint32_t
+#define SUF u32
+#define UT uint32_t
+#define ISF 0
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+
+#define T int64_t
+#define SUF i64
+#define UT uint64_t
+#define ISF 0
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+
+#define T uint64_t
+#define SUF u64
+#define UT uint64_t
+#define ISF 0
+#include "bsm_oracle_tpl.inc"
+#undef T
+#undef SUF
+#undef UT
+#undef ISF
+
+/* ---- synthetic inputs (bsm_synth.h recipe) ------------------------------ */
+
+int orc_gen_row_ptr(uint64_t seed, uint64_t rows, uint32_t n_cols, int rowlen_kind, uint32_t a,
+                    uint32_t b, uint64_t* row_ptr) {
+    row_ptr[0] = 0;
+    for (uint64_t r = 0; r < rows; ++r) {
+        uint64_t len;
+        if (rowlen_kind == BSM_ROWLEN_BINOMIAL) {
+            len = 0;
+            for (uint32_t j = 0; j < n_cols; ++j)
+                if ((bsm_hash(seed, r, j, BSM_SALT_ROWLEN) >> 32) < (uint64_t)a) ++len;
+        } else {
+            len = bsm_rowlen(seed, r, rowlen_kind, a, b);
+        }
+        if (len > n_cols) len = n_cols;
+        row_ptr[r + 1] = row_ptr[r] + len;
+    }
+    return 0;
+}
+
+static int cmp_u32(const void* x, const void* y) {
+    uint32_t a = *(const uint32_t*)x, b = *(const uint32_t*)y;
+    return (a > b) - (a < b);
+}
+
+int orc_gen_entries(uint64_t seed, uint64_t r0, uint64_t r1, uint32_t n_cols,
+                    const uint64_t* row_ptr, int value_kind, uint64_t* col_idx, double* vals) {
+    uint64_t maxlen = 0;
+    for (uint64_t r = r0; r < r1; ++r)
+        if (row_ptr[r + 1] - row_ptr[r] > maxlen) maxlen = row_ptr[r + 1] - row_ptr[r];
+    uint32_t* tmp = (uint32_t*)malloc((maxlen ? maxlen : 1) * sizeof(uint32_t));
+    if (!tmp) return ORC_ERR_ALLOC;
+    for (uint64_t r = r0; r < r1; ++r) {
+        uint64_t s = row_ptr[r], len = row_ptr[r + 1] - s;
+        for (uint64_t j = 0; j < len; ++j) tmp[j] = bsm_col_draw(seed, r, j, n_cols);
+        qsort(tmp, len, sizeof(uint32_t), cmp_u32);
+        /* forward bump: strictly increasing */
+        for (uint64_t j = 1; j < len; ++j)
+            if (tmp[j] <= tmp[j - 1]) tmp[j] = tmp[j - 1] + 1;
+        /* backward clamp into [0, n_cols) */
+        if (len) {
+            if (tmp[len - 1] > n_cols - 1) tmp[len - 1] = n_cols - 1;
+            for (uint64_t j = len - 1; j-- > 0;)
+                if (tmp[j] >= tmp[j + 1]) tmp[j] = tmp[j + 1] - 1;
+        }
+        for (uint64_t j = 0; j < len; ++j) {
+            if (col_idx) col_idx[s + j] = tmp[j];
+            if (vals) vals[s + j] = bsm_a_value(seed, r, j, value_kind);
+        }
+    }
+    free(tmp);
+    return 0;
+}
+
+void orc_gen_x_colmajor(uint64_t seed, uint64_t n_cols, uint64_t k, int value_kind, double* x) {
+    for (uint64_t c = 0; c < k; ++c)
+        for (uint64_t r = 0; r < n_cols; ++r) x[c * n_cols + r] = bsm_x_value(seed, r, c, value_kind);
+}
+
+uint64_t orc_gen_poisson2d(uint64_t g, uint64_t* row_ptr, uint64_t* col_idx, double* v) {
+    uint64_t n = g * g, p = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t iy = i / g, ix = i % g;
+        if (row_ptr) row_ptr[i] = p;
+        if (iy > 0) { if (col_idx) { col_idx[p] = i - g; v[p] = -1.0; } ++p; }
+        if (ix > 0) { if (col_idx) { col_idx[p] = i - 1; v[p] = -1.0; } ++p; }
+        if (col_idx) { col_idx[p] = i; v[p] = 4.0; }
+        ++p;
+        if (ix + 1 < g) { if (col_idx) { col_idx[p] = i + 1; v[p] = -1.0; } ++p; }
+        if (iy + 1 < g) { if (col_idx) { col_idx[p] = i + g; v[p] = -1.0; } ++p; }
+    }
+    if (row_ptr) row_ptr[n] = p;
+    return p;
+}

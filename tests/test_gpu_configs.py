@@ -1,0 +1,100 @@
+"""GPU parity at the BASELINE.json configurations.
+
+C2: 1M x 1M, 10 nnz/row, k=1 (SpMV); C3: same A, k=32 (SpMM); C4: 10M x 10M,
+1000 nnz/row, k=32 -- checked on a row sample plus size-independent
+properties, since the full C4 oracle run is ~1 h of CPU. Inputs come from
+the device generator, which is first shown to equal the host restatement
+integer for integer.
+"""
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from basic_sparse_matrix_amd import _lib  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    from basic_sparse_matrix_amd import device
+
+    return device
+
+
+def test_device_generator_matches_host(orc):
+    device = _dev()
+    for (rows, n_cols, kind, a, b, vk, dt) in [
+        (5000, 100_000, orc.ROWLEN_CONST, 10, 10, orc.VAL_UNIFORM, np.float64),
+        (3000, 5000, orc.ROWLEN_UNIFORM, 0, 1200, orc.VAL_SMALLINT, np.int32),
+        (400, 1500, orc.ROWLEN_UNIFORM, 1000, 1500, orc.VAL_UNIFORM, np.float32),  # bump passes
+    ]:
+        blk = device.DeviceCsrBlock.generate(1000, 777, rows, n_cols, kind, a, b, vk, dt)
+        rp = orc.gen_row_ptr(1000, rows + 777, n_cols, kind, a, b)
+        rp = (rp[777:] - rp[777]).astype(np.int64)
+        assert np.array_equal(blk.row_ptr.cpu().numpy(), rp)
+        full_rp = orc.gen_row_ptr(1000, rows + 777, n_cols, kind, a, b)
+        ci, v = orc.gen_entries(1000, full_rp, n_cols, vk, r0=777, r1=777 + rows)
+        lo = int(full_rp[777])
+        assert np.array_equal(blk.col.cpu().numpy().astype(np.uint64), ci[lo:])
+        assert np.array_equal(blk.vals.cpu().numpy(), v[lo:].astype(dt))
+        cols = ci[lo:].astype(np.int64)
+        # strictly increasing inside every row, within [0, n_cols)
+        inside = np.ones(max(0, len(cols) - 1), dtype=bool)
+        b = rp[1:-1]
+        inside[b[(b > 0) & (b < len(cols))] - 1] = False
+        assert (np.diff(cols)[inside] > 0).all() and cols.min() >= 0 and cols.max() < n_cols
+    x = device.gen_dense(1001, 5, 1000, 7)
+    ex = np.stack(orc.gen_x_cols(1001, 1005, 7), axis=1)[5:]
+    assert np.array_equal(x.cpu().numpy(), ex)
+
+
+def _run_spmm(blk, x, k):
+    device = _dev()
+    y = torch.empty((blk.rows, k), dtype=torch.float64, device="cuda")
+    row_nnz = torch.empty(blk.rows, dtype=torch.int32, device="cuda")
+    blk.spmm(x, y, row_nnz)
+    comp = device.Compactor(blk.rows, k, np.float64)
+    comp(y, row_nnz)
+    torch.cuda.synchronize()
+    return y, comp
+
+
+@pytest.mark.parametrize("k", [1, 32])
+def test_c2_c3_full_size_bit_exact(orc, k):
+    """C2 (k=1) and C3 (k=32) at full size, every output element checked."""
+    device = _dev()
+    rows = n_cols = 1_000_000
+    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_CONST, 10, 10)
+    x = device.gen_dense(1001, 0, n_cols, k)
+    y, comp = _run_spmm(blk, x, k)
+    rp = orc.gen_row_ptr(1000, rows, n_cols, orc.ROWLEN_CONST, 10, 10)
+    ci, v = orc.gen_entries(1000, rp, n_cols)
+    x_cols = orc.gen_x_cols(1001, n_cols, k)
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    assert np.array_equal(comp.row_ptr.cpu().numpy(), erp.astype(np.int64))
+    n = comp.nnz()
+    assert np.array_equal(comp.col[:n].cpu().numpy().astype(np.uint64), eci)
+    assert np.array_equal(comp.vals[:n].cpu().numpy().view(np.uint64), ev.view(np.uint64))
+
+
+def test_c4_shape_sampled_rows(orc):
+    """C4 shape (10M columns, 1000 nnz/row, k=32) on a 4k-row block taken
+    from the middle of the 10M rows: every output of the block is compared
+    bit-exactly with the oracle."""
+    device = _dev()
+    n_cols, k, row0, rows = 10_000_000, 32, 4_321_000, 4_000
+    blk = device.DeviceCsrBlock.generate(1000, row0, rows, n_cols, _lib.ROWLEN_CONST, 1000, 1000)
+    x = device.gen_dense(1001, 0, n_cols, k)
+    y, comp = _run_spmm(blk, x, k)
+    rp = np.arange(rows + 1, dtype=np.uint64) * 1000
+    full = np.zeros(row0 + rows + 1, dtype=np.uint64)
+    full[row0:] = rp  # only rows [row0, row0+rows) are generated
+    ci, v = orc.gen_entries(1000, full, n_cols, r0=row0, r1=row0 + rows)
+    x_cols = orc.gen_x_cols(1001, n_cols, k)
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    assert np.array_equal(comp.row_ptr.cpu().numpy(), erp.astype(np.int64))
+    n = comp.nnz()
+    assert n == rows * k  # positive inputs: nothing is dropped
+    assert np.array_equal(comp.vals[:n].cpu().numpy().view(np.uint64), ev.view(np.uint64))

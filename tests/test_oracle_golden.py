@@ -1,0 +1,125 @@
+"""Pin the CPU oracle (oracle/) to the reference's own golden vectors.
+
+Every expected value comes from tests/golden/reference_unit_tests.json,
+transcribed from the reference's #[test] functions (file:line in each entry).
+The oracle is the checker for the GPU parity tests, so it must reproduce
+these bit for bit first.
+"""
+
+import numpy as np
+import pytest
+
+from golden.golden_io import f32, matrix, scalars
+
+DT = {"i32": np.int32, "f32": np.float32, "f64": np.float64}
+
+
+def csr_of(rows, dtype):
+    """Csr::from_data semantics (sparse.rs:193-203) as plain arrays."""
+    a = np.asarray(rows, dtype=dtype)
+    nzr, nzc = np.nonzero(~(a == 0))
+    counts = np.bincount(nzr, minlength=a.shape[0])
+    rp = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    return a.shape[0], a.shape[1], rp, nzc.astype(np.uint64), a[nzr, nzc]
+
+
+def test_dense_mul(orc, golden):
+    g = golden["test_dense_mul"]
+    rows, cols, rp, ci, v = csr_of(g["rows"], np.int32)
+    x_cols = [np.asarray(c, dtype=np.int32) for c in g["x_cols"]]
+    o_rp, o_ci, o_v = orc.mul_dense(rows, cols, rp, ci, v, x_cols)
+    e_rows, e_cols, e_rp, e_ci, e_v = csr_of(g["out_rows"], np.int32)
+    assert np.array_equal(o_rp, e_rp) and np.array_equal(o_ci, e_ci) and np.array_equal(o_v, e_v)
+
+
+def test_nnz_zero_skipping(orc, golden):
+    g = golden["test_nnz"]
+    rows, cols, rp, ci, v = csr_of(g["rows"], np.int32)
+    x_cols = [np.asarray(c, dtype=np.int32) for c in g["x_cols"]]
+    o_rp, o_ci, o_v = orc.mul_dense(rows, cols, rp, ci, v, x_cols)
+    _, _, e_rp, e_ci, e_v = csr_of(g["out_rows"], np.int32)
+    assert list(o_rp) == list(e_rp) and list(o_ci) == list(e_ci) and list(o_v) == list(e_v)
+    assert int(o_rp[-1]) == g["out_nnz"]
+
+
+def test_mul_dense_dimension_error(orc):
+    rows, cols, rp, ci, v = csr_of([[1, 2], [3, 4]], np.int32)
+    with pytest.raises(orc.OracleError) as e:
+        orc.mul_dense(rows, cols, rp, ci, v, [np.zeros(3, np.int32)], x_rows=3)
+    assert e.value.code == orc.ORC_ERR_INCORRECT_DIMENSIONS
+
+
+@pytest.mark.parametrize("name", ["transpose_1x1", "transpose_nxn", "transpose_mxn"])
+def test_transpose(orc, golden, name):
+    g = golden[name]
+    rows, cols, rp, ci, v = csr_of(g["rows"], np.int32)
+    t_rp, t_ci, t_v = orc.transpose(rows, cols, rp, ci, v)
+    _, _, e_rp, e_ci, e_v = csr_of(g["t_rows"], np.int32)
+    assert list(t_rp) == list(e_rp) and list(t_ci) == list(e_ci) and list(t_v) == list(e_v)
+
+
+def test_mul_vector(orc, golden):
+    g = golden["test_mul_vector"]
+    vec = np.asarray(g["v"], dtype=np.int32)
+    rows, cols, rp, ci, v = csr_of(g["err_rows"], np.int32)
+    with pytest.raises(orc.OracleError) as e:
+        orc.mul_vector(rows, cols, rp, ci, v, vec, out_len=g["err_out_len"])
+    assert e.value.code == orc.ORC_ERR_INCORRECT_DIMENSIONS
+    rows, cols, rp, ci, v = csr_of(g["eye_rows"], np.int32)
+    assert list(orc.mul_vector(rows, cols, rp, ci, v, vec)) == list(vec)
+    rows, cols, rp, ci, v = csr_of(g["rows"], np.int32)
+    assert list(orc.mul_vector(rows, cols, rp, ci, v, vec)) == g["out"]
+
+
+@pytest.mark.parametrize("band", [False, True])
+@pytest.mark.parametrize("name", ["cholesky_decomposition_0", "cholesky_decomposition_1"])
+def test_cholesky_f32_bit_exact(orc, golden, name, band):
+    g = golden[name]
+    rows, cols, rp, ci, v = csr_of(matrix(g["rows"], np.float32), np.float32)
+    l_rp, l_ci, l_v = orc.cholesky(rows, cols, rp, ci, v, band=band)
+    _, _, e_rp, e_ci, e_v = csr_of(matrix(g["l_rows"], np.float32), np.float32)
+    assert list(l_rp) == list(e_rp) and list(l_ci) == list(e_ci)
+    assert l_v.dtype == np.float32
+    assert l_v.view(np.uint32).tolist() == np.asarray(e_v, np.float32).view(np.uint32).tolist()
+    if "u_rows" in g:
+        u_rp, u_ci, u_v = orc.transpose(rows, cols, l_rp, l_ci, l_v)
+        _, _, f_rp, f_ci, f_v = csr_of(matrix(g["u_rows"], np.float32), np.float32)
+        assert list(u_rp) == list(f_rp) and list(u_ci) == list(f_ci)
+        assert u_v.view(np.uint32).tolist() == np.asarray(f_v, np.float32).view(np.uint32).tolist()
+
+
+def test_cholesky_non_square(orc):
+    rows, cols, rp, ci, v = csr_of([[1.0, 2.0, 3.0]], np.float32)
+    with pytest.raises(orc.OracleError) as e:
+        orc.cholesky(rows, cols, rp, ci, v)
+    assert e.value.code == orc.ORC_ERR_NON_SQUARE
+
+
+def _bits(xs):
+    return np.asarray(xs, dtype=np.float32).view(np.uint32).tolist()
+
+
+def test_forward_substitution(orc, golden):
+    g = golden["forward_substitution_test_0"]
+    n, _, rp, ci, v = csr_of(matrix(g["l_rows"], np.float32), np.float32)
+    b = [np.asarray(scalars(c, np.float32), np.float32) for c in g["b_cols"]]
+    y = orc.forward_substitution(n, rp, ci, v, b)
+    assert _bits(y[0]) == _bits([f32(s) for s in g["y_cols"][0]])
+
+
+def test_backward_substitution(orc, golden):
+    g = golden["backward_substitution_test_0"]
+    n, _, rp, ci, v = csr_of(matrix(g["u_rows"], np.float32), np.float32)
+    y = [np.asarray(scalars(c, np.float32), np.float32) for c in g["y_cols"]]
+    x = orc.backward_substitution(n, rp, ci, v, y)
+    assert _bits(x[0]) == _bits([f32(s) for s in g["x_cols"][0]])
+
+
+@pytest.mark.parametrize("band", [False, True])
+def test_solve(orc, golden, band):
+    g = golden["solve_test"]
+    n, _, rp, ci, v = csr_of(matrix(g["rows"], np.float32), np.float32)
+    b = [np.asarray(scalars(c, np.float32), np.float32) for c in g["b_cols"]]
+    x = orc.solve(n, rp, ci, v, b, band=band)
+    # x_ref = [0.625, -0.1, 2.6999998, 0.5]: the f32 rounding of the chain
+    assert _bits(x[0]) == _bits([f32(s) for s in g["x_cols"][0]])
