@@ -11,6 +11,9 @@
 #include "bsm_internal.hpp"
 #include "bsm_synth.h"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace bsm {
 namespace {
 
@@ -173,6 +176,107 @@ __global__ __launch_bounds__(256) void spmm_rowwave(int64_t rows, const int64_t*
         nz_count += __popcll(m);
     }
     if (lane == 0 && row_nnz) row_nnz[row] = nz_count;
+}
+
+// ---------------------------------------------------------------------------
+// SpMM specialised for f64 with k = 32 (the C3/C4 shape): one wavefront per
+// CSR row; lane l = 16*g + q gathers the 16-byte pair X[col_e][2q..2q+1] of
+// entry e = e0 + 4u + g, so ONE global_load_dwordx4 wave instruction fetches
+// four whole 256-B X rows. The four products of a column pair are
+// brought to the group-0 lanes with v_permlane16/32_swap (no LDS) and added
+// in entry order: own (g0), lane^16 (g1), lane^32 (g2), lane^48 (g3).
+// Per 4 entries: 1 gather + 2 index/value loads (VMEM), 12 permlanes, 8 adds.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double from_u2(unsigned lo, unsigned hi) {
+    return __hiloint2double((int)hi, (int)lo);
+}
+// value of lane^16 (valid in even 16-lane rows, i.e. lanes 0-15 and 32-47)
+__device__ __forceinline__ double xchg16_even(double v) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return from_u2(rl[1], rh[1]);
+}
+// value of lane^32 (valid in lanes 0-31)
+__device__ __forceinline__ double xchg32_low(double v) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return from_u2(rl[1], rh[1]);
+}
+
+template <int STEPS, bool PIPE>
+__global__ __launch_bounds__(256) void spmm_k32_f64(int64_t rows, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col,
+                                                    const double* __restrict__ val,
+                                                    const double2* __restrict__ X,
+                                                    double2* __restrict__ Y,
+                                                    int32_t* __restrict__ row_nnz) {
+    constexpr int CH = 4 * STEPS;  // entries per iteration
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+    if (row >= rows) return;
+    const int g = lane >> 4, q = lane & 15;
+    const int64_t start = rp[row], end = rp[row + 1];
+    double a0 = 0.0, a1 = 0.0;
+    int64_t e0 = start;
+    // each lane loads the index/value of ITS entry (4 distinct addresses per
+    // wave instruction, one cache line)
+    int32_t c[STEPS];
+    double v[STEPS];
+    if (PIPE && e0 + CH <= end) {
+#pragma unroll
+        for (int u = 0; u < STEPS; ++u) { c[u] = col[e0 + 4 * u + g]; v[u] = val[e0 + 4 * u + g]; }
+    }
+    for (; e0 + CH <= end; e0 += CH) {  // full chunks
+        if (!PIPE) {
+#pragma unroll
+            for (int u = 0; u < STEPS; ++u) { c[u] = col[e0 + 4 * u + g]; v[u] = val[e0 + 4 * u + g]; }
+        }
+        double2 x[STEPS];
+#pragma unroll
+        for (int u = 0; u < STEPS; ++u) x[u] = X[(int64_t)c[u] * 16 + q];
+        double vc[STEPS];
+#pragma unroll
+        for (int u = 0; u < STEPS; ++u) vc[u] = v[u];
+        if (PIPE && e0 + 2 * CH <= end) {  // software pipeline: next chunk's indices
+#pragma unroll
+            for (int u = 0; u < STEPS; ++u) {
+                c[u] = col[e0 + CH + 4 * u + g];
+                v[u] = val[e0 + CH + 4 * u + g];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < STEPS; ++u) {
+            const double vv = vc[u];
+            const double p0 = __dmul_rn(vv, x[u].x), p1 = __dmul_rn(vv, x[u].y);
+            const double p0_16 = xchg16_even(p0), p1_16 = xchg16_even(p1);
+            const double p0_32 = xchg32_low(p0), p1_32 = xchg32_low(p1);
+            const double p0_48 = xchg32_low(p0_16), p1_48 = xchg32_low(p1_16);
+            a0 = __dadd_rn(a0, p0); a1 = __dadd_rn(a1, p1);
+            a0 = __dadd_rn(a0, p0_16); a1 = __dadd_rn(a1, p1_16);
+            a0 = __dadd_rn(a0, p0_32); a1 = __dadd_rn(a1, p1_32);
+            a0 = __dadd_rn(a0, p0_48); a1 = __dadd_rn(a1, p1_48);
+        }
+    }
+    for (; e0 < end; e0 += 4) {  // tail: < CH entries, 4 at a time, clamped
+        const int64_t e = min<int64_t>(e0 + g, end - 1);
+        const int nv = (int)min<int64_t>(4, end - e0);
+        const double2 x = X[(int64_t)col[e] * 16 + q];
+        const double vv = val[e];
+        const double p0 = __dmul_rn(vv, x.x), p1 = __dmul_rn(vv, x.y);
+        const double p0_16 = xchg16_even(p0), p1_16 = xchg16_even(p1);
+        const double p0_32 = xchg32_low(p0), p1_32 = xchg32_low(p1);
+        const double p0_48 = xchg32_low(p0_16), p1_48 = xchg32_low(p1_16);
+        a0 = __dadd_rn(a0, p0); a1 = __dadd_rn(a1, p1);
+        if (nv > 1) { a0 = __dadd_rn(a0, p0_16); a1 = __dadd_rn(a1, p1_16); }
+        if (nv > 2) { a0 = __dadd_rn(a0, p0_32); a1 = __dadd_rn(a1, p1_32); }
+        if (nv > 3) { a0 = __dadd_rn(a0, p0_48); a1 = __dadd_rn(a1, p1_48); }
+    }
+    if (g == 0) Y[row * 16 + q] = make_double2(a0, a1);
+    const uint64_t m0 = __ballot(g == 0 && a0 != 0.0), m1 = __ballot(g == 0 && a1 != 0.0);
+    if (lane == 0 && row_nnz) row_nnz[row] = __popcll(m0) + __popcll(m1);
 }
 
 // ---------------------------------------------------------------------------
@@ -463,6 +567,13 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
 }
 
 namespace {
+// Kernel-variant override for A/B timing (BSM_SPMM_VARIANT): 0 default,
+// 1 generic row-wave, 2 k32 unpipelined, 3 k32 pipelined x4, 4 k32 pipelined x8.
+int spmm_variant() {
+    const char* e = getenv("BSM_SPMM_VARIANT");
+    return e ? atoi(e) : 0;
+}
+
 template <typename T>
 int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
                 const T* vals, uint64_t k, const T* x, T* y, int32_t* row_nnz, bool neg_init,
@@ -477,7 +588,24 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
         return BSM_OK;
     }
     BSM_REQUIRE(!neg_init, BSM_ERR_INVALID, "-0 init only for k = 1");
-    BSM_REQUIRE(k < (1ull << 30), BSM_ERR_UNSUPPORTED, "k too large");
+    const int variant = spmm_variant();
+    if constexpr (std::is_same_v<T, double>) {
+        if (k == 32 && variant != 1 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0) {
+            const uint64_t nb = (rows + 3) / 4;
+            BSM_REQUIRE(nb < (1ull << 32), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
+            auto X2 = reinterpret_cast<const double2*>(x);
+            auto Y2 = reinterpret_cast<double2*>(y);
+            const int64_t r = (int64_t)rows;
+            if (variant == 2)
+                spmm_k32_f64<4, false><<<(unsigned)nb, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
+            else if (variant == 4)
+                spmm_k32_f64<8, true><<<(unsigned)nb, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
+            else
+                spmm_k32_f64<4, true><<<(unsigned)nb, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
+            BSM_HIP_TRY(hipGetLastError());
+            return BSM_OK;
+        }
+    }
     const uint64_t blocks = (rows + 3) / 4;
     BSM_REQUIRE(blocks < (1ull << 32), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
     const int ki = (int)k;
