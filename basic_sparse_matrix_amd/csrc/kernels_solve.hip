@@ -59,13 +59,19 @@ __device__ __forceinline__ double pow_half(double x) {
     if (isinf(x) && x < 0) return INFINITY;
     return fabs(__dsqrt_rn(x));
 }
+// f32 sqrt and division are formed in f64 and rounded once to f32: for
+// sqrt and '/', a result correctly rounded to 53 bits and then rounded to 24
+// is the correctly rounded f32 result (53 >= 2*24 + 2), i.e. IEEE f32 exactly
+// as the reference's host computes it, independent of device math flags.
 __device__ __forceinline__ float pow_half(float x) {
     if (isinf(x) && x < 0) return INFINITY;
-    return fabsf(__fsqrt_rn(x));
+    return fabsf(__double2float_rn(__dsqrt_rn((double)x)));
 }
 template <typename T> __device__ __forceinline__ T div_rn(T a, T b);
 template <> __device__ __forceinline__ double div_rn(double a, double b) { return __ddiv_rn(a, b); }
-template <> __device__ __forceinline__ float div_rn(float a, float b) { return __fdiv_rn(a, b); }
+template <> __device__ __forceinline__ float div_rn(float a, float b) {
+    return __double2float_rn(__ddiv_rn((double)a, (double)b));
+}
 
 // ---------------------------------------------------------------------------
 // band construction

@@ -109,12 +109,15 @@ def main():
     from basic_sparse_matrix_amd import _lib
     from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
 
+    from basic_sparse_matrix_amd.distributed import padded_block_rows, partition_rows_even
+
     rows, n_cols, nnz_r, k = CONFIGS[args.config]
     # contiguous row blocks, equal rows (= equal nnz: constant row length);
     # padded to a common size for the equal-count all-gather
-    per = (rows + world - 1) // world
-    row0 = min(rows, rank * per)
-    my_rows = max(0, min(rows, row0 + per) - row0)
+    bounds = partition_rows_even(rows, world)
+    per = padded_block_rows(bounds)
+    row0 = int(bounds[rank])
+    my_rows = int(bounds[rank + 1]) - row0
 
     t0 = time.perf_counter()
     blk = DeviceCsrBlock.generate(SEED_A, row0, my_rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r,
@@ -143,7 +146,7 @@ def main():
         blk.spmm(x, y_local[:my_rows], nnz_local[:my_rows])
         if timed:
             ev_k1.record()
-        if world > 1:
+        if world > 1:  # RCCL all-gather of the dense Y blocks (+ their nnz counts)
             dist.all_gather_into_tensor(y_full, y_local)
             dist.all_gather_into_tensor(nnz_full, nnz_local)
         if timed:
