@@ -30,8 +30,8 @@
 namespace bsm {
 namespace {
 
-constexpr int TR = 32;              // rows per tile-row
-constexpr int CH_THREADS = 1024;    // 16 row pairs x 64 column lanes
+constexpr int TR = 16;              // rows per tile-row
+constexpr int CH_THREADS = 1024;    // 16 rows x 64 column lanes
 constexpr int PUBLISH_EVERY = 8;    // columns between progress publications
 constexpr long long SPIN_LIMIT = 1ll << 25;
 
@@ -108,135 +108,201 @@ __global__ __launch_bounds__(256) void band_fill(const int64_t* __restrict__ rp,
 }
 
 // ---------------------------------------------------------------------------
-// band_chol: see file header. Thread t: row pair rp2 = t >> 6 (rows 2*rp2,
-// 2*rp2+1 of the tile-row), column lane c = t & 63, accumulators for
-// j = jb + c + 64 m, m < M.
+// band_chol: see file header. 1024 threads:
+//   every thread: row r = t >> 6 of the tile-row, column lane c = t & 63,
+//     accumulators for j = jb + c + 64 m (m < M);
+//   all threads: prefetch, CH_PF columns ahead, the column values
+//     L[k+d][k] of the rows above the tile-row (into colL), the 16 A values
+//     A[i][k] of the tile-row and the pivot L[k][k] (into LDS double
+//     buffers), plus the predecessor's progress counter, so neither a data
+//     load nor a flag poll sits on a step's critical path. Every thread
+//     issues exactly four unconditional (clamped) loads per step, so the
+//     compiler can count its s_waitcnt vmcnt(N) across the ring;
+//   wave 0, lanes 0..15: store the tile-row's column k after each step.
+//     Its VMEM stream per step is 4 loads then 1 store, so "the store of
+//     step k - CH_PUB is done" is s_waitcnt vmcnt(5 * CH_PUB) -- a delayed
+//     publication that never waits on a fresh load or store.
+// A tile-row needs column k of the rows above it (tile-rows < I): it waits
+// on tile-row I-1's progress counter (columns done), published every
+// CH_PUB columns by wave 0 with the write-through (sc1) hand-off of
+// MI355X_MICROARCH.md "Valid forms", row 1.
 // ---------------------------------------------------------------------------
+constexpr int CH_PF = 4;   // prefetch distance (columns)
+constexpr int CH_PUB = 4;  // publication period (columns); lag = CH_PF + CH_PUB
+
 template <typename T, int M>
 __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                          int* __restrict__ progress, int* __restrict__ status,
                                                          int64_t n_tiles) {
     using A = Arith<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    T* colL = reinterpret_cast<T*>(smem_raw);  // [b + 1]: L[k + d][k]
-    __shared__ T rowval[TR];                   // L[i][k] of the 32 rows at this step
+    T* colL = reinterpret_cast<T*>(smem_raw);  // [b + 1]: L[k + d][k] of column k
+    __shared__ T rowval[TR];                   // L[i][k] of the tile-row's rows at this step
+    __shared__ T aval[2][TR];                  // A[i][k] of those rows (double buffer by k & 1)
+    __shared__ T pval[2];                      // L[k][k] for k < i0 (double buffer)
     __shared__ T s_pivot;
     const int tid = threadIdx.x;
-    const int rp2 = tid >> 6, c = tid & 63;
+    const int r = tid >> 6, c = tid & 63;
+    const int pf = tid;  // prefetch lane
+    constexpr int PFN = CH_THREADS;
     for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
         const int64_t i0 = I * TR;
-        const int64_t iA = i0 + 2 * rp2;  // this thread: rows iA, iA + 1
+        const int64_t i = i0 + r;  // this thread's row
         const int64_t jb = i0 - b > 0 ? i0 - b : 0;
         const int64_t kend = i0 + TR < n ? i0 + TR : n;
-        T acc[2][M];
+        T acc[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) { acc[0][m] = A::zero(); acc[1][m] = A::zero(); }
-        int64_t seen = -1;  // thread 0: last observed progress of tile-row I-1
-        T pre = A::zero();  // prefetched L[k + 1 + tid][k]
-        bool have_pre = false;
-        for (int64_t k = jb; k < kend; ++k) {
-            // (a) column k (and k+1, for the prefetch) of the rows above must be final
-            if (tid == 0 && I > 0) {
-                const int64_t need = (k + 2 < i0 ? k + 2 : i0);  // progress counts columns done
-                long long spins = 0;
-                while (seen < need) {
-                    seen = __hip_atomic_load(&progress[I - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (seen >= need) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > SPIN_LIMIT ||
-                        ((spins & 1023) == 0 &&
-                         (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
-                        atomicOr(status, ST_TIMEOUT);
-                        seen = INT32_MAX;
-                        break;
-                    }
+        for (int m = 0; m < M; ++m) acc[m] = A::zero();
+        int64_t seen = -1;  // last progress of tile-row I-1 this thread observed
+        // prefetch ring: every thread issues exactly three
+        // UNCONDITIONAL loads per column (clamped, always in-bounds addresses)
+        // so the compiler's s_waitcnt before a ring slot is used can count
+        // (a conditional load makes it fall back to vmcnt(0)): two column
+        // values L[kc+d][kc] and one "extra": A[i0+pf][kc] for pf < TR, the
+        // pivot L[kc][kc] for pf == TR, a dummy otherwise. Validity is decided
+        // when a slot is staged into LDS.
+        T pc0[CH_PF], pc1[CH_PF], px[CH_PF];
+        int pp[CH_PF];  // progress[I-1] as loaded CH_PF steps earlier
+#pragma unroll
+        for (int q = 0; q < CH_PF; ++q) { pc0[q] = A::zero(); pc1[q] = A::zero(); px[q] = A::zero(); pp[q] = -1; }
+        int* prev_progress = &progress[I > 0 ? I - 1 : 0];
+        // blocking poll (rare: the prefetched counter normally suffices)
+        auto wait_progress = [&](int64_t need) {
+            long long spins = 0;
+            while (seen < need) {
+                seen = __hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen >= need) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT ||
+                    ((spins & 1023) == 0 &&
+                     (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
+                    atomicOr(status, ST_TIMEOUT);
+                    seen = INT32_MAX;
+                    break;
                 }
             }
-            __syncthreads();  // B1: colL / rowval of step k-1 are no longer read
-            const int64_t kk = k - jb;
-            const int mk = (int)(kk >> 6), ck = (int)(kk & 63);
-            // (b) finalise column k. Diagonal first when row k is ours.
-            T piv;
-            if (k >= i0) {
-                if ((k - i0) >> 1 == rp2 && c == ck) {
-                    const int w = (int)((k - i0) & 1);
-                    T s = A::zero();
-#pragma unroll
-                    for (int m = 0; m < M; ++m) if (m == mk) s = acc[w][m];
-                    const T a = CB[k * ld];
-                    const T l = pow_half(A::sub(a, s));
-                    if (!(l > A::zero()) || isinf(l)) atomicOr(status, ST_NOT_PD);
-                    st_sc1(&CB[k * ld], l);
-                    s_pivot = l;
-                }
-                __syncthreads();
-                piv = s_pivot;
-            } else {
-                piv = (c == ck) ? ld_sc1(&CB[k * ld]) : A::zero();
+        };
+        const int64_t last = n * ld - 1;  // clamp target
+        auto clampi = [&](int64_t x) { return x < 0 ? 0 : (x > last ? last : x); };
+        auto issue = [&](int q, int64_t kc) {
+            const int64_t base = kc * ld;
+            const int64_t d0 = 1 + pf, d1 = 1 + pf + PFN;
+            pc0[q] = ld_sc1(&CB[clampi(base + d0)]);
+            pc1[q] = ld_sc1(&CB[clampi(base + d1)]);
+            const int64_t xo = pf < TR ? base + (i0 + pf - kc) : (pf == TR ? base : base + d0);
+            px[q] = ld_sc1(&CB[clampi(xo)]);
+            pp[q] = __hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        auto stage_cols = [&](int q, int64_t kc) {
+            const int64_t d0 = 1 + pf, d1 = 1 + pf + PFN;
+            const int64_t dmax = (i0 - 1 - kc < b) ? i0 - 1 - kc : b;  // rows kc+1 .. i0-1 above us
+            if (d0 <= dmax) colL[d0] = pc0[q];
+            if (d1 <= dmax) colL[d1] = pc1[q];
+        };
+        auto stage_ap = [&](int q, int64_t kc) {
+            if (pf < TR) {
+                const int64_t ia = i0 + pf;
+                aval[kc & 1][pf] = (ia < n && ia >= kc && ia - kc <= b) ? px[q] : A::zero();
+            } else if (pf == TR) {
+                pval[kc & 1] = kc < i0 ? px[q] : A::zero();
             }
-            if (c == ck) {
+        };
+        // prologue: columns jb .. jb+CH_PF-1 must be final above us
+        if (I > 0) wait_progress(jb + CH_PF < i0 ? jb + CH_PF : i0);
+        __syncthreads();
 #pragma unroll
-                for (int w = 0; w < 2; ++w) {
-                    const int64_t i = iA + w;
-                    T lik = A::zero();
-                    if (i < n && i >= k && i - k <= b) {
-                        if (i == k) {
-                            lik = piv;
-                        } else {
-                            T s = A::zero();
+        for (int q = 0; q < CH_PF; ++q) issue(q, jb + q);
+        stage_ap(0, jb);
+        __syncthreads();
+        // The k loop is unrolled by CH_PF so every ring slot index is a
+        // compile-time constant (a register ring that is shifted instead
+        // would force a wait on every in-flight load), and the unrolled body
+        // runs unconditionally -- up to CH_PF-1 idle steps past kend, which
+        // do nothing -- so the compiler can count its s_waitcnt vmcnt(N).
+        for (int64_t k0 = jb; k0 < kend; k0 += CH_PF) {
 #pragma unroll
-                            for (int m = 0; m < M; ++m) if (m == mk) s = acc[w][m];
-                            const T a = CB[k * ld + (i - k)];
-                            const T one = (T)1;
-                            lik = A::mul(div_rn(one, piv), A::sub(a, s));
-                            st_sc1(&CB[k * ld + (i - k)], lik);
+            for (int q = 0; q < CH_PF; ++q) {
+                const int64_t k = k0 + q;
+                {
+                    const int64_t kk = k - jb;
+                    const int mk = (int)(kk >> 6), ck = (int)(kk & 63);
+                    // (b) finalise column k (diagonal first when row k is ours)
+                    T piv;
+                    if (k >= i0) {
+                        if (i == k && i < n && c == ck) {
+                            T sacc = A::zero();
+#pragma unroll
+                            for (int m = 0; m < M; ++m) if (m == mk) sacc = acc[m];
+                            const T l = pow_half(A::sub(aval[k & 1][r], sacc));
+                            if (!(l > A::zero()) || isinf(l)) atomicOr(status, ST_NOT_PD);
+                            s_pivot = l;
                         }
-                        if (i > k) colL[i - k] = lik;
+                        __syncthreads();
+                        piv = s_pivot;
+                    } else {
+                        piv = pval[k & 1];
                     }
-                    rowval[2 * rp2 + w] = lik;
-                }
-            }
-            // (c) column k of the rows above this tile-row (prefetched last step)
-            if (have_pre) colL[1 + tid] = pre;
-            {
-                const int64_t dmax = (i0 - 1 - k < b) ? i0 - 1 - k : b;  // rows k+1 .. i0-1
-                for (int64_t d = 1 + tid + CH_THREADS; d <= dmax; d += CH_THREADS) colL[d] = ld_sc1(&CB[k * ld + d]);
-                if (!have_pre && 1 + tid <= dmax) colL[1 + tid] = ld_sc1(&CB[k * ld + 1 + tid]);
-            }
-            __syncthreads();  // B2
-            // prefetch column k+1 for the next step (rows above the tile-row)
-            {
-                const int64_t k1 = k + 1;
-                const int64_t dmax1 = (i0 - 1 - k1 < b) ? i0 - 1 - k1 : b;
-                have_pre = (k1 < kend) && (1 + tid <= dmax1);
-                if (have_pre) pre = ld_sc1(&CB[k1 * ld + 1 + tid]);
-            }
-            // (d) right-looking update of this thread's accumulators
-            const T l0 = rowval[2 * rp2], l1 = rowval[2 * rp2 + 1];
-            {
-                // 32-bit relative indices: d = j - k, j = jb + c + 64 m
-                const int dbase = (int)(jb - k) + c;
-                const int dA = (int)(iA - k), dB = dA + 1, bb = (int)b;
+                    if (c == ck) {
+                        T lik = A::zero();
+                        if (i < n && i >= k && i - k <= b) {
+                            if (i == k) {
+                                lik = piv;
+                            } else {
+                                T sacc = A::zero();
 #pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    const int d = dbase + 64 * m;
-                    if (d >= 1 && d <= bb) {
-                        const T ljk = colL[d];
-                        if (d <= dA) acc[0][m] = A::add(acc[0][m], A::mul(l0, ljk));
-                        if (d <= dB) acc[1][m] = A::add(acc[1][m], A::mul(l1, ljk));
+                                for (int m = 0; m < M; ++m) if (m == mk) sacc = acc[m];
+                                lik = A::mul(div_rn((T)1, piv), A::sub(aval[k & 1][r], sacc));
+                                colL[i - k] = lik;
+                            }
+                        }
+                        rowval[r] = lik;
                     }
+                    // (c) prefetch waves: stage column k from ring slot q; make
+                    // sure column k + CH_PF is final above us before reloading q
+                    stage_cols(q, k);
+                    if (I > 0) {
+                        const int64_t need = (k + CH_PF + 1 < i0) ? k + CH_PF + 1 : i0;
+                        if (pp[q] > seen) seen = pp[q];
+                        if (seen < need) wait_progress(need);
+                    }
+                    __syncthreads();  // B: column k staged; rowval final; slot q free
+                    issue(q, k + CH_PF);
+                    stage_ap((q + 1) % CH_PF, k + 1);
+                    // (e) wave 0 stores column k of the tile-row; delayed publication
+                    if (tid < 64) {
+                        if (tid < TR) {
+                            const int64_t is = i0 + tid;
+                            if (is < n && is >= k && is - k <= b) st_sc1(&CB[k * ld + (is - k)], rowval[tid]);
+                        }
+                        if (k + 1 == kend) {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            if (tid == 0)
+                                __hip_atomic_store(&progress[I], (int)kend, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        } else if (k + 1 < kend && (kk + 1) % CH_PUB == 0 && kk + 1 > CH_PUB) {
+                            // wave 0 issues 4 loads + 1 store per step: all but the
+                            // 5*CH_PUB youngest ops done => stores of columns <= k - CH_PUB done
+                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * CH_PUB) : "memory");
+                            if (tid == 0)
+                                __hip_atomic_store(&progress[I], (int)(k + 1 - CH_PUB), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    // (d) right-looking update of this thread's accumulators
+                    const T lk = rowval[r];
+                    if (lk != A::zero()) {
+                        const int dbase = (int)(jb - k) + c;
+                        const int di = (int)(i - k), bb = (int)b;
+#pragma unroll
+                        for (int m = 0; m < M; ++m) {
+                            const int d = dbase + 64 * m;
+                            if (d >= 1 && d <= bb && d <= di) acc[m] = A::add(acc[m], A::mul(lk, colL[d]));
+                        }
+                    }
+                    __syncthreads();  // colL / rowval / aval[k & 1] are reused at step k + 1
                 }
-            }
-            // (e) publish progress: all stores of columns <= k drained first
-            if ((kk + 1) % PUBLISH_EVERY == 0 || k + 1 == kend) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0)
-                    __hip_atomic_store(&progress[I], (int)(k + 1 == kend ? kend : k + 1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -244,10 +310,13 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
 // forward substitution on the band (lib.rs:28-46): y_i = (b_i - sum_{j<i}
 // L_ij y_j) / L_ii, sum in ascending j. One workgroup per RHS column; blocks
 // of 256 rows: the "far" terms (j < block start) are summed first, one thread
-// per row, then the in-block terms column by column. y lives in an LDS ring.
+// per row (loads batched ahead of the dependent adds), then the in-block
+// terms column by column with the band values prefetched FW_PF steps ahead
+// and one barrier per step (double-buffered y). y lives in an LDS ring.
 // ---------------------------------------------------------------------------
 constexpr int FW_BLOCK = 256;
 constexpr int FW_RING = 2048;  // >= b + FW_BLOCK
+constexpr int FW_PF = 16;
 
 template <typename T>
 __global__ __launch_bounds__(FW_BLOCK) void band_forward(int64_t n, int64_t b, int64_t ld,
@@ -255,65 +324,122 @@ __global__ __launch_bounds__(FW_BLOCK) void band_forward(int64_t n, int64_t b, i
                                                          T* __restrict__ Y) {
     using A = Arith<T>;
     __shared__ T ring[FW_RING];
-    __shared__ T s_y;
+    __shared__ T s_y[2];
     const int t = threadIdx.x;
     const T* bc = B + (int64_t)blockIdx.x * n;
     T* yc = Y + (int64_t)blockIdx.x * n;
     for (int64_t i0 = 0; i0 < n; i0 += FW_BLOCK) {
         const int64_t i = i0 + t;
+        const bool valid = i < n;
+        const T bi = valid ? bc[i] : A::zero();
+        const T lii = valid ? CB[i * ld] : A::zero();
         T s = A::zero();
         const int64_t j0 = (i - b > 0) ? i - b : 0;
-        if (i < n)
-            for (int64_t j = j0; j < i0; ++j) s = A::add(s, A::mul(CB[j * ld + (i - j)], ring[j & (FW_RING - 1)]));
-        const int64_t nb = (n - i0 < FW_BLOCK) ? n - i0 : FW_BLOCK;
-        for (int64_t tt = 0; tt < nb; ++tt) {
-            const int64_t j = i0 + tt;
-            if (t == tt) {
-                const T y = div_rn(A::sub(bc[i], s), CB[i * ld]);
-                ring[i & (FW_RING - 1)] = y;
-                s_y = y;
-                yc[i] = y;
+        if (valid) {
+            int64_t j = j0;
+            for (; j + 16 <= i0; j += 16) {
+                T lv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) lv[u] = CB[(j + u) * ld + (i - j - u)];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s = A::add(s, A::mul(lv[u], ring[(j + u) & (FW_RING - 1)]));
             }
-            __syncthreads();
-            if (i < n && i > j && i - j <= b) s = A::add(s, A::mul(CB[j * ld + (i - j)], s_y));
-            __syncthreads();
+            for (; j < i0; ++j) s = A::add(s, A::mul(CB[j * ld + (i - j)], ring[j & (FW_RING - 1)]));
         }
+        const int64_t nb = (n - i0 < FW_BLOCK) ? n - i0 : FW_BLOCK;
+        // near-part band values L[i][i0 + tt] for tt = 0.. (prefetch ring of
+        // unconditional loads from clamped addresses; validity checked at use)
+        const int64_t last = n * ld - 1;
+        auto lnear = [&](int64_t tt) -> T {
+            const int64_t j = i0 + tt;
+            int64_t a = j * ld + (i - j);
+            a = a < 0 ? 0 : (a > last ? last : a);
+            return CB[a];
+        };
+        auto near_ok = [&](int64_t tt) { const int64_t j = i0 + tt; return valid && i > j && i - j <= b; };
+        T pre[FW_PF];
+#pragma unroll
+        for (int q = 0; q < FW_PF; ++q) pre[q] = lnear(q);
+        for (int64_t tt0 = 0; tt0 < nb; tt0 += FW_PF) {
+#pragma unroll
+            for (int q = 0; q < FW_PF; ++q) {
+                const int64_t tt = tt0 + q;  // runs past nb: idle steps
+                if (t == tt && valid) {
+                    const T y = div_rn(A::sub(bi, s), lii);
+                    ring[i & (FW_RING - 1)] = y;
+                    s_y[tt & 1] = y;
+                    yc[i] = y;
+                }
+                __syncthreads();
+                const T lij = pre[q];
+                pre[q] = lnear(tt + FW_PF);
+                if (tt < nb && t > tt && near_ok(tt)) s = A::add(s, A::mul(lij, s_y[tt & 1]));
+            }
+        }
+        __syncthreads();
     }
 }
 
 // ---------------------------------------------------------------------------
 // backward substitution on the band (lib.rs:49-65) with L* = L^T: x_i =
-// (y_i - sum_{j>i} L_ji x_j) / L_ii, sum in ascending j. The ascending order
-// makes each row's sum start with the most recent x, so the solve is one
-// serial chain; one wavefront per RHS column: lanes form the products, lane
-// 0 adds them in order.
+// (y_i - sum_{j>i} L_ji x_j) / L_ii, sum in ascending j. Ascending order makes
+// each row's sum START with the newest x, so the solve is one serial chain of
+// N*b dependent adds. Two wavefronts: wave 1 forms row i-1's products for
+// j >= i+1 (and stages L_ii, L_{i,i-1}... inputs) while lane 0 of wave 0 runs
+// row i's chain; one barrier per row.
 // ---------------------------------------------------------------------------
 constexpr int BW_RING = 2048;
 
 template <typename T>
-__global__ __launch_bounds__(64) void band_backward(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
-                                                    const T* __restrict__ Yin, T* __restrict__ X) {
+__global__ __launch_bounds__(128) void band_backward(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                     const T* __restrict__ Yin, T* __restrict__ X) {
     using A = Arith<T>;
     __shared__ T ring[BW_RING];
-    __shared__ T prod[BW_RING];
-    const int lane = threadIdx.x;
+    __shared__ T prod[2][BW_RING];  // prod[r & 1][d] = L[r+d][r] * x[r+d], d >= 2
+    __shared__ T meta[2][3];        // {L[r][r], L[r+1][r], y[r]} for row r (by r & 1)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool producer = tid >= 64;
     const T* yc = Yin + (int64_t)blockIdx.x * n;
     T* xc = X + (int64_t)blockIdx.x * n;
-    for (int64_t i = n - 1; i >= 0; --i) {
-        const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
-        const T* colI = CB + i * ld;
-        for (int64_t d = 1 + lane; d <= dmax; d += 64) prod[d] = A::mul(colI[d], ring[(i + d) & (BW_RING - 1)]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    // producer work for row r: products d >= 2 and the row's scalars
+    auto produce = [&](int64_t r) {
+        if (r < 0) return;
+        const int64_t dmax = (n - 1 - r < b) ? n - 1 - r : b;
+        const T* col = CB + r * ld;
+        for (int64_t d = 2 + lane; d <= dmax; d += 64)
+            prod[r & 1][d] = A::mul(col[d], ring[(r + d) & (BW_RING - 1)]);
         if (lane == 0) {
+            meta[r & 1][0] = col[0];
+            meta[r & 1][1] = dmax >= 1 ? col[1] : A::zero();
+            meta[r & 1][2] = yc[r];
+        }
+    };
+    if (producer) produce(n - 1);
+    __syncthreads();
+    T x_next = A::zero();  // wave 0 lane 0: x[i + 1]
+    for (int64_t i = n - 1; i >= 0; --i) {
+        if (producer) {
+            produce(i - 1);  // needs x[i+1..]: final before this iteration
+        } else if (lane == 0) {
+            const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
             T s = A::zero();
-            for (int64_t d = 1; d <= dmax; ++d) s = A::add(s, prod[d]);
-            const T x = div_rn(A::sub(yc[i], s), colI[0]);
+            if (dmax >= 1) s = A::add(s, A::mul(meta[i & 1][1], x_next));
+            const T* p = prod[i & 1];
+            int64_t d = 2;
+            for (; d + 8 <= dmax + 1; d += 8) {
+                T v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = p[d + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s = A::add(s, v[u]);
+            }
+            for (; d <= dmax; ++d) s = A::add(s, p[d]);
+            const T x = div_rn(A::sub(meta[i & 1][2], s), meta[i & 1][0]);
             ring[i & (BW_RING - 1)] = x;
             xc[i] = x;
+            x_next = x;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
     }
 }
 
