@@ -24,6 +24,8 @@
 // is published every few columns (write-through sc1 stores + counter, the
 // hand-off of MI355X_MICROARCH.md "Valid forms", table row 1).
 #include <cmath>
+#include <cstdlib>
+#include <vector>
 
 #include "bsm_internal.hpp"
 
@@ -32,7 +34,6 @@ namespace {
 
 constexpr int TR = 16;              // rows per tile-row
 constexpr int CH_THREADS = 1024;    // 16 rows x 64 column lanes
-constexpr int PUBLISH_EVERY = 8;    // columns between progress publications
 constexpr long long SPIN_LIMIT = 1ll << 25;
 
 enum { ST_NOT_PD = 1, ST_TIMEOUT = 2, ST_EMPTY_ROW = 4 };
@@ -130,10 +131,12 @@ __global__ __launch_bounds__(256) void band_fill(const int64_t* __restrict__ rp,
 constexpr int CH_PF = 4;   // prefetch distance (columns)
 constexpr int CH_PUB = 4;  // publication period (columns); lag = CH_PF + CH_PUB
 
+constexpr int TRACE_TILES = 4096;  // diagnostic trace (BSM_CHOL_TRACE=1): first tile-rows
+
 template <typename T, int M>
 __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                          int* __restrict__ progress, int* __restrict__ status,
-                                                         int64_t n_tiles) {
+                                                         int64_t n_tiles, unsigned long long* __restrict__ trace) {
     using A = Arith<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* colL = reinterpret_cast<T*>(smem_raw);  // [b + 1]: L[k + d][k] of column k
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
         // blocking poll (rare: the prefetched counter normally suffices)
         auto wait_progress = [&](int64_t need) {
             long long spins = 0;
+            if (trace && tid == 0 && seen < need) atomicAdd(&trace[3 * TRACE_TILES], 1ull);
             while (seen < need) {
                 seen = __hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (seen >= need) break;
@@ -181,6 +185,7 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
                     break;
                 }
             }
+            if (trace && tid == 0 && spins) atomicAdd(&trace[3 * TRACE_TILES + 1], (unsigned long long)spins);
         };
         const int64_t last = n * ld - 1;  // clamp target
         auto clampi = [&](int64_t x) { return x < 0 ? 0 : (x > last ? last : x); };
@@ -207,9 +212,11 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
                 pval[kc & 1] = kc < i0 ? px[q] : A::zero();
             }
         };
+        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I] = wall_clock64();
         // prologue: columns jb .. jb+CH_PF-1 must be final above us
         if (I > 0) wait_progress(jb + CH_PF < i0 ? jb + CH_PF : i0);
         __syncthreads();
+        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 1] = wall_clock64();
 #pragma unroll
         for (int q = 0; q < CH_PF; ++q) issue(q, jb + q);
         stage_ap(0, jb);
@@ -303,6 +310,7 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
                 }
             }
         }
+        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 2] = wall_clock64();
     }
 }
 
@@ -585,7 +593,7 @@ int band_analyse(const bsm_csr* a, hipStream_t s, int64_t* bw_out, bool* sorted,
 }
 
 template <typename T, int M>
-int launch_chol(Band& bd, int* progress, int* status, hipStream_t s) {
+int launch_chol(Band& bd, int* progress, int* status, hipStream_t s, unsigned long long* trace) {
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
     const size_t shm = (size_t)(bd.b + 1) * sizeof(T);
     int dev = 0, cus = 0;
@@ -599,7 +607,7 @@ int launch_chol(Band& bd, int* progress, int* status, hipStream_t s) {
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol<T, M><<<(unsigned)grid, CH_THREADS, shm, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), progress, status,
-                                                             n_tiles);
+                                                             n_tiles, trace);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -628,13 +636,43 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     BSM_TRY(prog.alloc((n_tiles + 1) * sizeof(int) + 16));
     BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, (n_tiles + 1) * sizeof(int) + 16, s));
     int* status = prog.as<int>() + n_tiles;
+    // optional diagnostic trace: per-tile-row clocks + blocking-poll counts
+    DBuf trace_buf;
+    const bool tracing = getenv("BSM_CHOL_TRACE") != nullptr;
+    if (tracing) {
+        BSM_TRY(trace_buf.alloc((3 * TRACE_TILES + 2) * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(trace_buf.p, 0, (3 * TRACE_TILES + 2) * sizeof(unsigned long long), s));
+    }
+    unsigned long long* tr = tracing ? trace_buf.as<unsigned long long>() : nullptr;
     int rc;
-    if (need <= 64) rc = launch_chol<T, 1>(bd, prog.as<int>(), status, s);
-    else if (need <= 128) rc = launch_chol<T, 2>(bd, prog.as<int>(), status, s);
-    else if (need <= 256) rc = launch_chol<T, 4>(bd, prog.as<int>(), status, s);
-    else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s);
-    else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s);
+    if (need <= 64) rc = launch_chol<T, 1>(bd, prog.as<int>(), status, s, tr);
+    else if (need <= 128) rc = launch_chol<T, 2>(bd, prog.as<int>(), status, s, tr);
+    else if (need <= 256) rc = launch_chol<T, 4>(bd, prog.as<int>(), status, s, tr);
+    else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s, tr);
+    else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s, tr);
     BSM_TRY(rc);
+    if (tracing) {
+        std::vector<unsigned long long> h(3 * TRACE_TILES + 2);
+        BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        const int64_t nt = n_tiles < TRACE_TILES ? n_tiles : TRACE_TILES;
+        double dur = 0, pro = 0, gap = 0;
+        int64_t cnt = 0;
+        for (int64_t I = 1; I < nt; ++I) {
+            if (!h[3 * I] || !h[3 * I + 2]) continue;
+            dur += (double)(h[3 * I + 2] - h[3 * I + 1]);
+            pro += (double)(h[3 * I + 1] - h[3 * I]);
+            gap += (double)(h[3 * I + 1]) - (double)(h[3 * (I - 1) + 1]);
+            ++cnt;
+        }
+        const double us = 0.01;  // wall_clock64 ticks at 100 MHz
+        const double steps = (double)(bd.b + TR);
+        fprintf(stderr,
+                "[bsm chol trace] tile-rows %lld (traced %lld): run %.1f us (%.3f us/step), prologue wait %.1f us, "
+                "start-to-start %.2f us (= %.1f steps); blocking polls %llu, spins %llu\n",
+                (long long)n_tiles, (long long)cnt, dur / cnt * us, dur / cnt * us / steps, pro / cnt * us,
+                gap / cnt * us, gap / cnt / (dur / cnt / steps), h[3 * TRACE_TILES], h[3 * TRACE_TILES + 1]);
+    }
     int st = 0;
     BSM_HIP_TRY(hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
@@ -781,7 +819,7 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
             band_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), bc.as<T>(),
                                                              yc.as<T>());
             BSM_HIP_TRY(hipGetLastError());
-            band_backward<T><<<(unsigned)k, 64, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(),
+            band_backward<T><<<(unsigned)k, 128, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(),
                                                         xc.as<T>());
             BSM_HIP_TRY(hipGetLastError());
         }

@@ -193,7 +193,14 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             log("timing cpu baseline ...")
             cpu = cpu_baseline(args.config, args.cpu_sample_rows)
-        traffic = args.traffic_bytes
+        traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
+        pmc_json = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+        if traffic is None and world == 1 and os.path.exists(pmc_json):
+            # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this kernel on
+            # this config (separate runs), corrected per MI355X_MICROARCH.md
+            with open(pmc_json) as f:
+                pmc = json.load(f)
+            traffic, traffic_src = pmc["traffic_bytes_per_launch"], os.path.relpath(pmc_json, ROOT)
         line = {
             "metric": "CSR x dense SpMM effective GB/s (B_alg / step time); nnz/s",
             "value": round(value, 2),
@@ -227,12 +234,14 @@ def main():
             "output_nnz": out_nnz,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "spmm_rowwave<double,32,8>",
+                "kernel": "spmm_k32_f64<4,true>" if k == 32 else ("spmv_stream<double>" if k == 1 else "spmm_rowwave<double>"),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "traffic_GBps": round(traffic / (float(np.mean(kern_ms)) / 1e3) / 1e9, 1) if traffic else None,
                 "bytes_per_launch_alg": b_launch,
             },
             "cpu_baseline": cpu,
