@@ -94,6 +94,11 @@ SIGNATURES = [
     ("bsm_dev_gen_dense", _int, [_int, _u64, _u64, _u64, _u64, _int, _vp, _vp]),
     ("bsm_dev_scan_workspace_bytes", _u64, [_u64]),
     ("bsm_dev_spmm", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp]),
+    ("bsm_csr_panel_cols", _int, [_vp, _u64p]),
+    ("bsm_dev_spmm_panel_cols", _u64, [_int, _u64, _u64]),
+    ("bsm_dev_spmm_plan_bytes", _u64, [_u64, _u64, _u64]),
+    ("bsm_dev_spmm_plan", _int, [_u64, _u64, _vp, _vp, _u64, _vp, ctypes.POINTER(_int), _vp]),
+    ("bsm_dev_spmm_panelled", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
     ("bsm_dev_compact", _int, [_int, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
 ]
 
@@ -190,6 +195,12 @@ class DeviceCsr:
         v = np.empty(self.nnz, dtype=self.dtype)
         check(lib.bsm_csr_download(self.handle, ptr(rp), ptr(ci), ptr(v)))
         return rp, ci, v
+
+    def plan_width(self) -> int:
+        """Column-panel width mul_dense uses on this handle (0 = one pass)."""
+        w = _u64()
+        check(load().bsm_csr_panel_cols(self.handle, ctypes.byref(w)))
+        return w.value
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -156,6 +156,10 @@ struct bsm_csr {
     bool analysed = false;
     bool rows_sorted = true;  // col non-decreasing inside every row
     uint64_t max_row_len = 0;
+    // cached column-panel plan of mul_dense (spmm_plan), keyed by panel width
+    mutable int32_t* plan_seg = nullptr;
+    mutable uint64_t plan_cols = 0;
+    mutable bool plan_usable = false;
 };
 
 namespace bsm {
@@ -169,6 +173,13 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
 int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
                   int32_t* row_nnz, bool neg_zero_init, hipStream_t s);
+uint64_t spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k);  // 0 = single pass
+uint64_t spmm_plan_bytes(uint64_t rows, uint64_t n_cols, uint64_t panel_cols);
+int spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* rp, const int32_t* col,
+              uint64_t panel_cols, int32_t* seg, int* usable, hipStream_t s);  // synchronous
+int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
+                  const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
+                  int32_t* row_nnz, uint64_t panel_cols, const int32_t* seg, hipStream_t s);
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
                      int32_t* out_col, void* out_vals, hipStream_t s);
 int pack_cols_to_rowmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor, void* rowmajor,

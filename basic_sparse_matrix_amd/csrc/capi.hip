@@ -146,8 +146,26 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     if (k == 0) {
         BSM_HIP_TRY(hipMemsetAsync(row_nnz.p, 0, rows * sizeof(int32_t), s));
     } else {
-        BSM_TRY(spmm_dispatch(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
-                              y.p, row_nnz.as<int32_t>(), false, s));
+        const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
+        if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
+            if (a->plan_seg) (void)hipFree(a->plan_seg);
+            a->plan_seg = nullptr;
+            a->plan_cols = 0;
+            DBuf seg;
+            BSM_TRY(seg.alloc(spmm_plan_bytes(rows, a->cols, w)));
+            int usable = 0;
+            BSM_TRY(spmm_plan(rows, a->cols, a->row_ptr, a->col, w, seg.as<int32_t>(), &usable, s));
+            a->plan_seg = seg.as<int32_t>();
+            seg.release();
+            a->plan_cols = w;
+            a->plan_usable = usable != 0;
+        }
+        if (w && a->plan_usable)
+            BSM_TRY(spmm_panelled(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
+                                  y.p, row_nnz.as<int32_t>(), w, a->plan_seg, s));
+        else
+            BSM_TRY(spmm_dispatch(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
+                                  y.p, row_nnz.as<int32_t>(), false, s));
     }
     BSM_TRY(exclusive_scan_i32_to_i64(row_nnz.as<int32_t>(), out_rp.as<int64_t>(), rows, ws.p,
                                       ws.bytes, s));
@@ -297,6 +315,7 @@ void bsm_csr_free(bsm_csr* m) {
     if (m->row_ptr) (void)hipFree(m->row_ptr);
     if (m->col) (void)hipFree(m->col);
     if (m->vals) (void)hipFree(m->vals);
+    if (m->plan_seg) (void)hipFree(m->plan_seg);
     delete m;
 }
 
@@ -444,6 +463,39 @@ int bsm_dev_spmm(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     if (k == 0) return BSM_OK;
     return spmm_dispatch(dtype, rows, n_cols, nnz, row_ptr, col, vals, k, x, y, row_nnz, false,
                          static_cast<hipStream_t>(stream));
+}
+
+int bsm_csr_panel_cols(const bsm_csr* m, uint64_t* panel_cols) {
+    BSM_REQUIRE(m && panel_cols, BSM_ERR_INVALID, "null argument");
+    *panel_cols = m->plan_usable ? m->plan_cols : 0;
+    return BSM_OK;
+}
+
+uint64_t bsm_dev_spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k) {
+    return spmm_panel_cols(dtype, n_cols, k);
+}
+
+uint64_t bsm_dev_spmm_plan_bytes(uint64_t rows, uint64_t n_cols, uint64_t panel_cols) {
+    return spmm_plan_bytes(rows, n_cols, panel_cols);
+}
+
+int bsm_dev_spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* row_ptr, const int32_t* col,
+                      uint64_t panel_cols, int32_t* seg, int* usable, void* stream) {
+    BSM_REQUIRE(row_ptr && usable && (spmm_plan_bytes(rows, n_cols, panel_cols) == 0 || seg),
+                BSM_ERR_INVALID, "null argument");
+    return spmm_plan(rows, n_cols, row_ptr, col, panel_cols, seg, usable,
+                     static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz,
+                          const int64_t* row_ptr, const int32_t* col, const void* vals, uint64_t k,
+                          const void* x, void* y, int32_t* row_nnz, uint64_t panel_cols,
+                          const int32_t* seg, void* stream) {
+    BSM_REQUIRE(row_ptr && (nnz == 0 || (col && vals)) && (k == 0 || (x && y)), BSM_ERR_INVALID,
+                "null argument");
+    if (k == 0) return BSM_OK;
+    return spmm_panelled(dtype, rows, n_cols, nnz, row_ptr, col, vals, k, x, y, row_nnz, panel_cols,
+                         seg, static_cast<hipStream_t>(stream));
 }
 
 int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y, const int32_t* row_nnz,

@@ -205,21 +205,38 @@ __device__ __forceinline__ double xchg32_low(double v) {
     return from_u2(rl[1], rh[1]);
 }
 
-template <int STEPS, bool PIPE>
+//
+// PANEL = one pass of the column-panel schedule (spmm_panelled below): the
+// row's entries are cut at panel boundaries, seg_lo/seg_hi give the pass's
+// entry range relative to the row start (nullptr = row start / row end) and a
+// pass other than the first resumes the running sums from Y. Carrying the
+// f64 sum through Y is exact, so the per-element order is unchanged.
+template <int STEPS, bool PIPE, bool PANEL = false>
 __global__ __launch_bounds__(256) void spmm_k32_f64(int64_t rows, const int64_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const double* __restrict__ val,
                                                     const double2* __restrict__ X,
                                                     double2* __restrict__ Y,
-                                                    int32_t* __restrict__ row_nnz) {
+                                                    int32_t* __restrict__ row_nnz,
+                                                    const int32_t* __restrict__ seg_lo = nullptr,
+                                                    const int32_t* __restrict__ seg_hi = nullptr) {
     constexpr int CH = 4 * STEPS;  // entries per iteration
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
     if (row >= rows) return;
     const int g = lane >> 4, q = lane & 15;
-    const int64_t start = rp[row], end = rp[row + 1];
+    int64_t start = rp[row], end = rp[row + 1];
     double a0 = 0.0, a1 = 0.0;
+    if constexpr (PANEL) {
+        if (seg_hi) end = start + seg_hi[row];
+        if (seg_lo) {
+            start += seg_lo[row];
+            const double2 y0 = Y[row * 16 + q];
+            a0 = y0.x;
+            a1 = y0.y;
+        }
+    }
     int64_t e0 = start;
     // each lane loads the index/value of ITS entry (4 distinct addresses per
     // wave instruction, one cache line)
@@ -277,6 +294,38 @@ __global__ __launch_bounds__(256) void spmm_k32_f64(int64_t rows, const int64_t*
     if (g == 0) Y[row * 16 + q] = make_double2(a0, a1);
     const uint64_t m0 = __ballot(g == 0 && a0 != 0.0), m1 = __ballot(g == 0 && a1 != 0.0);
     if (lane == 0 && row_nnz) row_nnz[row] = __popcll(m0) + __popcll(m1);
+}
+
+// Column-panel plan: seg[(p-1)*rows + r] = offset (from the row start) of
+// the first entry of row r whose column lies in panel p = col / panel_cols,
+// for p = 1 .. n_panels-1. One wavefront per row; lane e finds the panels
+// that start at its entry. *bad |= 1 if a row's panels are not
+// non-decreasing in storage order (the schedule would reorder its sum),
+// |= 2 if a row is longer than int32.
+__global__ __launch_bounds__(256) void spmm_plan_panels(int64_t rows, const int64_t* __restrict__ rp,
+                                                        const int32_t* __restrict__ col,
+                                                        uint32_t panel_cols, int n_panels,
+                                                        int32_t* __restrict__ seg,
+                                                        unsigned* __restrict__ bad) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    if (row >= rows) return;
+    const int64_t start = rp[row], end = rp[row + 1];
+    if (end - start > INT32_MAX) {
+        if (lane == 0) atomicOr(bad, 2u);
+        return;
+    }
+    const int last = n_panels - 1;
+    for (int64_t e = start + lane; e < end; e += WAVE) {
+        const int pe = (int)min<uint32_t>((uint32_t)col[e] / panel_cols, (uint32_t)last);
+        const int pp = e > start ? (int)min<uint32_t>((uint32_t)col[e - 1] / panel_cols, (uint32_t)last) : 0;
+        if (pe < pp) atomicOr(bad, 1u);
+        for (int p = pp + 1; p <= pe; ++p) seg[(int64_t)(p - 1) * rows + row] = (int32_t)(e - start);
+    }
+    if (lane == 0) {  // panels after the row's last entry (all of them for an empty row)
+        const int pl = end > start ? (int)min<uint32_t>((uint32_t)col[end - 1] / panel_cols, (uint32_t)last) : 0;
+        for (int p = pl + 1; p <= last; ++p) seg[(int64_t)(p - 1) * rows + row] = (int32_t)(end - start);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -630,6 +679,83 @@ int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const
                               static_cast<const T*>(x), static_cast<T*>(y), row_nnz,
                               neg_zero_init, s);
     });
+}
+
+// ---------------------------------------------------------------------------
+// Column-panel schedule for large X (DESIGN.md "SpMM: column panels"). With
+// uniformly random columns every CSR entry gathers a whole X row and X
+// (C4: 2.56 GB) is far larger than the 256 MiB Infinity Cache, so gathers
+// are served by HBM. Cutting the columns into panels whose slice of X fits
+// the Infinity Cache and sweeping the rows once per panel serves the gathers
+// on-die; the running sums travel through Y between passes (exact).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint64_t PANEL_X_BYTES = 512ull << 20;      // X slice per pass (C4: 5 passes)
+constexpr uint64_t PANEL_MIN_X_BYTES = 1ull << 30;    // below: one pass
+}  // namespace
+
+uint64_t spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k) {
+    if (dtype != BSM_F64 || k != 32 || n_cols == 0) return 0;  // panelled kernel: k32 f64 only
+    uint64_t w;
+    if (const char* e = getenv("BSM_SPMM_PANEL_COLS")) {  // A/B and tests; 0 = off
+        w = strtoull(e, nullptr, 10);
+    } else {
+        const uint64_t x_bytes = n_cols * k * sizeof(double);
+        if (x_bytes <= PANEL_MIN_X_BYTES) return 0;
+        const uint64_t passes = (x_bytes + PANEL_X_BYTES - 1) / PANEL_X_BYTES;
+        w = (n_cols + passes - 1) / passes;
+    }
+    return (w == 0 || w >= n_cols || w > UINT32_MAX) ? 0 : w;
+}
+
+uint64_t spmm_plan_bytes(uint64_t rows, uint64_t n_cols, uint64_t panel_cols) {
+    if (panel_cols == 0 || panel_cols >= n_cols) return 0;
+    const uint64_t passes = (n_cols + panel_cols - 1) / panel_cols;
+    return (passes - 1) * rows * sizeof(int32_t);
+}
+
+int spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* rp, const int32_t* col,
+              uint64_t panel_cols, int32_t* seg, int* usable, hipStream_t s) {
+    *usable = 0;
+    if (panel_cols == 0 || panel_cols >= n_cols) return BSM_OK;
+    const uint64_t passes = (n_cols + panel_cols - 1) / panel_cols;
+    BSM_REQUIRE(passes < (1u << 20) && panel_cols <= UINT32_MAX, BSM_ERR_UNSUPPORTED, "too many panels");
+    DBuf flag;
+    BSM_TRY(flag.alloc(sizeof(unsigned)));
+    BSM_HIP_TRY(hipMemsetAsync(flag.p, 0, sizeof(unsigned), s));
+    if (rows) {
+        spmm_plan_panels<<<grid1d(rows, 4), 256, 0, s>>>((int64_t)rows, rp, col, (uint32_t)panel_cols,
+                                                          (int)passes, seg, flag.as<unsigned>());
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    unsigned bad = 0;
+    BSM_HIP_TRY(hipMemcpyAsync(&bad, flag.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    *usable = bad == 0;
+    return BSM_OK;
+}
+
+int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
+                  const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
+                  int32_t* row_nnz, uint64_t panel_cols, const int32_t* seg, hipStream_t s) {
+    const bool aligned = ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0;
+    if (!seg || panel_cols == 0 || panel_cols >= n_cols || dtype != BSM_F64 || k != 32 || !aligned ||
+        rows == 0)
+        return spmm_dispatch(dtype, rows, n_cols, nnz, rp, col, vals, k, x, y, row_nnz, false, s);
+    const uint64_t passes = (n_cols + panel_cols - 1) / panel_cols;
+    const uint64_t nb = (rows + 3) / 4;
+    BSM_REQUIRE(nb < (1ull << 32), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
+    auto X2 = static_cast<const double2*>(x);
+    auto Y2 = static_cast<double2*>(y);
+    auto V = static_cast<const double*>(vals);
+    for (uint64_t p = 0; p < passes; ++p) {
+        const int32_t* lo = p ? seg + (p - 1) * rows : nullptr;
+        const int32_t* hi = p + 1 < passes ? seg + p * rows : nullptr;
+        spmm_k32_f64<4, true, true><<<(unsigned)nb, 256, 0, s>>>((int64_t)rows, rp, col, V, X2, Y2,
+                                                                 p + 1 < passes ? nullptr : row_nnz, lo, hi);
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    return BSM_OK;
 }
 
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,

@@ -9,6 +9,7 @@ kernels of libbsm_hip.so.
 
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -47,6 +48,8 @@ class DeviceCsrBlock:
     col: torch.Tensor  # int32 [nnz]
     vals: torch.Tensor  # T [nnz]
     dtype: np.dtype
+    panel_cols: int = 0  # column-panel plan (bsm_dev_spmm_plan), 0 = none
+    seg: torch.Tensor | None = None
 
     @property
     def nnz(self) -> int:
@@ -70,10 +73,35 @@ class DeviceCsrBlock:
                                            _p(col), _p(vals), s))
         return cls(row0, rows, n_cols, rp, col, vals, dt)
 
+    def plan(self, k: int, panel_cols: int | None = None) -> int:
+        """Build the column-panel plan for k right-hand columns (synchronous,
+        once per matrix). Returns the panel width in use (0 = single pass)."""
+        lib = _lib.require_device()
+        w = lib.bsm_dev_spmm_panel_cols(_lib.DTYPE_CODES[self.dtype], self.n_cols, k) if panel_cols is None \
+            else panel_cols
+        self.panel_cols, self.seg = 0, None
+        nbytes = lib.bsm_dev_spmm_plan_bytes(self.rows, self.n_cols, w)
+        if w == 0 or nbytes == 0:
+            return 0
+        seg = torch.empty(nbytes // 4, dtype=torch.int32, device=self.col.device)
+        usable = ctypes.c_int(0)
+        _lib.check(lib.bsm_dev_spmm_plan(self.rows, self.n_cols, _p(self.row_ptr), _p(self.col), w, _p(seg),
+                                         ctypes.byref(usable), _stream()))
+        if usable.value:
+            self.panel_cols, self.seg = w, seg
+        return self.panel_cols
+
     def spmm(self, x: torch.Tensor, y: torch.Tensor, row_nnz: torch.Tensor | None = None, stream=None) -> None:
-        """Y = A X (x: n_cols x k row-major, y: rows x k row-major), async."""
+        """Y = A X (x: n_cols x k row-major, y: rows x k row-major), async.
+        Uses the column-panel plan when one was built (same bits)."""
         lib = _lib.load()
         k = x.shape[1] if x.dim() == 2 else 1
+        if self.seg is not None:
+            _lib.check(lib.bsm_dev_spmm_panelled(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz,
+                                                 _p(self.row_ptr), _p(self.col), _p(self.vals), k, _p(x), _p(y),
+                                                 _p(row_nnz) if row_nnz is not None else 0, self.panel_cols,
+                                                 _p(self.seg), _stream(stream)))
+            return
         _lib.check(lib.bsm_dev_spmm(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz, _p(self.row_ptr),
                                     _p(self.col), _p(self.vals), k, _p(x), _p(y),
                                     _p(row_nnz) if row_nnz is not None else 0, _stream(stream)))

@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=5000)
+    ap.add_argument("--panel-cols", type=int, default=None,
+                    help="column-panel width of the SpMM schedule (default: the library's choice; 0 = one pass)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
     args = ap.parse_args()
@@ -133,6 +135,14 @@ def main():
     comp = Compactor(rows, k, np.float64, device=dev)
     torch.cuda.synchronize()
     log(f"rank {rank}: rows [{row0},{row0 + my_rows}) nnz {blk.nnz:,} generated in {time.perf_counter() - t0:.1f} s")
+    # column-panel plan: built once per matrix (like the matrix itself, outside
+    # the timed region; its cost is reported as plan_ms)
+    t0 = time.perf_counter()
+    panel_cols = blk.plan(k, args.panel_cols)
+    torch.cuda.synchronize()
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    n_passes = -(-n_cols // panel_cols) if panel_cols else 1
+    log(f"rank {rank}: panel width {panel_cols} ({n_passes} passes), plan {plan_ms:.1f} ms")
 
     ev_k0 = torch.cuda.Event(enable_timing=True)
     ev_k1 = torch.cuda.Event(enable_timing=True)
@@ -184,8 +194,9 @@ def main():
     nnz_total = rows * nnz_r
     ms_per_step = elapsed / args.steps * 1e3
     value = b_alg(rows, n_cols, nnz_total, k) / (elapsed / args.steps) / 1e9
-    # roofline of the dominant kernel (spmm_rowwave): per-launch algorithmic
-    # bytes of THIS rank's launch over its measured average duration
+    # roofline of the dominant kernel (the SpMM: n_passes launches of the
+    # panelled kernel, bracketed together by the HIP events): algorithmic
+    # bytes of THIS rank's SpMM over its measured average duration
     b_launch = b_alg(my_rows, n_cols, blk.nnz, k)
     achieved = b_launch / (float(np.mean(kern_ms)) / 1e3) / 1e9
     if rank == 0:
@@ -200,7 +211,9 @@ def main():
             # this config (separate runs), corrected per MI355X_MICROARCH.md
             with open(pmc_json) as f:
                 pmc = json.load(f)
-            traffic, traffic_src = pmc["traffic_bytes_per_launch"], os.path.relpath(pmc_json, ROOT)
+            if pmc.get("panel_cols", 0) == panel_cols:  # same schedule as this run
+                traffic = pmc["traffic_bytes_per_launch"] * pmc.get("launches_per_spmm", 1)
+                traffic_src = os.path.relpath(pmc_json, ROOT)
         line = {
             "metric": "CSR x dense SpMM effective GB/s (B_alg / step time); nnz/s",
             "value": round(value, 2),
@@ -222,6 +235,7 @@ def main():
                             f"to Csr",
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
                 "parallelism": f"row-block x{world}" + (" + all-gather" if world > 1 else ""),
+                "panel_cols": panel_cols, "passes": n_passes, "plan_ms": round(plan_ms, 1),
             },
             "nnz_per_s": round(nnz_total / (elapsed / args.steps), 1),
             "hbm_frac_of_peak": round(value / (world * HBM_PEAK_GBS), 5),
@@ -234,7 +248,9 @@ def main():
             "output_nnz": out_nnz,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "spmm_k32_f64<4,true>" if k == 32 else ("spmv_stream<double>" if k == 1 else "spmm_rowwave<double>"),
+                "kernel": (f"spmm_k32_f64<4,true,{'true' if panel_cols else 'false'}>" if k == 32
+                           else ("spmv_stream<double>" if k == 1 else "spmm_rowwave<double>")),
+                "launches_per_spmm": n_passes,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -139,6 +139,25 @@ uint64_t bsm_dev_scan_workspace_bytes(uint64_t n);
 int bsm_dev_spmm(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz,
                  const int64_t* row_ptr, const int32_t* col, const void* vals, uint64_t k,
                  const void* x, void* y, int32_t* row_nnz, void* stream);
+/* Width of the column-panel plan bsm_csr_mul_dense has cached for this
+ * handle and uses (0 = one pass); diagnostic (see bsm_dev_spmm_plan). */
+int bsm_csr_panel_cols(const bsm_csr* m, uint64_t* panel_cols);
+/* Column-panel schedule of bsm_dev_spmm for an X larger than the 256 MiB
+ * Infinity Cache (DESIGN.md "SpMM: column panels"); same results, bit for
+ * bit. bsm_dev_spmm_panel_cols gives the panel width for (dtype, n_cols, k)
+ * (0 = one pass is best: the schedule is used for f64, k = 32, X > 1 GiB;
+ * env BSM_SPMM_PANEL_COLS overrides). bsm_dev_spmm_plan fills seg
+ * (bsm_dev_spmm_plan_bytes bytes) once per matrix, synchronously, and sets
+ * *usable = 0 when some row's columns do not visit the panels in order (then
+ * call bsm_dev_spmm). bsm_dev_spmm_panelled = bsm_dev_spmm with the plan. */
+uint64_t bsm_dev_spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k);
+uint64_t bsm_dev_spmm_plan_bytes(uint64_t rows, uint64_t n_cols, uint64_t panel_cols);
+int bsm_dev_spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* row_ptr, const int32_t* col,
+                      uint64_t panel_cols, int32_t* seg, int* usable, void* stream);
+int bsm_dev_spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz,
+                          const int64_t* row_ptr, const int32_t* col, const void* vals, uint64_t k,
+                          const void* x, void* y, int32_t* row_nnz, uint64_t panel_cols,
+                          const int32_t* seg, void* stream);
 /* Compaction of a dense result into the reference's output Csr (insert's
  * zero skip, sparse.rs:229): out_row_ptr (rows+1), out_col/out_vals with
  * capacity rows*k. */

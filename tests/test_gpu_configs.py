@@ -98,3 +98,8 @@ def test_c4_shape_sampled_rows(orc):
     n = comp.nnz()
     assert n == rows * k  # positive inputs: nothing is dropped
     assert np.array_equal(comp.vals[:n].cpu().numpy().view(np.uint64), ev.view(np.uint64))
+    # the column-panel schedule bench.py uses at C4 (default width) gives the same bits
+    assert blk.plan(k) == 2_000_000
+    y2, comp2 = _run_spmm(blk, x, k)
+    assert torch.equal(y2.view(torch.int64), y.view(torch.int64))
+    assert torch.equal(comp2.row_ptr, comp.row_ptr)

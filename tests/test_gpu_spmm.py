@@ -112,6 +112,39 @@ def test_mul_dense_random_parity(orc, dtype, k):
     assert_csr_bits(got, *oracle_mul_dense(orc, a, x_cols))
 
 
+@pytest.mark.parametrize("panel", [1, 37, 350, 699])
+def test_mul_dense_panelled_parity(orc, monkeypatch, panel):
+    """Column-panel schedule (k = 32, f64), forced at a small size through
+    BSM_SPMM_PANEL_COLS: rows cut into one slice per panel, sums carried
+    through Y between passes, same bits as the oracle. Empty rows, rows
+    inside one panel and rows spanning every panel included."""
+    monkeypatch.setenv("BSM_SPMM_PANEL_COLS", str(panel))
+    rows, n_cols, k = 1500, 700, 32
+    rp, ci, v = orc.gen_csr(70 + panel, rows, n_cols, kind=orc.ROWLEN_UNIFORM, a=0, b=90)
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    x_cols = orc.gen_x_cols(71, n_cols, k, value_kind=orc.VAL_SMALLINT)  # exact zeros too
+    got = a.mul_dense(Dense.from_columns(x_cols))
+    assert_csr_bits(got, *oracle_mul_dense(orc, a, x_cols))
+    assert a._device().plan_width() == panel
+
+
+def test_mul_dense_panel_plan_rejects_unsorted_rows(orc, monkeypatch):
+    """A row whose columns go back to an earlier panel would be summed out of
+    storage order by the panel schedule: the plan is refused and the one-pass
+    kernel runs (still bit-exact)."""
+    monkeypatch.setenv("BSM_SPMM_PANEL_COLS", "100")
+    rows, n_cols, k = 300, 400, 32
+    rp, ci, v = orc.gen_csr(5, rows, n_cols, kind=orc.ROWLEN_UNIFORM, a=1, b=30)
+    ci = ci.copy()
+    lo, hi = int(rp[7]), int(rp[8])
+    ci[lo:hi] = ci[lo:hi][::-1].copy()  # row 7 descending
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    x_cols = orc.gen_x_cols(6, n_cols, k)
+    got = a.mul_dense(Dense.from_columns(x_cols))
+    assert_csr_bits(got, *oracle_mul_dense(orc, a, x_cols))
+    assert a._device().plan_width() == 0
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.int64])
 def test_mul_dense_exact_cancellations(orc, dtype):
     """Small-integer values and an X with ~1/7 zeros: exact sums that hit 0
