@@ -33,6 +33,26 @@ __device__ __forceinline__ int64_t lower_bound_rp(const int64_t* rp, int64_t n, 
     return lo;
 }
 
+// The same, searched by a whole wavefront: 64 probes per step, so
+// ceil(log64 n) dependent loads instead of log2 n. Call from all 64 lanes;
+// the result is the same in every lane.
+__device__ __forceinline__ int64_t wave_lower_bound_rp(const int64_t* rp, int64_t n, int64_t v) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    int64_t lo = 0, hi = n;  // answer in [lo, hi]
+    while (lo < hi) {
+        const int64_t step = (hi - lo + WAVE - 1) / WAVE;
+        const int64_t pos = lo + (int64_t)lane * step;
+        const bool ge = pos >= hi || rp[pos] >= v;
+        const uint64_t m = __ballot(ge);
+        const int f = m ? __builtin_ctzll(m) : WAVE;  // first probe at or past the answer
+        if (f == 0) break;                             // rp[lo] >= v
+        const int64_t nlo = lo + (int64_t)(f - 1) * step + 1;
+        hi = min<int64_t>(hi, lo + (int64_t)f * step);
+        lo = nlo;
+    }
+    return lo;
+}
+
 // ---------------------------------------------------------------------------
 // Exclusive scan int32 -> int64 (n+1 outputs; out[n] = total).
 // Three launches: per-tile sums, scan of tile sums (one workgroup), apply.
@@ -296,6 +316,59 @@ __global__ __launch_bounds__(256) void spmm_k32_f64(int64_t rows, const int64_t*
     if (lane == 0 && row_nnz) row_nnz[row] = __popcll(m0) + __popcll(m1);
 }
 
+// k = 32, f64, SHORT rows (C3: 10 entries): four CSR rows per wavefront, one
+// per 16-lane group. Lane q of group g owns Y[row][2q..2q+1] and walks its
+// row's entries in storage order (sequential sums, no cross-lane combine);
+// a wave instruction still gathers four whole 256-B X rows, one per group.
+// U entries per group are in flight per iteration (clamped, unconditional
+// loads); the wave runs to the longest of its four rows.
+template <int U>
+__global__ __launch_bounds__(256) void spmm_k32_f64_rows4(int64_t rows, const int64_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ col,
+                                                          const double* __restrict__ val,
+                                                          const double2* __restrict__ X,
+                                                          double2* __restrict__ Y,
+                                                          int32_t* __restrict__ row_nnz) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int g = lane >> 4, q = lane & 15;
+    const int64_t row = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) * 4 + g;
+    const bool live = row < rows;
+    int64_t start = 0, len = 0;
+    if (live) {
+        start = rp[row];
+        len = rp[row + 1] - start;
+    }
+    long long m = len;  // longest row of the wave
+    m = max(m, (long long)__shfl_xor(m, 16));
+    m = max(m, (long long)__shfl_xor(m, 32));
+    double a0 = 0.0, a1 = 0.0;
+    for (int64_t b = 0; b < m; b += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = len ? start + min<int64_t>(b + u, len - 1) : 0;  // nnz > 0 here
+            c[u] = col[e];
+            v[u] = val[e];
+        }
+        double2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = X[(int64_t)c[u] * 16 + q];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double s0 = __dadd_rn(a0, __dmul_rn(v[u], x[u].x));
+            const double s1 = __dadd_rn(a1, __dmul_rn(v[u], x[u].y));
+            const bool in = b + u < len;
+            a0 = in ? s0 : a0;
+            a1 = in ? s1 : a1;
+        }
+    }
+    if (live) Y[row * 16 + q] = make_double2(a0, a1);
+    const uint64_t m0 = __ballot(live && a0 != 0.0), m1 = __ballot(live && a1 != 0.0);
+    if (q == 0 && live && row_nnz)
+        row_nnz[row] = __popcll((m0 >> (16 * g)) & 0xffffull) + __popcll((m1 >> (16 * g)) & 0xffffull);
+}
+
 // Column-panel plan: seg[(p-1)*rows + r] = offset (from the row start) of
 // the first entry of row r whose column lies in panel p = col / panel_cols,
 // for p = 1 .. n_panels-1. One wavefront per row; lane e finds the panels
@@ -337,10 +410,7 @@ __global__ __launch_bounds__(256) void spmm_plan_panels(int64_t rows, const int6
 // thread-per-row sums for short rows and a workgroup-wide pass per long row.
 // init = +0 for mul_dense (T::default()), -0 for mul_vector (float Sum).
 // ---------------------------------------------------------------------------
-constexpr int SPMV_CHUNK = 1024;
-constexpr int SPMV_CAP = 2048;
-
-template <typename T>
+template <typename T, int ITEMS>
 __global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
                                                    const int64_t* __restrict__ rp,
                                                    const int32_t* __restrict__ col,
@@ -348,27 +418,56 @@ __global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
                                                    const T* __restrict__ x, T* __restrict__ y,
                                                    int32_t* __restrict__ row_nnz, bool neg_init) {
     using A = Arith<T>;
-    __shared__ T prod[SPMV_CAP];
+    constexpr int CHUNK = 256 * ITEMS, CAP = 2 * CHUNK;
+    __shared__ T prod[CAP];
     __shared__ int64_t s_r[2];
-    const int64_t lo = (int64_t)blockIdx.x * SPMV_CHUNK;
-    const int64_t hi = lo + SPMV_CHUNK;
-    if (threadIdx.x == 0) {
-        s_r[0] = lower_bound_rp(rp, rows, lo);
-        s_r[1] = hi > nnz ? rows : lower_bound_rp(rp, rows, hi);
+    const int64_t lo = (int64_t)blockIdx.x * CHUNK;
+    const int64_t hi = lo + CHUNK;
+    const int wave = threadIdx.x / WAVE;  // waves 0 and 1 find the two row bounds
+    if (wave == 0) {
+        const int64_t r = wave_lower_bound_rp(rp, rows, lo);
+        if (threadIdx.x == 0) s_r[0] = r;
+    } else if (wave == 1) {
+        const int64_t r = hi > nnz ? rows : wave_lower_bound_rp(rp, rows, hi);
+        if (threadIdx.x == WAVE) s_r[1] = r;
     }
     __syncthreads();
     const int64_t r0 = s_r[0], r1 = s_r[1];
     if (r0 >= r1) return;
     const T init = neg_init ? A::neg_zero() : A::zero();
     const int64_t e0 = rp[r0], e1 = rp[r1];
-    if (e1 - e0 <= SPMV_CAP) {
-        for (int64_t i = threadIdx.x; i < e1 - e0; i += blockDim.x) {
-            const int64_t e = e0 + i;
-            prod[i] = A::mul(val[e], x[col[e]]);
+    const int64_t n = e1 - e0;
+    if (n <= CAP) {
+        // this thread's first row bounds, in flight with the products
+        const int64_t rr = r0 + threadIdx.x;
+        int64_t ra = 0, rb = 0;
+        if (rr < r1) {
+            ra = rp[rr];
+            rb = rp[rr + 1];
+        }
+        // products: ITEMS coalesced col/val loads per thread issued together,
+        // then ITEMS gathers (clamped indices, unconditional loads)
+        for (int64_t base = 0; base < n; base += CHUNK) {
+            int32_t c[ITEMS];
+            T v[ITEMS];
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                const int64_t e = e0 + min<int64_t>(base + it * 256 + threadIdx.x, n - 1);
+                c[it] = col[e];
+                v[it] = val[e];
+            }
+            T xv[ITEMS];
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) xv[it] = x[c[it]];
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                const int64_t i = base + it * 256 + threadIdx.x;
+                if (i < n) prod[i] = A::mul(v[it], xv[it]);
+            }
         }
         __syncthreads();
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-            const int64_t a = rp[r] - e0, b = rp[r + 1] - e0;
+        for (int64_t r = rr; r < r1; r += blockDim.x) {
+            const int64_t a = (r == rr ? ra : rp[r]) - e0, b = (r == rr ? rb : rp[r + 1]) - e0;
             T acc = init;
             for (int64_t i = a; i < b; ++i) acc = A::add(acc, prod[i]);
             y[r] = acc;
@@ -376,10 +475,10 @@ __global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
         }
         return;
     }
-    // fallback: block contains a row longer than SPMV_CHUNK
+    // fallback: block contains a row longer than CHUNK
     for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
         const int64_t a = rp[r], b = rp[r + 1];
-        if (b - a > SPMV_CHUNK) continue;
+        if (b - a > CHUNK) continue;
         T acc = init;
         for (int64_t e = a; e < b; ++e) acc = A::add(acc, A::mul(val[e], x[col[e]]));
         y[r] = acc;
@@ -387,10 +486,10 @@ __global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
     }
     for (int64_t r = r0; r < r1; ++r) {  // uniform loop over long rows
         const int64_t a = rp[r], b = rp[r + 1];
-        if (b - a <= SPMV_CHUNK) continue;
+        if (b - a <= CHUNK) continue;
         T acc = init;
-        for (int64_t cs = a; cs < b; cs += SPMV_CAP) {
-            const int64_t n = min<int64_t>(SPMV_CAP, b - cs);
+        for (int64_t cs = a; cs < b; cs += CAP) {
+            const int64_t n = min<int64_t>(CAP, b - cs);
             __syncthreads();
             for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
                 const int64_t e = cs + i;
@@ -617,7 +716,15 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
 
 namespace {
 // Kernel-variant override for A/B timing (BSM_SPMM_VARIANT): 0 default,
-// 1 generic row-wave, 2 k32 unpipelined, 3 k32 pipelined x4, 4 k32 pipelined x8.
+// 1 generic row-wave, 2 k32 unpipelined, 3 k32 pipelined x4, 4 k32 pipelined x8,
+// 5 k32 four rows per wave (U = 4), 6 the same with U = 2.
+// entries per thread of spmv_stream (BSM_SPMV_ITEMS = 2, 4 or 8 for A/B)
+int spmv_items() {
+    const char* e = getenv("BSM_SPMV_ITEMS");
+    const int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 8) ? v : 4;
+}
+constexpr uint64_t SHORT_ROW_AVG = 24;  // nnz/rows at or below: four rows per wave
 int spmm_variant() {
     const char* e = getenv("BSM_SPMM_VARIANT");
     return e ? atoi(e) : 0;
@@ -629,10 +736,16 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
                 hipStream_t s) {
     if (rows == 0) return BSM_OK;
     if (k == 1) {
-        const uint64_t blocks = nnz / SPMV_CHUNK + 1;
+        const int items = spmv_items();
+        const uint64_t blocks = nnz / (256ull * items) + 1;
         BSM_REQUIRE(blocks < (1ull << 31), BSM_ERR_UNSUPPORTED, "nnz too large for one launch");
-        spmv_stream<T><<<(unsigned)blocks, 256, 0, s>>>((int64_t)rows, (int64_t)nnz, rp, col, vals,
-                                                        x, y, row_nnz, neg_init);
+        const int64_t r = (int64_t)rows, z = (int64_t)nnz;
+        if (items == 2)
+            spmv_stream<T, 2><<<(unsigned)blocks, 256, 0, s>>>(r, z, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (items == 8)
+            spmv_stream<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, z, rp, col, vals, x, y, row_nnz, neg_init);
+        else
+            spmv_stream<T, 4><<<(unsigned)blocks, 256, 0, s>>>(r, z, rp, col, vals, x, y, row_nnz, neg_init);
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     }
@@ -645,6 +758,17 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
             auto X2 = reinterpret_cast<const double2*>(x);
             auto Y2 = reinterpret_cast<double2*>(y);
             const int64_t r = (int64_t)rows;
+            // short rows on average: four rows per wave (variants 5/6 force it)
+            const bool short_rows = nnz <= SHORT_ROW_AVG * rows;
+            if (variant == 5 || variant == 6 || (variant == 0 && short_rows)) {
+                const uint64_t nb4 = (rows + 15) / 16;
+                if (variant == 6)
+                    spmm_k32_f64_rows4<2><<<(unsigned)nb4, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
+                else
+                    spmm_k32_f64_rows4<4><<<(unsigned)nb4, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
+                BSM_HIP_TRY(hipGetLastError());
+                return BSM_OK;
+            }
             if (variant == 2)
                 spmm_k32_f64<4, false><<<(unsigned)nb, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
             else if (variant == 4)

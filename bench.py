@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--cpu-sample-rows", type=int, default=5000)
     ap.add_argument("--panel-cols", type=int, default=None,
                     help="column-panel width of the SpMM schedule (default: the library's choice; 0 = one pass)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
     args = ap.parse_args()
@@ -103,10 +106,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; ranks beyond the visible GPUs share them (rehearsals)
+    ordinal = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(ordinal)
+    dev = torch.device("cuda", ordinal)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from basic_sparse_matrix_amd import _lib
     from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
@@ -190,6 +198,21 @@ def main():
     else:
         kmax = float(np.mean(kern_ms))
 
+    verified = None
+    if args.verify:
+        if rank == 0:  # the whole product on one GPU, compared with the assembled one
+            full = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r,
+                                           _lib.VAL_UNIFORM, np.float64, device=dev)
+            full.plan(k, args.panel_cols)
+            y_ref = torch.empty((rows, k), dtype=torch.float64, device=dev)
+            nnz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
+            full.spmm(x, y_ref, nnz_ref)
+            verified = bool(torch.equal(y_ref.view(torch.int64), y_full[:rows].reshape(rows, k).view(torch.int64))
+                            and torch.equal(nnz_ref, nnz_full[:rows]))
+            del full, y_ref, nnz_ref
+            log(f"verify: assembled Y {'==' if verified else '!='} single-GPU Y")
+        if world > 1:
+            dist.barrier()
     out_nnz = comp.nnz()
     nnz_total = rows * nnz_r
     ms_per_step = elapsed / args.steps * 1e3
@@ -246,6 +269,7 @@ def main():
                 "compaction_mean": round(float(np.mean(comp_ms)), 3),
             },
             "output_nnz": out_nnz,
+            "verified_vs_single_gpu": verified,
             "roofline": {
                 "bound": "hbm",
                 "kernel": (f"spmm_k32_f64<4,true,{'true' if panel_cols else 'false'}>" if k == 32

@@ -21,6 +21,7 @@ ap.add_argument("--nnz-row", type=int, default=1000)
 ap.add_argument("--k", type=int, default=32)
 ap.add_argument("--variants", default="1,2,3,4")
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--env", default="BSM_SPMM_VARIANT", help="environment variable the variants set")
 args = ap.parse_args()
 
 blk = DeviceCsrBlock.generate(1000, 0, args.rows, args.cols, _lib.ROWLEN_CONST, args.nnz_row, args.nnz_row)
@@ -34,7 +35,7 @@ for v in variants:
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(args.rounds + 1):
     for v in variants:
-        os.environ["BSM_SPMM_VARIANT"] = str(v)
+        os.environ[args.env] = str(v)
         e0.record()
         blk.spmm(x, ys[v])
         e1.record()

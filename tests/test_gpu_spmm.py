@@ -112,6 +112,22 @@ def test_mul_dense_random_parity(orc, dtype, k):
     assert_csr_bits(got, *oracle_mul_dense(orc, a, x_cols))
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+def test_mul_dense_k32_kernel_variants(orc, monkeypatch, variant):
+    """Every k = 32 f64 kernel (BSM_SPMM_VARIANT: row-wave, one row per wave
+    unpipelined / x4 / x8, four rows per wave U = 4 / 2) on ragged rows with
+    empty and long ones: all bit-exact."""
+    monkeypatch.setenv("BSM_SPMM_VARIANT", str(variant))
+    rows, n_cols, k = 901, 3000, 32
+    lens = np.array([(r * 37) % 23 if r % 50 else 700 + r for r in range(rows)], dtype=np.uint64)
+    lens[::7] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ci, vals = orc.gen_entries(8, rp, n_cols)
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, vals)
+    x_cols = orc.gen_x_cols(9, n_cols, k, value_kind=orc.VAL_SMALLINT)
+    assert_csr_bits(a.mul_dense(Dense.from_columns(x_cols)), *oracle_mul_dense(orc, a, x_cols))
+
+
 @pytest.mark.parametrize("panel", [1, 37, 350, 699])
 def test_mul_dense_panelled_parity(orc, monkeypatch, panel):
     """Column-panel schedule (k = 32, f64), forced at a small size through
@@ -161,9 +177,11 @@ def test_mul_dense_exact_cancellations(orc, dtype):
     assert_csr_bits(got, erp, eci, ev)
 
 
-@pytest.mark.parametrize("k", [1, 3, 32])
-def test_long_rows_and_empty_rows(orc, k):
-    """Rows longer than the SpMV LDS chunk (1024/2048), mixed with empty rows."""
+@pytest.mark.parametrize("k,items", [(1, 2), (1, 4), (1, 8), (3, 4), (32, 4)])
+def test_long_rows_and_empty_rows(orc, monkeypatch, k, items):
+    """Rows longer than the SpMV LDS chunk (256*items entries, twice that in
+    LDS), mixed with empty rows."""
+    monkeypatch.setenv("BSM_SPMV_ITEMS", str(items))
     rows, n_cols = 40, 6000
     lens = np.array([0, 5000, 0, 3, 2100, 1, 0, 1025] + [7] * 32, dtype=np.uint64)
     rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
@@ -248,11 +266,14 @@ def test_mul_vector_random(orc, dtype):
     rp, ci, v = orc.gen_csr(21, rows, n_cols, kind=orc.ROWLEN_UNIFORM, a=0, b=30, value_kind=vk, dtype=dt)
     a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
     x = orc.gen_x_cols(22, n_cols, 1, value_kind=vk, dtype=dt)[0]
-    out = np.zeros(rows, dtype=dt)
-    a.mul_vector(x, out)
     exp = orc.mul_vector(rows, n_cols, rp, ci, v, x)
     ib = {8: np.uint64, 4: np.uint32}[dt.itemsize]
-    assert np.array_equal(out.view(ib), exp.view(ib))  # includes -0.0 of empty rows
+    for items in ("2", "4", "8"):  # SpMV chunk sizes
+        with pytest.MonkeyPatch.context() as mp:
+            mp.setenv("BSM_SPMV_ITEMS", items)
+            out = np.zeros(rows, dtype=dt)
+            a.mul_vector(x, out)
+        assert np.array_equal(out.view(ib), exp.view(ib))  # includes -0.0 of empty rows
 
 
 def test_mul_vector_unsorted_duplicates(orc):
