@@ -452,6 +452,89 @@ __global__ __launch_bounds__(128) void band_backward(int64_t n, int64_t b, int64
 }
 
 // ---------------------------------------------------------------------------
+// band_backward_hop: the same solve with the chain kept in registers. One
+// wavefront per RHS column. Row i's terms m = 1..dmax are split into 64
+// segments of SEG consecutive terms; lane l holds the products of segment l
+// in registers, and the running sum walks the lanes: lane l adds its SEG
+// products in order, then the sum moves to lane l+1 through an SGPR
+// (v_readlane). A dependent f64 add costs 8 cycles on gfx950, the same add
+// fed from LDS 13-19 (scripts/micro/*chain*), so the chain pays ~8 cycles
+// per term plus one lane hop per SEG terms. Per row, before the chain:
+// products from the x ring in LDS and the L column prefetched two rows
+// ahead. Padding terms are +0: the sum starts at +0 and can never become
+// -0, so adding +0 leaves it unchanged (bit-exact).
+// ---------------------------------------------------------------------------
+constexpr int BH_RING = 4096;  // x ring (power of two > b)
+
+__device__ __forceinline__ double readlane_t(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float readlane_t(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+template <typename T, int SEG>
+__global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                        const T* __restrict__ Yin, T* __restrict__ X) {
+    using A = Arith<T>;
+    __shared__ T xr[BH_RING];
+    const int lane = threadIdx.x;
+    const T* yc = Yin + (int64_t)blockIdx.x * n;
+    T* xc = X + (int64_t)blockIdx.x * n;
+    const int64_t last = n * ld - 1;
+    const int m0 = SEG * lane + 1;  // first term of this lane's segment
+    // L[i+m][i] = CB[i*ld + m] for this lane's m, rows i prefetched two ahead
+    T lvA[SEG], lvB[SEG];
+    T diagA = A::zero(), diagB = A::zero(), yA = A::zero(), yB = A::zero();
+    auto load_row = [&](T (&lv)[SEG], T& dg, T& yv, int64_t r) {
+        const int64_t rr = r < 0 ? 0 : r;
+#pragma unroll
+        for (int u = 0; u < SEG; ++u) {
+            int64_t a = rr * ld + m0 + u;
+            lv[u] = CB[a > last ? last : a];
+        }
+        dg = CB[rr * ld];
+        yv = yc[rr];
+    };
+    auto do_row = [&](const T (&lv)[SEG], T dg, T yv, int64_t i) {
+        const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
+        T p[SEG];
+#pragma unroll
+        for (int u = 0; u < SEG; ++u) {  // unconditional ring reads (always in range), then select
+            const int64_t m = m0 + u;
+            const T xv = xr[(i + m) & (BH_RING - 1)];
+            const T pr = A::mul(lv[u], xv);
+            p[u] = m <= dmax ? pr : A::zero();
+        }
+        const int nseg = (int)((dmax + SEG - 1) / SEG);
+        T sv = A::zero();  // running sum, wave-uniform between segments
+        for (int l = 0; l < nseg; ++l) {
+            T sl = sv;
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) sl = A::add(sl, p[u]);
+            sv = readlane_t(sl, l);
+        }
+        const T x = div_rn(A::sub(yv, sv), dg);
+        if (lane == 0) {
+            xr[i & (BH_RING - 1)] = x;
+            xc[i] = x;
+        }
+    };
+    int64_t i = n - 1;
+    load_row(lvA, diagA, yA, i);
+    load_row(lvB, diagB, yB, i - 1);
+    for (; i >= 1; i -= 2) {
+        do_row(lvA, diagA, yA, i);
+        load_row(lvA, diagA, yA, i - 2);
+        do_row(lvB, diagB, yB, i - 1);
+        load_row(lvB, diagB, yB, i - 3);
+    }
+    if (i == 0) do_row(lvA, diagA, yA, 0);
+}
+
+// ---------------------------------------------------------------------------
 // band -> CSR (the Csr returned by cholesky_decomp: zero results are not
 // stored, sparse.rs:229,710; row i lists columns ascending, diagonal last).
 // ---------------------------------------------------------------------------
@@ -799,6 +882,29 @@ int solve_dispatch_trsv(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, co
     return BSM_ERR_INVALID;
 }
 
+// band backward solve: the lane-hopping chain (band_backward_hop) for b up
+// to 64*32; the two-wave LDS chain (band_backward) beyond that or when
+// BSM_BW_VARIANT=1 (A/B).
+template <typename T>
+static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const T* cb, const T* y, T* x,
+                           hipStream_t s) {
+    const char* e = getenv("BSM_BW_VARIANT");
+    const bool legacy = (e && atoi(e) == 1) || b >= BH_RING || b > 64 * 32;
+    const int64_t N = (int64_t)n;
+    if (legacy)
+        band_backward<T><<<(unsigned)k, 128, 0, s>>>(N, b, ld, cb, y, x);
+    else if (b <= 64)
+        band_backward_hop<T, 1><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    else if (b <= 64 * 4)
+        band_backward_hop<T, 4><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    else if (b <= 64 * 16)
+        band_backward_hop<T, 16><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    else
+        band_backward_hop<T, 32><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
 int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
     auto run = [&]<typename T>() -> int {
         BSM_REQUIRE(a->rows == n, BSM_ERR_PANIC,
@@ -819,9 +925,7 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
             band_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), bc.as<T>(),
                                                              yc.as<T>());
             BSM_HIP_TRY(hipGetLastError());
-            band_backward<T><<<(unsigned)k, 128, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(),
-                                                        xc.as<T>());
-            BSM_HIP_TRY(hipGetLastError());
+            BSM_TRY(launch_backward<T>(n, k, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(), xc.as<T>(), s));
         }
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));

@@ -116,7 +116,9 @@ def test_cholesky_random_vs_literal_oracle(orc, dtype, n, density):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("g", [3, 16, 40])
-def test_poisson_cholesky_and_solve_vs_oracle(orc, dtype, g):
+@pytest.mark.parametrize("bw_variant", ["0", "1"])  # lane-hopping / two-wave LDS backward chain
+def test_poisson_cholesky_and_solve_vs_oracle(orc, monkeypatch, dtype, g, bw_variant):
+    monkeypatch.setenv("BSM_BW_VARIANT", bw_variant)
     n = g * g
     rp, ci, v = orc.poisson2d(g)
     v = v.astype(dtype)
@@ -160,6 +162,27 @@ def test_poisson_250_bit_exact_solve_f64(orc):
     rp, ci, v = orc.poisson2d(g)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
     b = orc.gen_x_cols(1002, n, 1)
+    x = solve(A, Dense.from_columns(b))
+    ex = orc.solve(n, rp, ci, v, b, band=True)[0]
+    assert bits(x.get_col(0)).tolist() == bits(ex).tolist()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_wide_band_solve_vs_oracle(orc, dtype):
+    """Bandwidth 1060 (> 1024: the 32-term lane segments of the backward
+    chain; band_chol takes b <= 1072) on a short banded SPD system,
+    bit-exact vs the band oracle."""
+    n, g = 2400, 1060
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        for j, v in ((i - g, -1.0), (i - 1, -1.0), (i, 4.5), (i + 1, -1.0), (i + g, -1.0)):
+            if 0 <= j < n:
+                rows.append(i), cols.append(j), vals.append(v)
+    rp = np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=n))]).astype(np.uint64)
+    ci = np.asarray(cols, dtype=np.uint64)
+    v = np.asarray(vals, dtype=dtype)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    b = orc.gen_x_cols(1003, n, 1, dtype=dtype)
     x = solve(A, Dense.from_columns(b))
     ex = orc.solve(n, rp, ci, v, b, band=True)[0]
     assert bits(x.get_col(0)).tolist() == bits(ex).tolist()
