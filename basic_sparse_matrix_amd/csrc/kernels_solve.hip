@@ -464,7 +464,8 @@ __global__ __launch_bounds__(128) void band_backward(int64_t n, int64_t b, int64
 // ahead. Padding terms are +0: the sum starts at +0 and can never become
 // -0, so adding +0 leaves it unchanged (bit-exact).
 // ---------------------------------------------------------------------------
-constexpr int BH_RING = 4096;  // x ring (power of two > b)
+constexpr int BH_RING = 4096;        // x ring (power of two > b)
+constexpr size_t BAND_PAD = 64 * 32;  // zero elements after the band (whole-segment reads of the last rows)
 
 __device__ __forceinline__ double readlane_t(double v, int l) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -483,22 +484,25 @@ __global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, in
     const int lane = threadIdx.x;
     const T* yc = Yin + (int64_t)blockIdx.x * n;
     T* xc = X + (int64_t)blockIdx.x * n;
-    const int64_t last = n * ld - 1;
     const int m0 = SEG * lane + 1;  // first term of this lane's segment
-    // L[i+m][i] = CB[i*ld + m] for this lane's m, rows i prefetched two ahead
+    // L[i+m][i] = CB[i*ld + m] for this lane's m, rows prefetched two ahead;
+    // CB is padded by BAND_PAD zeros, so row n-1's reads stay in bounds
     T lvA[SEG], lvB[SEG];
-    T diagA = A::zero(), diagB = A::zero(), yA = A::zero(), yB = A::zero();
-    auto load_row = [&](T (&lv)[SEG], T& dg, T& yv, int64_t r) {
-        const int64_t rr = r < 0 ? 0 : r;
+    auto load_row = [&](T (&lv)[SEG], int64_t r) {
+        const T* src = CB + (r < 0 ? 0 : r) * ld + m0;
 #pragma unroll
-        for (int u = 0; u < SEG; ++u) {
-            int64_t a = rr * ld + m0 + u;
-            lv[u] = CB[a > last ? last : a];
-        }
-        dg = CB[rr * ld];
-        yv = yc[rr];
+        for (int u = 0; u < SEG; ++u) lv[u] = src[u];
     };
-    auto do_row = [&](const T (&lv)[SEG], T dg, T yv, int64_t i) {
+    // y_i and L_ii of a block of 64 rows, one per lane (read with v_readlane)
+    T yblk = A::zero(), dblk = A::zero();
+    int64_t blk = -1;
+    auto do_row = [&](const T (&lv)[SEG], int64_t i) {
+        if ((i >> 6) != blk) {
+            blk = i >> 6;
+            const int64_t r = (blk << 6) + lane < n ? (blk << 6) + lane : n - 1;
+            yblk = yc[r];
+            dblk = CB[r * ld];
+        }
         const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
         T p[SEG];
 #pragma unroll
@@ -516,22 +520,23 @@ __global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, in
             for (int u = 0; u < SEG; ++u) sl = A::add(sl, p[u]);
             sv = readlane_t(sl, l);
         }
-        const T x = div_rn(A::sub(yv, sv), dg);
+        const int li = (int)(i & 63);
+        const T x = div_rn(A::sub(readlane_t(yblk, li), sv), readlane_t(dblk, li));
         if (lane == 0) {
             xr[i & (BH_RING - 1)] = x;
             xc[i] = x;
         }
     };
     int64_t i = n - 1;
-    load_row(lvA, diagA, yA, i);
-    load_row(lvB, diagB, yB, i - 1);
+    load_row(lvA, i);
+    load_row(lvB, i - 1);
     for (; i >= 1; i -= 2) {
-        do_row(lvA, diagA, yA, i);
-        load_row(lvA, diagA, yA, i - 2);
-        do_row(lvB, diagB, yB, i - 1);
-        load_row(lvB, diagB, yB, i - 3);
+        do_row(lvA, i);
+        load_row(lvA, i - 2);
+        do_row(lvB, i - 1);
+        load_row(lvB, i - 3);
     }
-    if (i == 0) do_row(lvA, diagA, yA, 0);
+    if (i == 0) do_row(lvA, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -708,8 +713,8 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     bd.n = (int64_t)a->rows;
     bd.b = bw;
     bd.ld = bw + 1;
-    BSM_TRY(bd.cb.alloc((size_t)bd.n * bd.ld * sizeof(T)));
-    BSM_HIP_TRY(hipMemsetAsync(bd.cb.p, 0, (size_t)bd.n * bd.ld * sizeof(T), s));
+    BSM_TRY(bd.cb.alloc(((size_t)bd.n * bd.ld + BAND_PAD) * sizeof(T)));
+    BSM_HIP_TRY(hipMemsetAsync(bd.cb.p, 0, ((size_t)bd.n * bd.ld + BAND_PAD) * sizeof(T), s));
     if (bd.n == 0) return BSM_OK;
     band_fill<T><<<nblk(bd.n, 256), 256, 0, s>>>(a->row_ptr, a->col, static_cast<const T*>(a->vals), bd.n, bd.ld,
                                                  bd.cb.as<T>());
@@ -897,7 +902,12 @@ static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const 
         band_backward_hop<T, 1><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
     else if (b <= 64 * 4)
         band_backward_hop<T, 4><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64 * 16)
+    else if (b <= 64 * 8)
+        band_backward_hop<T, 8><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    else if (b <= 64 * 16 && !(e && atoi(e) == 2))
+        // 16-term segments: at C5 (b = 1000) 4.2 s against 5.0 s with 32-term
+        // segments, whose per-row product set-up (registers spill to AGPRs)
+        // costs more than the 31 lane hops it saves (BSM_BW_VARIANT=2: A/B)
         band_backward_hop<T, 16><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
     else
         band_backward_hop<T, 32><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
