@@ -25,6 +25,8 @@
 // hand-off of MI355X_MICROARCH.md "Valid forms", table row 1).
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "bsm_internal.hpp"
@@ -72,6 +74,21 @@ template <typename T> __device__ __forceinline__ T div_rn(T a, T b);
 template <> __device__ __forceinline__ double div_rn(double a, double b) { return __ddiv_rn(a, b); }
 template <> __device__ __forceinline__ float div_rn(float a, float b) {
     return __double2float_rn(__ddiv_rn((double)a, (double)b));
+}
+
+constexpr int BH_RING = 4096;        // x ring (power of two > b)
+// zero elements after the band: whole-segment reads of the last rows
+// (band_backward_hop) and band_chol3's unclamped staging of columns up to
+// 32 past the last one
+__host__ __device__ inline int64_t band_pad(int64_t ld) { return 32 * ld + 4096; }
+
+__device__ __forceinline__ double readlane_t(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float readlane_t(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
 // ---------------------------------------------------------------------------
@@ -315,6 +332,280 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
 }
 
 // ---------------------------------------------------------------------------
+// band_chol3: the same factorisation with one workgroup barrier per C3S
+// columns instead of two or three per column. 512 threads = 8 waves, one
+// workgroup per CU (2 waves per SIMD, up to 256 VGPRs each).
+//   * Wave w owns rows ia = i0 + 2w and ib = ia + 1 of tile-row I. Their
+//     accumulators for the columns left of the tile (j < i0) sit in M
+//     register slots per row, lane c holding j = jb + c + 64 m; the k loop
+//     runs window by window (64 columns per slot, one instantiation per
+//     window), so the slot of column k is a compile-time index. Per column
+//     k the wave forms L[i][k] = (1/L[k][k]) * (A[i][k] - acc) in every
+//     lane, takes lane (k - jb) & 63's value with v_readlane and adds
+//     L[i][k] * L[j][k] to every later slot, one LDS read of L[j][k] serving
+//     both rows. No other wave is involved: a column step has no barrier.
+//   * The accumulators of the tile's own columns (j in [i0, i0+16), lanes
+//     0..15) are kept apart and updated once per batch from the tile's own
+//     L values of the batch (an LDS history), in ascending k.
+//   * Column k of the rows above the tile and 1/L[k][k] (array R, written
+//     once per column by the tile-row that owns row k) are staged into LDS
+//     C3S columns at a time from a register ring loaded C3LA batches ahead:
+//     unconditional sc1 loads, so every s_waitcnt vmcnt is a count.
+//   * The 16x16 diagonal block is factored by wave 0 alone at the end of the
+//     tile-row (registers + LDS), which then publishes the tile-row's
+//     progress. During the sweep, progress is published per batch, one
+//     batch behind: every wave's stores drained by a counted wait, the
+//     barrier, then one lane's sc1 flag store (MI355X_MICROARCH.md "Valid
+//     forms", row 1).
+// Operation order per element is the reference's (sparse.rs:689-708), so
+// the result is bit-identical to band_chol and to the oracle.
+// ---------------------------------------------------------------------------
+constexpr int C3S = 4;  // columns per staging batch (one barrier per batch)
+
+// RW rows per wave: 16 / RW waves, 1024 / RW threads
+template <typename T, int M, int RW>
+__global__ __launch_bounds__(1024 / RW) void band_chol3(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
+                                                         T* __restrict__ R, int* __restrict__ progress,
+                                                         int* __restrict__ status, int64_t n_tiles,
+                                                         unsigned long long* __restrict__ trace) {
+    using A = Arith<T>;
+    constexpr int NT = 1024 / RW;           // threads
+    constexpr int SPAN = 64 * M;            // staged d = 1 .. SPAN of each column
+    constexpr int CSTR = 64 * (M + 1) + 8;  // staged column k: [64 + d] = CB[k * ld + d], d in [-63, SPAN]
+    constexpr int PFN = (C3S * SPAN + NT - 1) / NT;
+    __shared__ T colbuf[2][C3S][CSTR];
+    __shared__ T rbuf[2][C3S];
+    __shared__ T hist[2][C3S][TR];
+    __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
+    __shared__ T lcol[64];
+    const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
+    // staged element e = tid + NT q of a batch: column e / SPAN, d = e % SPAN + 1,
+    // at offset off[q] from the batch's first column (int: n * ld + pad < 2^31)
+    int off[PFN];
+#pragma unroll
+    for (int q = 0; q < PFN; ++q) {
+        const int e = tid + NT * q;
+        off[q] = e < C3S * SPAN ? (e / SPAN) * (int)ld + e % SPAN + 1 : 0;
+    }
+    for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
+        const int i0 = (int)(I * TR);
+        const int jb = i0 - (int)b > 0 ? i0 - (int)b : 0;
+        const int nb = (i0 - jb + C3S - 1) / C3S;  // batches of the sweep
+        int* prev = &progress[I > 0 ? I - 1 : 0];
+        int seen = I > 0 ? -1 : INT32_MAX;
+        auto poll = [&](int need) {  // wave 0 only; blocking, bounded
+            long long spins = 0;
+            if (trace && c == 0 && seen < need) atomicAdd(&trace[3 * TRACE_TILES], 1ull);
+            while (seen < need) {
+                seen = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen >= need) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT ||
+                    ((spins & 1023) == 0 &&
+                     (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
+                    atomicOr(status, ST_TIMEOUT);
+                    seen = INT32_MAX;
+                    break;
+                }
+            }
+            if (trace && c == 0 && spins) atomicAdd(&trace[3 * TRACE_TILES + 1], (unsigned long long)spins);
+        };
+        auto batch_end = [&](int p) { return jb + C3S * (p + 1) < i0 ? jb + C3S * (p + 1) : i0; };
+        T acc[RW][M], aT[RW], accT[RW];
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+            const int rr = RW * w + q;  // A[i0 + rr][i0 + c] for the diagonal block (read at the end)
+            const bool ok = c < TR && c <= rr && rr - c <= (int)b && i0 + rr < n;
+            aT[q] = ok ? CB[(int64_t)(i0 + c) * ld + (rr - c)] : A::zero();
+            accT[q] = A::zero();
+#pragma unroll
+            for (int m = 0; m < M; ++m) acc[q][m] = A::zero();
+        }
+        // one register batch in flight: loaded at boundary p - 1 for batch p + 1
+        T pf[PFN + 1];
+        auto issue = [&](int kb) {
+            const T* base = CB + (int64_t)kb * ld;
+#pragma unroll
+            for (int q = 0; q < PFN; ++q) pf[q] = ld_sc1(base + off[q]);
+            pf[PFN] = ld_sc1(&R[kb + (tid & (C3S - 1))]);
+        };
+        auto stage = [&](int buf) {
+#pragma unroll
+            for (int q = 0; q < PFN; ++q) {
+                const int e = tid + NT * q;
+                if (C3S * SPAN % NT == 0 || e < C3S * SPAN) colbuf[buf][e / SPAN][64 + e % SPAN + 1] = pf[q];
+            }
+            rbuf[buf][tid & (C3S - 1)] = pf[PFN];  // every thread (same values): no branch, no vmcnt(0)
+        };
+        int pv = -1;  // progress[I-1] as loaded at the last boundary
+        // diagnostic phase clocks (BSM_CHOL_TRACE): steps, boundary up to the
+        // poll, poll, barrier, after the barrier -- summed by thread 0
+        const bool tr0 = trace && tid == 0 && I < TRACE_TILES;
+        long long tph[5] = {0, 0, 0, 0, 0}, tlast = 0;
+        auto mark = [&](int ph) {
+            if (tr0) {
+                const long long t = clock64();
+                tph[ph] += t - tlast;
+                tlast = t;
+            }
+        };
+        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I] = wall_clock64();
+        if (tid < 64 && I > 0) poll(batch_end(1));
+        __syncthreads();
+        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 1] = wall_clock64();
+        issue(jb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stage(0);
+        if (tid < 64) pv = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        issue(jb + C3S);
+        __syncthreads();
+        if (tr0) tlast = clock64();
+        // one instantiation per window m (64 columns = 8 batches): the slot index
+        // and the update range m..M-1 are compile-time
+        auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
+            for (int pw = 0; pw < 64 / C3S; ++pw) {
+                const int p = (64 / C3S) * m + pw;  // batch
+                if (p >= nb) return;
+                const int kb = jb + C3S * p, cur = p & 1;
+                // ---- C3S column steps, no barrier
+                for (int s = 0; s < C3S; ++s) {
+                    const int k = kb + s;
+                    if (k < i0) {
+                        const int ck = C3S * pw + s;
+                        // every LDS read of the step first (none depends on this step's L values)
+                        const T rk = rbuf[cur][s];
+                        const T* colk = &colbuf[cur][s][64 + (jb - k) + c];  // colk[64 mm] = L[jb + c + 64 mm][k]
+                        T lv[M];
+#pragma unroll
+                        for (int mm = m; mm < M; ++mm) lv[mm] = colk[64 * mm];
+                        T av[RW];
+#pragma unroll
+                        for (int q = 0; q < RW; ++q) {  // A[i0 + rr][k], staged at d = i0 + rr - k (not yet overwritten)
+                            const int d = i0 + RW * w + q - k;
+                            const T a = colbuf[cur][s][64 + (d < SPAN ? d : SPAN)];
+                            av[q] = d <= (int)b ? a : A::zero();
+                        }
+                        T x[RW];
+#pragma unroll
+                        for (int q = 0; q < RW; ++q) {
+                            x[q] = readlane_t(A::mul(rk, A::sub(av[q], acc[q][m])), ck);
+                            if (c == ck) hist[cur][s][RW * w + q] = x[q];
+                        }
+#pragma unroll
+                        for (int mm = m; mm < M; ++mm)
+#pragma unroll
+                            for (int q = 0; q < RW; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(x[q], lv[mm]));
+                    }
+                }
+                mark(0);
+                // ---- batch boundary
+                {  // store the batch's values: lane l -> row RW w + l / 32 (RW = 2), column kb + l % 8
+                    const int hs = c & (C3S - 1);
+                    const int rr = RW * w + (RW == 2 ? (c >> 5) : 0);
+                    const int i = i0 + rr, k = kb + hs;
+                    const T xv = hist[cur][hs][rr];
+                    const bool ok = i < n && k < i0 && i - k <= (int)b;
+                    st_sc1(ok ? &CB[(int64_t)k * ld + (i - k)] : &R[n + c], xv);
+                }
+                // everything but that store is done: the previous batch's stores,
+                // the next batch's columns, the last progress load
+                asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                stage(cur ^ 1);
+                mark(1);
+                if (tid < 64 && I > 0) {
+                    const int need = batch_end(p + 2);
+                    if (pv > seen) seen = pv;
+                    if (seen < need) poll(need);
+                }
+                mark(2);
+                __syncthreads();
+                mark(3);
+                if (tid == 0)  // columns < kb are final for this tile-row
+                    __hip_atomic_store(&progress[I], kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (c < TR) {  // tile-column accumulators, ascending k (reads first, then the chain)
+                    T hc[C3S], hr[C3S][RW];
+#pragma unroll
+                    for (int s = 0; s < C3S; ++s) {
+                        hc[s] = hist[cur][s][c];
+#pragma unroll
+                        for (int q = 0; q < RW; ++q) hr[s][q] = hist[cur][s][RW * w + q];
+                    }
+#pragma unroll
+                    for (int s = 0; s < C3S; ++s)
+                        if (kb + s < i0)
+#pragma unroll
+                            for (int q = 0; q < RW; ++q) accT[q] = A::add(accT[q], A::mul(hr[s][q], hc[s]));
+                }
+                if (tid < 64) pv = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                issue(kb + 2 * C3S);
+                mark(4);
+            }
+        };
+        [&]<int... ms>(std::integer_sequence<int, ms...>) __attribute__((always_inline)) {
+            (window(std::integral_constant<int, ms>{}), ...);
+        }(std::make_integer_sequence<int, M>{});
+        // ---- diagonal block: wave 0 factors the 16 x 16 block
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (c < TR) {
+#pragma unroll
+            for (int q = 0; q < RW; ++q) {
+                dacc[RW * w + q][c] = accT[q];
+                dA[RW * w + q][c] = aT[q];
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // lane c owns the block elements (r, j) = ((c + 64 u) / 16, (c + 64 u) % 16), u < 4:
+            // q = their accumulators, av = their A values; column t at step t
+            T q[4], av[4];
+            int er[4], ej[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                er[u] = (c + 64 * u) >> 4;
+                ej[u] = (c + 64 * u) & 15;
+                const bool live = i0 + er[u] < n;
+                q[u] = live ? dacc[er[u]][ej[u]] : A::zero();
+                av[u] = live ? dA[er[u]][ej[u]] : (er[u] == ej[u] ? (T)1 : A::zero());
+            }
+#pragma unroll 1
+            for (int t = 0; t < TR; ++t) {
+                // the pivot: element (t, t) is owned by lane (16 t + t) & 63, slot (16 t + t) >> 6
+                const int pe = 17 * t;
+                T dd = A::zero();
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u == (pe >> 6)) dd = A::sub(av[u], q[u]);
+                const T piv = readlane_t(pow_half(dd), pe & 63);
+                const T rt = div_rn((T)1, piv);
+                if (c == 0) {
+                    if (i0 + t < n && (!(piv > A::zero()) || isinf(piv))) atomicOr(status, ST_NOT_PD);
+                    if (i0 + t < n) st_sc1(&R[i0 + t], rt);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {  // column t: L[i0 + r][i0 + t], r >= t
+                    if (ej[u] == t && er[u] >= t) {
+                        const T x = er[u] == t ? piv : A::mul(rt, A::sub(av[u], q[u]));
+                        lcol[er[u]] = x;
+                        if (i0 + er[u] < n && er[u] - t <= b) st_sc1(&CB[(i0 + t) * ld + (er[u] - t)], x);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)  // acc[r][j] += L[r][t] * L[j][t] for t < j <= r
+                    if (ej[u] > t && er[u] >= ej[u]) q[u] = A::add(q[u], A::mul(lcol[er[u]], lcol[ej[u]]));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0)
+                __hip_atomic_store(&progress[I], (int)(i0 + TR < n ? i0 + TR : n), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tr0) {
+            trace[3 * I + 2] = wall_clock64();
+            for (int ph = 0; ph < 5; ++ph) atomicAdd(&trace[3 * TRACE_TILES + 2 + ph], (unsigned long long)tph[ph]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // forward substitution on the band (lib.rs:28-46): y_i = (b_i - sum_{j<i}
 // L_ij y_j) / L_ii, sum in ascending j. One workgroup per RHS column; blocks
 // of 256 rows: the "far" terms (j < block start) are summed first, one thread
@@ -464,18 +755,6 @@ __global__ __launch_bounds__(128) void band_backward(int64_t n, int64_t b, int64
 // ahead. Padding terms are +0: the sum starts at +0 and can never become
 // -0, so adding +0 leaves it unchanged (bit-exact).
 // ---------------------------------------------------------------------------
-constexpr int BH_RING = 4096;        // x ring (power of two > b)
-constexpr size_t BAND_PAD = 64 * 32;  // zero elements after the band (whole-segment reads of the last rows)
-
-__device__ __forceinline__ double readlane_t(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ float readlane_t(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
 template <typename T, int SEG>
 __global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
                                                         const T* __restrict__ Yin, T* __restrict__ X) {
@@ -659,6 +938,7 @@ inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 // --------------------------------------------------------------------------
 struct Band {
     DBuf cb;
+    DBuf r;  // 1 / L[k][k] per column (+64 scratch entries), band_chol3
     int64_t n = 0, b = 0, ld = 1;
 };
 
@@ -700,6 +980,24 @@ int launch_chol(Band& bd, int* progress, int* status, hipStream_t s, unsigned lo
     return BSM_OK;
 }
 
+template <typename T, int M, int RW = 1>
+int launch_chol3(Band& bd, int* progress, int* status, hipStream_t s, unsigned long long* trace) {
+    const int64_t n_tiles = (bd.n + TR - 1) / TR;
+    int dev = 0, cus = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    int per_cu = 0;
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol3<T, M, RW>, 1024 / RW, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol3 does not fit a CU");
+    int64_t grid = cus;  // every workgroup resident: tile-row I waits on tile-row I-1
+    if (grid > n_tiles) grid = n_tiles;
+    if (grid < 1) grid = 1;
+    band_chol3<T, M, RW><<<(unsigned)grid, 1024 / RW, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), progress,
+                                                            status, n_tiles, trace);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
 template <typename T>
 int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     int64_t bw = 0;
@@ -713,8 +1011,9 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     bd.n = (int64_t)a->rows;
     bd.b = bw;
     bd.ld = bw + 1;
-    BSM_TRY(bd.cb.alloc(((size_t)bd.n * bd.ld + BAND_PAD) * sizeof(T)));
-    BSM_HIP_TRY(hipMemsetAsync(bd.cb.p, 0, ((size_t)bd.n * bd.ld + BAND_PAD) * sizeof(T), s));
+    const size_t cb_elems = (size_t)bd.n * bd.ld + (size_t)band_pad(bd.ld);
+    BSM_TRY(bd.cb.alloc(cb_elems * sizeof(T)));
+    BSM_HIP_TRY(hipMemsetAsync(bd.cb.p, 0, cb_elems * sizeof(T), s));
     if (bd.n == 0) return BSM_OK;
     band_fill<T><<<nblk(bd.n, 256), 256, 0, s>>>(a->row_ptr, a->col, static_cast<const T*>(a->vals), bd.n, bd.ld,
                                                  bd.cb.as<T>());
@@ -728,19 +1027,30 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     DBuf trace_buf;
     const bool tracing = getenv("BSM_CHOL_TRACE") != nullptr;
     if (tracing) {
-        BSM_TRY(trace_buf.alloc((3 * TRACE_TILES + 2) * sizeof(unsigned long long)));
-        BSM_HIP_TRY(hipMemsetAsync(trace_buf.p, 0, (3 * TRACE_TILES + 2) * sizeof(unsigned long long), s));
+        BSM_TRY(trace_buf.alloc((3 * TRACE_TILES + 8) * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(trace_buf.p, 0, (3 * TRACE_TILES + 8) * sizeof(unsigned long long), s));
     }
     unsigned long long* tr = tracing ? trace_buf.as<unsigned long long>() : nullptr;
     int rc;
-    if (need <= 64) rc = launch_chol<T, 1>(bd, prog.as<int>(), status, s, tr);
+    const char* cv = getenv("BSM_CHOL_VARIANT");
+    // band_chol3 indexes the band with 32-bit offsets
+    const bool fits32 = (int64_t)a->rows * (bw + 1) + band_pad(bw + 1) < ((int64_t)1 << 31);
+    const bool v1 = (cv && atoi(cv) == 1) || bw > 64 * 16 || !fits32;
+    if (!v1) {
+        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));  // R[n .. n+63]: dummy store / staging targets
+        if (bw <= 64) rc = launch_chol3<T, 1>(bd, prog.as<int>(), status, s, tr);
+        else if (bw <= 128) rc = launch_chol3<T, 2>(bd, prog.as<int>(), status, s, tr);
+        else if (bw <= 256) rc = launch_chol3<T, 4>(bd, prog.as<int>(), status, s, tr);
+        else if (bw <= 512) rc = launch_chol3<T, 8>(bd, prog.as<int>(), status, s, tr);
+        else rc = launch_chol3<T, 16>(bd, prog.as<int>(), status, s, tr);
+    } else if (need <= 64) rc = launch_chol<T, 1>(bd, prog.as<int>(), status, s, tr);
     else if (need <= 128) rc = launch_chol<T, 2>(bd, prog.as<int>(), status, s, tr);
     else if (need <= 256) rc = launch_chol<T, 4>(bd, prog.as<int>(), status, s, tr);
     else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s, tr);
     else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s, tr);
     BSM_TRY(rc);
     if (tracing) {
-        std::vector<unsigned long long> h(3 * TRACE_TILES + 2);
+        std::vector<unsigned long long> h(3 * TRACE_TILES + 8);
         BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         const int64_t nt = n_tiles < TRACE_TILES ? n_tiles : TRACE_TILES;
@@ -760,6 +1070,13 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
                 "start-to-start %.2f us (= %.1f steps); blocking polls %llu, spins %llu\n",
                 (long long)n_tiles, (long long)cnt, dur / cnt * us, dur / cnt * us / steps, pro / cnt * us,
                 gap / cnt * us, gap / cnt / (dur / cnt / steps), h[3 * TRACE_TILES], h[3 * TRACE_TILES + 1]);
+        const unsigned long long* ph = &h[3 * TRACE_TILES + 2];
+        const double nbd = (double)nt * (double)((bd.b + 3) / 4);  // boundaries traced (band_chol3)
+        if (ph[0])
+            fprintf(stderr,
+                    "[bsm chol trace] band_chol3 cycles per batch of 4 columns: steps %.0f, store+stage %.0f, "
+                    "poll %.0f, barrier %.0f, after barrier %.0f\n",
+                    ph[0] / nbd, ph[1] / nbd, ph[2] / nbd, ph[3] / nbd, ph[4] / nbd);
     }
     int st = 0;
     BSM_HIP_TRY(hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, s));

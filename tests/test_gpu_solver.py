@@ -103,9 +103,11 @@ def csr_arrays(dense):
     return rp, nzc.astype(np.uint64), dense[nzr, nzc]
 
 
+@pytest.mark.parametrize("chol_variant", ["0", "1"])  # band_chol3 / band_chol
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("n,density", [(1, 1.0), (7, 0.5), (33, 0.2), (64, 0.05), (150, 0.1), (300, 0.02)])
-def test_cholesky_random_vs_literal_oracle(orc, dtype, n, density):
+def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, chol_variant):
+    monkeypatch.setenv("BSM_CHOL_VARIANT", chol_variant)
     rng = np.random.default_rng(n)
     a = random_spd(rng, n, density, dtype)
     rp, ci, v = csr_arrays(a)
