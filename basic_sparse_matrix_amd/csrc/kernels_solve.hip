@@ -680,6 +680,156 @@ __global__ __launch_bounds__(FW_BLOCK) void band_forward(int64_t n, int64_t b, i
 }
 
 // ---------------------------------------------------------------------------
+// band_forward2: the forward solve with one 64-row block per wave and no
+// workgroup barrier. 16 waves per workgroup (one workgroup per RHS column);
+// block B belongs to wave B % 16. A wave first adds, in ascending j, the
+// terms of its rows left of the block -- following the "frontier" (rows
+// whose y is final, an LDS counter) as the earlier blocks are solved -- and
+// stages its block's 64 x 64 triangle of L into LDS. When the frontier
+// reaches the block, it solves the block row by row: lane t forms
+// y = (b - sum) / L[i][i] (true division, lib.rs:41), v_readlane broadcasts
+// y, every later lane adds L[i][i0+t] * y. The serial chain per row is one
+// subtraction, one division, one multiply and one add; the reads of the band
+// (8 B per nonzero) are spread over the waiting waves.
+// Terms outside the band are +0 products, which never change a sum that
+// starts at +0 (bit-exact, as band_forward).
+// ---------------------------------------------------------------------------
+constexpr int FW2_RING = 4096;  // y ring (power of two >= b + NW * 64 + 64)
+
+// NW waves, FW2_PF far-term loads in flight per lane: the waiting waves'
+// bytes in flight are what hides the HBM latency of the row-wise band reads
+template <typename T, int NW, int FW2_PF>
+__global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                         const T* __restrict__ B, T* __restrict__ Y,
+                                                         unsigned long long* __restrict__ trace) {
+    using A = Arith<T>;
+    __shared__ T yr[FW2_RING];
+    __shared__ T tri[2][64][64];  // tri[buf][t][l] = L[i0 + l][i0 + t]
+    __shared__ int frontier;      // y[0 .. frontier) are final in yr
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const T* bc = B + (int64_t)blockIdx.x * n;
+    T* yc = Y + (int64_t)blockIdx.x * n;
+    if (threadIdx.x == 0) frontier = 0;
+    __syncthreads();
+    // LDS atomics on the __shared__ counter itself (a volatile generic
+    // pointer compiles to flat_* accesses, and a flat store is waited on
+    // with vmcnt(0) together with the global y store)
+    auto fr_load = [&]() -> int64_t { return __hip_atomic_load(&frontier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    const int64_t nblk = (n + 63) / 64;
+    const int64_t pad_off = n * ld;  // band_pad zeros follow the band
+    // diagnostic (BSM_FW_TRACE): cycles per block in the far phase, waiting
+    // for the previous block, and solving the block -- summed over blocks
+    long long t_far = 0, t_wait = 0, t_step = 0, t_spin = 0;
+    for (int64_t blk = w; blk < nblk; blk += NW) {
+        const long long c0 = trace ? clock64() : 0;
+        const int64_t i0 = blk * 64, i = i0 + lane;
+        const bool live = i < n;
+        const int buf = (int)(blk & 1);
+        const T bi = live ? bc[i] : A::zero();
+        const T lii = live ? CB[i * ld] : (T)1;
+        // the block's triangle: column t of rows i0 + l, l > t (coalesced per
+        // t). Staged once block blk - 2 is solved: tri[buf] was block blk - 2's
+        // and block blk - 1 (being solved meanwhile) uses the other buffer.
+        bool staged = false;
+        auto stage_tri = [&]() {
+            for (int t = 0; t < 64; ++t) {
+                const int64_t a = (i0 + t) * ld + (lane - t);
+                const bool ok = live && lane > t && lane - t <= b;
+                const T v = CB[ok ? a : 0];
+                tri[buf][t][lane] = ok ? v : A::zero();
+            }
+            staged = true;
+        };
+        // wait until y[0 .. need) are final, staging the triangle on the way
+        // (once block blk - 2 is solved); the only call site of stage_tri
+        auto wait_frontier = [&](int64_t need) {
+            for (;;) {
+                const int64_t f = fr_load();
+                if (!staged && f >= i0 - 64) stage_tri();
+                if (f >= need && staged) break;
+                if (f >= need && i0 - 64 > f) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        // far terms j in [i0 - b, i0), ascending, as the frontier allows;
+        // out-of-band terms (j < i - b) are +0 products
+        T s = A::zero();
+        int64_t j = i0 - b > 0 ? i0 - b : 0;
+        // L[i][jj], or a zero of the band's padding outside the band / past
+        // the matrix: the ADDRESS is selected, the load is unconditional (a
+        // load under a branch costs a vmcnt(0) per term)
+        const uint32_t stride = (uint32_t)(ld - 1);  // L[i][jj] = CB[i + jj * (ld - 1)]
+        auto lfar = [&](int64_t jj) -> T {
+            const bool ok = live & (jj < i0) & (i - jj <= b);  // bitwise: no short-circuit branches
+            // select the operands, not the address: a selected address is
+            // lowered to an exec-masked branch around the address math
+            const uint32_t je = ok ? (uint32_t)jj : 0u;
+            const int64_t ie = ok ? i : pad_off;
+            return CB[ie + (int64_t)((uint64_t)je * stride)];
+        };
+        // batches of FW2_PF terms once the frontier covers them (terms at or
+        // past i0 predicated off); two register banks, so the loads of the
+        // batch after next are in flight while a batch is added
+        T pa[FW2_PF], pb[FW2_PF];
+#pragma unroll
+        for (int q = 0; q < FW2_PF; ++q) {
+            pa[q] = lfar(j + q);
+            pb[q] = lfar(j + FW2_PF + q);
+        }
+        auto batch = [&](T (&pf)[FW2_PF]) {
+            const int64_t need = j + FW2_PF < i0 ? j + FW2_PF : i0;
+            const long long cs = trace ? clock64() : 0;
+            wait_frontier(need);
+            if (trace) t_spin += clock64() - cs;
+            T pr[FW2_PF];  // the batch's products (y read from LDS all at once)
+#pragma unroll
+            for (int q = 0; q < FW2_PF; ++q) pr[q] = A::mul(pf[q], yr[(j + q) & (FW2_RING - 1)]);
+#pragma unroll
+            for (int q = 0; q < FW2_PF; ++q) pf[q] = lfar(j + 2 * FW2_PF + q);
+            // terms at or past i0: a +0 product (select, no branch), which
+            // leaves the sum unchanged (it starts at +0, never becomes -0)
+#pragma unroll
+            for (int q = 0; q < FW2_PF; ++q) s = A::add(s, j + q < i0 ? pr[q] : A::zero());
+            j += FW2_PF;
+        };
+        while (j < i0) {
+            batch(pa);
+            if (j >= i0) break;
+            batch(pb);
+        }
+        const long long c1 = trace ? clock64() : 0;
+        wait_frontier(i0);  // block blk - 1 solved (and the triangle staged)
+        const long long c2 = trace ? clock64() : 0;
+        // the block: one row per step
+        const int nb = (int)(n - i0 < 64 ? n - i0 : 64);
+        for (int t = 0; t < nb; ++t) {
+            const T lt = tri[buf][t][lane];  // read before the division: off the chain
+            const T yv = div_rn(A::sub(bi, s), lii);
+            const T y = readlane_t(yv, t);
+            if (lane == t) {
+                yr[(i0 + t) & (FW2_RING - 1)] = y;
+                yc[i0 + t] = y;
+                // y is in LDS before the frontier moves (LDS ops of one lane complete in order)
+                __hip_atomic_store(&frontier, (int)(i0 + t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (lane > t) s = A::add(s, A::mul(lt, y));
+        }
+        if (trace) {
+            const long long c3 = clock64();
+            t_far += c1 - c0;
+            t_wait += c2 - c1;
+            t_step += c3 - c2;
+        }
+    }
+    if (trace && lane == 0) {
+        atomicAdd(&trace[0], (unsigned long long)t_far);
+        atomicAdd(&trace[1], (unsigned long long)t_wait);
+        atomicAdd(&trace[2], (unsigned long long)t_step);
+        atomicAdd(&trace[3], (unsigned long long)t_spin);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // backward substitution on the band (lib.rs:49-65) with L* = L^T: x_i =
 // (y_i - sum_{j>i} L_ji x_j) / L_ii, sum in ascending j. Ascending order makes
 // each row's sum START with the newest x, so the solve is one serial chain of
@@ -1249,9 +1399,37 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
         BSM_TRY(xc.alloc(n * k * sizeof(T)));
         if (n && k) {
             // forward_substitution(l, b) over rows 0..n of L (lib.rs:31-44)
-            band_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), bc.as<T>(),
-                                                             yc.as<T>());
+            const char* fv = getenv("BSM_FW_VARIANT");
+            DBuf ftr;
+            unsigned long long* ftp = nullptr;
+            if (getenv("BSM_FW_TRACE")) {
+                BSM_TRY(ftr.alloc(4 * sizeof(unsigned long long)));
+                BSM_HIP_TRY(hipMemsetAsync(ftr.p, 0, 4 * sizeof(unsigned long long), s));
+                ftp = ftr.as<unsigned long long>();
+            }
+            if ((fv && atoi(fv) == 1) || bd.b + 16 * 64 + 64 > FW2_RING)
+                band_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
+                                                                 bc.as<T>(), yc.as<T>());
+            else if (fv && atoi(fv) == 2)
+                band_forward2<T, 16, 16><<<(unsigned)k, 1024, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
+                                                                      bc.as<T>(), yc.as<T>(), ftp);
+            else if (fv && atoi(fv) == 3)
+                band_forward2<T, 16, 8><<<(unsigned)k, 1024, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
+                                                                     bc.as<T>(), yc.as<T>(), ftp);
+            else
+                band_forward2<T, 8, 24><<<(unsigned)k, 512, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
+                                                                    bc.as<T>(), yc.as<T>(), ftp);
             BSM_HIP_TRY(hipGetLastError());
+            if (ftp) {
+                unsigned long long h[4];
+                BSM_HIP_TRY(hipMemcpyAsync(h, ftp, sizeof(h), hipMemcpyDeviceToHost, s));
+                BSM_HIP_TRY(hipStreamSynchronize(s));
+                const double nb = (double)((n + 63) / 64) * (double)k;
+                fprintf(stderr,
+                        "[bsm fw trace] cycles per 64-row block: far phase %.0f (of which waiting for the "
+                        "frontier %.0f), wait %.0f, solve %.0f\n",
+                        h[0] / nb, h[3] / nb, h[1] / nb, h[2] / nb);
+            }
             BSM_TRY(launch_backward<T>(n, k, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(), xc.as<T>(), s));
         }
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));

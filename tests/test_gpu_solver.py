@@ -118,9 +118,10 @@ def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("g", [3, 16, 40])
-@pytest.mark.parametrize("bw_variant", ["0", "1"])  # lane-hopping / two-wave LDS backward chain
-def test_poisson_cholesky_and_solve_vs_oracle(orc, monkeypatch, dtype, g, bw_variant):
-    monkeypatch.setenv("BSM_BW_VARIANT", bw_variant)
+@pytest.mark.parametrize("variant", ["0", "1"])  # new / first kernels of forward and backward solves
+def test_poisson_cholesky_and_solve_vs_oracle(orc, monkeypatch, dtype, g, variant):
+    monkeypatch.setenv("BSM_BW_VARIANT", variant)
+    monkeypatch.setenv("BSM_FW_VARIANT", variant)
     n = g * g
     rp, ci, v = orc.poisson2d(g)
     v = v.astype(dtype)
