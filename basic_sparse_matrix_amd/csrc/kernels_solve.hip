@@ -969,6 +969,148 @@ __global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, in
 }
 
 // ---------------------------------------------------------------------------
+// band_backward_reg: band_backward_hop with the lane walk unrolled and x held
+// in registers. On gfx950 one wave issues about one instruction per 4 cycles
+// and a dependent v_add_f64 every ~4.5 (scripts/micro/issue_cost.hip), so a
+// row costs ~4.5 cycles per chain add plus ~4 per other instruction; the
+// runtime loop over lanes of band_backward_hop also paid a taken branch per
+// hop (153 cycles per 16-add hop against 85 unrolled, hop_latency.hip). So:
+//  * the NL hops are unrolled (straight-line code per row pair). The running
+//    sum moves from lane l to lane l+1 by DPP wave_shr:1 (every lane adds its
+//    own products; lane l+1 then takes lane l's sum), or by v_readlane
+//    (DPP = false);
+//  * lane l keeps x[i+m] for its segment m = SEG*l+1 .. SEG*l+SEG in a
+//    register window; moving to row i-1 shifts every window by one: lane l
+//    takes lane l-1's last value through DPP and lane 0 takes the new x_i
+//    (no LDS ring, no barrier);
+//  * terms b < m <= W = SEG*NL read the zero padding of a band stored with
+//    ld >= W + 1 (band_walk_terms), so rows with all b terms need no masking;
+//    the first b rows (dmax < b) take the masked path. Every padding term is
+//    +-0 and the sum starts at +0, so it never changes the sum (bit-exact);
+//  * y_i and L_ii are uniform loads issued two rows ahead, like the band
+//    column, and x_i is stored by every lane to the same address (no
+//    exec-masked branch).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double shr1_t(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float shr1_t(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+
+template <typename T, int SEG, int NL, bool DPP, int... L>
+__device__ __forceinline__ T lane_walk(const T (&p)[SEG], std::integer_sequence<int, L...>) {
+    using A = Arith<T>;
+    T sv = A::zero();
+    auto hop = [&](auto lc) __attribute__((always_inline)) {
+        constexpr int l = decltype(lc)::value;
+        if constexpr (DPP) {
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) sv = A::add(sv, p[u]);
+            if constexpr (l + 1 < NL) sv = shr1_t(sv);
+        } else {
+            T sl = sv;
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) sl = A::add(sl, p[u]);
+            sv = readlane_t(sl, l);
+        }
+    };
+    (hop(std::integral_constant<int, L>{}), ...);
+    if constexpr (DPP) return readlane_t(sv, NL - 1);
+    return sv;
+}
+
+// (SEG, NL) of band_backward_reg for bandwidth b: NL lanes of SEG terms,
+// W = SEG * NL >= b terms walked per row. Fewer, longer segments save lane
+// hops (3 instructions each) but cost registers; (20, 50) is exact for the
+// C5 band (b = 1000). The band is stored with ld = max(b, W) + 1.
+struct BwCfg {
+    int seg, nl;
+};
+inline BwCfg band_walk_cfg(int64_t b) {
+    if (b <= 64) return {1, 64};
+    if (b <= 128) return {2, 64};
+    if (b <= 256) return {4, 64};
+    if (b <= 512) return {8, 64};
+    if (b <= 768) return {12, 64};
+    if (b <= 896) return {16, 56};
+    if (b <= 1000) return {20, 50};
+    if (b <= 1024) return {16, 64};
+    if (b <= 2048) return {32, 64};
+    return {0, 0};
+}
+inline int64_t band_walk_terms(int64_t b) {
+    const BwCfg c = band_walk_cfg(b);
+    return (int64_t)c.seg * c.nl;
+}
+
+template <typename T, int SEG, int NL, bool DPP>
+__global__ __launch_bounds__(64) void band_backward_reg(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                        const T* __restrict__ Yin, T* __restrict__ X) {
+    using A = Arith<T>;
+    const int lane = threadIdx.x;
+    const T* yc = Yin + (int64_t)blockIdx.x * n;
+    T* xc = X + (int64_t)blockIdx.x * n;
+    const int m0 = SEG * lane + 1;  // first term of this lane's segment
+    T lvA[SEG], lvB[SEG], xw[SEG];
+    T yA, dA, yB, dB;
+#pragma unroll
+    for (int u = 0; u < SEG; ++u) xw[u] = A::zero();  // x[i+m] = 0 past row n-1
+    // L[i+m][i] = CB[i*ld + m]; CB is padded by band_pad zeros, so row
+    // n-1's reads stay in bounds; rows < 0 (prefetch past the end) read row 0
+    auto load_row = [&](T (&lv)[SEG], T& y, T& d, int64_t r) __attribute__((always_inline)) {
+        const int64_t rr = r < 0 ? 0 : r;
+        const T* src = CB + rr * ld;
+#pragma unroll
+        for (int u = 0; u < SEG; ++u) lv[u] = src[m0 + u];
+        d = src[0];
+        y = yc[rr];
+    };
+    // row i; lv becomes the products. MASK: rows with dmax < b.
+    auto do_row = [&](auto mask, T (&lv)[SEG], T y, T d, int64_t i) __attribute__((always_inline)) {
+        if constexpr (decltype(mask)::value) {
+            const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) {
+                const T pr = A::mul(lv[u], xw[u]);
+                lv[u] = m0 + u <= dmax ? pr : A::zero();
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) lv[u] = A::mul(lv[u], xw[u]);
+        }
+        const T sv = lane_walk<T, SEG, NL, DPP>(lv, std::make_integer_sequence<int, NL>{});
+        const T x = div_rn(A::sub(y, sv), d);
+        xc[i] = x;  // every lane, same address and value
+        const T t = shr1_t(xw[SEG - 1]);
+#pragma unroll
+        for (int u = SEG - 1; u > 0; --u) xw[u] = xw[u - 1];
+        xw[0] = lane == 0 ? x : t;
+    };
+    constexpr std::true_type masked{};
+    constexpr std::false_type full{};
+    int64_t i = n - 1;
+    const int64_t i_full = n - 1 - b;  // rows <= i_full have all b terms
+    load_row(lvA, yA, dA, i);
+    load_row(lvB, yB, dB, i - 1);
+    for (; i >= 1 && i > i_full; i -= 2) {
+        do_row(masked, lvA, yA, dA, i);
+        load_row(lvA, yA, dA, i - 2);
+        do_row(masked, lvB, yB, dB, i - 1);
+        load_row(lvB, yB, dB, i - 3);
+    }
+    for (; i >= 1; i -= 2) {
+        do_row(full, lvA, yA, dA, i);
+        load_row(lvA, yA, dA, i - 2);
+        do_row(full, lvB, yB, dB, i - 1);
+        load_row(lvB, yB, dB, i - 3);
+    }
+    if (i == 0) do_row(masked, lvA, yA, dA, 0);
+}
+
+// ---------------------------------------------------------------------------
 // band -> CSR (the Csr returned by cholesky_decomp: zero results are not
 // stored, sparse.rs:229,710; row i lists columns ascending, diagonal last).
 // ---------------------------------------------------------------------------
@@ -1160,7 +1302,9 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
                 (long long)bw, 64 * 17 - TR);
     bd.n = (int64_t)a->rows;
     bd.b = bw;
-    bd.ld = bw + 1;
+    // the backward solve walks band_walk_terms(b) terms per row and reads the
+    // ones past b from this padding (zeros)
+    bd.ld = (band_walk_terms(bw) > bw ? band_walk_terms(bw) : bw) + 1;
     const size_t cb_elems = (size_t)bd.n * bd.ld + (size_t)band_pad(bd.ld);
     BSM_TRY(bd.cb.alloc(cb_elems * sizeof(T)));
     BSM_HIP_TRY(hipMemsetAsync(bd.cb.p, 0, cb_elems * sizeof(T), s));
@@ -1363,15 +1507,43 @@ static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const 
     const char* e = getenv("BSM_BW_VARIANT");
     const bool legacy = (e && atoi(e) == 1) || b >= BH_RING || b > 64 * 32;
     const int64_t N = (int64_t)n;
+    const bool hop = e && (atoi(e) == 2 || atoi(e) == 3);  // 2: hop with 32-term segments, 3: hop
     if (legacy)
         band_backward<T><<<(unsigned)k, 128, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64)
+    else if (!hop) {
+        // register window, unrolled walk of W = band_walk_terms(b) terms
+        // (ld >= W + 1 is set by band_factor); BSM_BW_VARIANT=4: v_readlane
+        // hops (16 x 64 only), 5: 16-term segments on 64 lanes for 512 < b <= 1024
+        const bool rl = e && atoi(e) == 4, seg16 = e && atoi(e) == 5;
+        BSM_REQUIRE(ld >= band_walk_terms(b) + 1, BSM_ERR_INVALID, "backward: band ld %lld too small",
+                    (long long)ld);
+        auto go = [&]<int SEG, int NL>() {
+            if constexpr (SEG == 16 && NL == 64) {
+                if (rl) {
+                    band_backward_reg<T, SEG, NL, false><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+                    return;
+                }
+            }
+            band_backward_reg<T, SEG, NL, true><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+        };
+        const BwCfg c = band_walk_cfg(b);
+        if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
+        else if (c.seg == 1) go.template operator()<1, 64>();
+        else if (c.seg == 2) go.template operator()<2, 64>();
+        else if (c.seg == 4) go.template operator()<4, 64>();
+        else if (c.seg == 8) go.template operator()<8, 64>();
+        else if (c.seg == 12) go.template operator()<12, 64>();
+        else if (c.seg == 16 && c.nl == 56) go.template operator()<16, 56>();
+        else if (c.seg == 20) go.template operator()<20, 50>();
+        else if (c.seg == 16) go.template operator()<16, 64>();
+        else go.template operator()<32, 64>();
+    } else if (b <= 64)
         band_backward_hop<T, 1><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
     else if (b <= 64 * 4)
         band_backward_hop<T, 4><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
     else if (b <= 64 * 8)
         band_backward_hop<T, 8><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64 * 16 && !(e && atoi(e) == 2))
+    else if (b <= 64 * 16 && atoi(e) != 2)
         // 16-term segments: at C5 (b = 1000) 4.2 s against 5.0 s with 32-term
         // segments, whose per-row product set-up (registers spill to AGPRs)
         // costs more than the 31 lane hops it saves (BSM_BW_VARIANT=2: A/B)

@@ -118,7 +118,7 @@ def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("g", [3, 16, 40])
-@pytest.mark.parametrize("variant", ["0", "1"])  # new / first kernels of forward and backward solves
+@pytest.mark.parametrize("variant", ["0", "1", "3", "4", "5"])  # BSM_BW_VARIANT / BSM_FW_VARIANT A/B kernels (see kernels_solve.hip)
 def test_poisson_cholesky_and_solve_vs_oracle(orc, monkeypatch, dtype, g, variant):
     monkeypatch.setenv("BSM_BW_VARIANT", variant)
     monkeypatch.setenv("BSM_FW_VARIANT", variant)
