@@ -79,6 +79,7 @@ SIGNATURES = [
     ("bsm_device_count", _int, [ctypes.POINTER(_int)]),
     ("bsm_set_device", _int, [_int]),
     ("bsm_csr_upload", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    ("bsm_csr_from_inserts", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     ("bsm_csr_shape", _int, [_vp, _u64p, _u64p, _u64p, ctypes.POINTER(_int)]),
     ("bsm_csr_download", _int, [_vp, _vp, _vp, _vp]),
     ("bsm_csr_free", None, [_vp]),
@@ -92,6 +93,8 @@ SIGNATURES = [
     ("bsm_dev_gen_row_ptr", _int, [_u64, _u64, _u64, _u32, _int, _u32, _u32, _vp, _vp, _u64, _vp]),
     ("bsm_dev_gen_entries", _int, [_int, _u64, _u64, _u64, _u32, _int, _vp, _vp, _vp, _vp]),
     ("bsm_dev_gen_dense", _int, [_int, _u64, _u64, _u64, _u64, _int, _vp, _vp]),
+    ("bsm_dev_gen_insert_stream", _int, [_int, _u64, _u64, _u64, _u64, _u64, _u64, _vp, _vp, _vp, _vp]),
+    ("bsm_dev_csr_from_inserts", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp), _vp]),
     ("bsm_dev_scan_workspace_bytes", _u64, [_u64]),
     ("bsm_dev_spmm", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp]),
     ("bsm_csr_panel_cols", _int, [_vp, _u64p]),
@@ -186,6 +189,23 @@ class DeviceCsr:
         vals = np.ascontiguousarray(vals)
         h = _vp()
         check(lib.bsm_csr_upload(code, rows, cols, vals.size, ptr(row_ptr), ptr(col_idx), ptr(vals), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_inserts(cls, rows, cols, row: np.ndarray, col: np.ndarray, vals: np.ndarray) -> "DeviceCsr":
+        """bsm_csr_from_inserts: Csr::insert(vals[i], row[i], col[i]) for every i,
+        then finalise (sparse.rs:206-250), built on the device."""
+        lib = require_device()
+        code = DTYPE_CODES.get(vals.dtype)
+        if code is None:
+            raise TypeError(f"dtype {vals.dtype} has no GPU path")
+        row = np.ascontiguousarray(row, dtype=np.uint64)
+        col = np.ascontiguousarray(col, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals)
+        h = _vp()
+        rc = lib.bsm_csr_from_inserts(code, rows, cols, vals.size, ptr(row), ptr(col), ptr(vals), ctypes.byref(h))
+        if rc != BSM_OK:
+            raise BsmError(rc, last_error())
         return cls(h.value)
 
     def download(self):

@@ -173,6 +173,15 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
 int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
                   int32_t* row_nnz, bool neg_zero_init, hipStream_t s);
+// nnz-balanced integer SpMM for skewed rows (zeroes y; row_nnz may be null)
+bool spmm_wants_split(int dtype, uint64_t k, uint64_t max_row_len);
+int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                        const void* vals, uint64_t k, const void* x, void* y, int32_t* row_nnz, hipStream_t s);
+// device construction from an insert sequence (kernels_build.hip)
+int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                            const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s);
+int gen_insert_stream(int dtype, uint64_t seed, uint64_t i0, uint64_t n, uint64_t rows, uint64_t cols,
+                      uint64_t vmod, uint64_t* row, uint64_t* col, void* vals, hipStream_t s);
 uint64_t spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k);  // 0 = single pass
 uint64_t spmm_plan_bytes(uint64_t rows, uint64_t n_cols, uint64_t panel_cols);
 int spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* rp, const int32_t* col,

@@ -50,7 +50,8 @@ enum {
     BSM_SALT_ROWLEN = 1,
     BSM_SALT_COL = 2,
     BSM_SALT_VAL = 3,
-    BSM_SALT_X = 4
+    BSM_SALT_X = 4,
+    BSM_SALT_STREAM = 5
 };
 
 /* Value families (bsm_gen_spec.value_kind). */
@@ -108,6 +109,16 @@ BSM_HD uint32_t bsm_rowlen(uint64_t seed, uint64_t row, int kind, uint32_t a, ui
         return a + (uint32_t)(((h >> 32) * span) >> 32);
     }
     return a;
+}
+
+/* Insert stream shaped like the reference bench (sparse_dense_mul.rs:16-22):
+ * entry i is insert(v, row, col) with row = draw0 % rows, col = draw1 % cols,
+ * v = draw2 % vmod (the bench: 1000, 1000, 255 -- v == 0 is skipped by
+ * insert, and the running-max row rule of insert_unchecked piles almost
+ * every entry into the last rows). Draw f of entry i is
+ * bsm_hash(seed, i, f, BSM_SALT_STREAM); StdRng itself is not vendored. */
+BSM_HD uint64_t bsm_stream_draw(uint64_t seed, uint64_t i, uint64_t field) {
+    return bsm_hash(seed, i, field, BSM_SALT_STREAM);
 }
 
 #endif /* BSM_SYNTH_H */

@@ -160,7 +160,10 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
             a->plan_cols = w;
             a->plan_usable = usable != 0;
         }
-        if (w && a->plan_usable)
+        if (spmm_wants_split(a->dtype, k, a->max_row_len))
+            BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, y.p,
+                                        row_nnz.as<int32_t>(), s));
+        else if (w && a->plan_usable)
             BSM_TRY(spmm_panelled(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
                                   y.p, row_nnz.as<int32_t>(), w, a->plan_seg, s));
         else
@@ -277,6 +280,36 @@ int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz, const 
     }
     *out = m;
     return BSM_OK;
+}
+
+int bsm_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                         const uint64_t* col, const void* vals, bsm_csr** out) {
+    BSM_REQUIRE(out && (n == 0 || (row && col && vals)), BSM_ERR_INVALID, "null argument");
+    const size_t es = dtype_size(dtype);
+    BSM_REQUIRE(es, BSM_ERR_INVALID, "unknown dtype %d", dtype);
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf dr, dc, dv;
+    BSM_TRY(dr.alloc((n ? n : 1) * sizeof(uint64_t)));
+    BSM_TRY(dc.alloc((n ? n : 1) * sizeof(uint64_t)));
+    BSM_TRY(dv.alloc((n ? n : 1) * es));
+    if (n) {
+        BSM_HIP_TRY(hipMemcpyAsync(dr.p, row, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        BSM_HIP_TRY(hipMemcpyAsync(dc.p, col, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        BSM_HIP_TRY(hipMemcpyAsync(dv.p, vals, n * es, hipMemcpyHostToDevice, s));
+    }
+    return csr_from_inserts_device(dtype, rows, cols, n, dr.as<uint64_t>(), dc.as<uint64_t>(), dv.p, out, s);
+}
+
+int bsm_dev_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                             const uint64_t* col, const void* vals, bsm_csr** out, void* stream) {
+    return csr_from_inserts_device(dtype, rows, cols, n, row, col, vals, out, static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_gen_insert_stream(int dtype, uint64_t seed, uint64_t i0, uint64_t n, uint64_t rows, uint64_t cols,
+                              uint64_t vmod, uint64_t* row, uint64_t* col, void* vals, void* stream) {
+    BSM_REQUIRE(n == 0 || (row && col && vals), BSM_ERR_INVALID, "null argument");
+    return gen_insert_stream(dtype, seed, i0, n, rows, cols, vmod, row, col, vals, static_cast<hipStream_t>(stream));
 }
 
 int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz, int* dtype) {

@@ -794,6 +794,120 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// nnz-balanced SpMM for INTEGER scalars (split rows). The reference bench's
+// insert order piles almost every entry into the last row (running-max row
+// rule, sparse.rs:237-250), so one wave per row
+// serialises the whole product. Integer sums wrap (Cargo.toml:18) and are
+// therefore order-free: each wave takes a fixed slice of SPLIT_CHUNK entries,
+// sums its part of every row it touches (lanes (s, c): entry slot s, output
+// column c, then an xor-butterfly over s) and stores rows it covers entirely
+// or atomically adds partial rows into a zeroed Y. Floating point keeps the
+// in-order row-wave kernels: its sums are not associative.
+// ---------------------------------------------------------------------------
+constexpr int64_t SPLIT_CHUNK = 2048;   // entries per wave
+constexpr uint64_t SPLIT_MIN_ROW = 8192;  // use the split kernel when some row is longer
+
+template <typename T> struct UnsignedOf;
+template <> struct UnsignedOf<int32_t> { using type = uint32_t; };
+template <> struct UnsignedOf<uint32_t> { using type = uint32_t; };
+template <> struct UnsignedOf<int64_t> { using type = unsigned long long; };
+template <> struct UnsignedOf<uint64_t> { using type = unsigned long long; };
+
+template <typename T, int KL>
+__global__ __launch_bounds__(256) void spmm_split_int(int64_t rows, int64_t nnz, const int64_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                      int k, const T* __restrict__ X, T* __restrict__ Y) {
+    using U = typename UnsignedOf<T>::type;
+    constexpr int S = WAVE / KL;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int s = lane / KL, c = lane % KL;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+    const int64_t e0 = w * SPLIT_CHUNK;
+    if (e0 >= nnz) return;  // wave-uniform
+    const int64_t e1 = min<int64_t>(nnz, e0 + SPLIT_CHUNK);
+    // the row holding e0: the last r with rp[r] <= e0 (rows before it are empty)
+    int64_t r = wave_lower_bound_rp(rp, rows + 1, e0 + 1) - 1;
+    for (; r < rows; ++r) {
+        const int64_t rs = rp[r], re = rp[r + 1];
+        if (rs >= e1) break;
+        const int64_t a = max<int64_t>(e0, rs), b = min<int64_t>(e1, re);
+        if (a >= b) continue;
+        const bool whole = a == rs && b == re;
+        for (int cb = 0; cb < k; cb += KL) {
+            const int jc = cb + c;
+            const bool cval = jc < k;
+            U acc = 0;
+            for (int64_t e = a + s; e < b; e += S) {
+                if (cval) acc += (U)val[e] * (U)X[(int64_t)col[e] * k + jc];
+            }
+#pragma unroll
+            for (int off = KL; off < WAVE; off <<= 1) acc += (U)__shfl_xor(acc, off, WAVE);
+            if (s == 0 && cval) {
+                T* dst = &Y[r * (int64_t)k + jc];
+                if (whole)
+                    *dst = (T)acc;
+                else
+                    atomicAdd(reinterpret_cast<U*>(dst), acc);
+            }
+        }
+    }
+}
+
+// nonzero results per row of a dense Y (rows x k), for the compaction
+template <typename T>
+__global__ __launch_bounds__(256) void count_row_nnz(int64_t rows, int k, const T* __restrict__ Y,
+                                                     int32_t* __restrict__ row_nnz) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    int32_t n = 0;
+    for (int j = 0; j < k; ++j) n += Arith<T>::nz(Y[r * (int64_t)k + j]) ? 1 : 0;
+    row_nnz[r] = n;
+}
+
+bool spmm_wants_split(int dtype, uint64_t k, uint64_t max_row_len) {
+    if (const char* e = getenv("BSM_SPMM_SPLIT")) return atoi(e) != 0 && k >= 2 &&
+                                                          !(dtype == BSM_F64 || dtype == BSM_F32);
+    return k >= 2 && max_row_len >= SPLIT_MIN_ROW && !(dtype == BSM_F64 || dtype == BSM_F32);
+}
+
+int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                        const void* vals, uint64_t k, const void* x, void* y, int32_t* row_nnz, hipStream_t s) {
+    BSM_REQUIRE(!(dtype == BSM_F64 || dtype == BSM_F32), BSM_ERR_INVALID, "split SpMM: integer scalars only");
+    if (rows == 0) return BSM_OK;
+    const size_t es = dtype_size(dtype);
+    BSM_HIP_TRY(hipMemsetAsync(y, 0, rows * k * es, s));
+    const uint64_t waves = (nnz + SPLIT_CHUNK - 1) / SPLIT_CHUNK;
+    const uint64_t blocks = (waves + 3) / 4;
+    BSM_REQUIRE(blocks < (1ull << 31) && k < (1ull << 31), BSM_ERR_UNSUPPORTED, "split SpMM: too large");
+    const int ki = (int)k;
+    return dispatch_dtype(dtype, [&]<typename T>() -> int {
+        if constexpr (std::is_integral_v<T>) {
+            auto go = [&]<int KL>() {
+                if (blocks)
+                    spmm_split_int<T, KL><<<(unsigned)blocks, 256, 0, s>>>(
+                        (int64_t)rows, (int64_t)nnz, rp, col, static_cast<const T*>(vals), ki,
+                        static_cast<const T*>(x), static_cast<T*>(y));
+            };
+            if (k <= 2) go.template operator()<2>();
+            else if (k <= 4) go.template operator()<4>();
+            else if (k <= 8) go.template operator()<8>();
+            else if (k <= 16) go.template operator()<16>();
+            else if (k <= 32) go.template operator()<32>();
+            else go.template operator()<64>();
+            BSM_HIP_TRY(hipGetLastError());
+            if (row_nnz) {
+                count_row_nnz<T><<<(unsigned)((rows + 255) / 256), 256, 0, s>>>((int64_t)rows, ki,
+                                                                                static_cast<const T*>(y), row_nnz);
+                BSM_HIP_TRY(hipGetLastError());
+            }
+            return BSM_OK;
+        } else {
+            return BSM_ERR_INVALID;
+        }
+    });
+}
+
 int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
                   int32_t* row_nnz, bool neg_zero_init, hipStream_t s) {

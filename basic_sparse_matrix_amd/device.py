@@ -137,3 +137,32 @@ class Compactor:
 
     def nnz(self) -> int:
         return int(self.row_ptr[self.rows].item())
+
+
+def gen_insert_stream(seed, n, rows=1000, cols=1000, vmod=255, dtype=np.uint32, device="cuda"):
+    """Bench-shaped insert stream on the device (bsm_dev_gen_insert_stream;
+    benches/sparse_dense_mul.rs:16-22): (row u64, col u64, v dtype) tensors."""
+    lib = _lib.require_device()
+    dt = np.dtype(dtype)
+    r = torch.empty(max(1, n), dtype=torch.uint64, device=device)
+    c = torch.empty(max(1, n), dtype=torch.uint64, device=device)
+    v = torch.empty(max(1, n), dtype=TORCH_DT[dt], device=device)
+    _lib.check(lib.bsm_dev_gen_insert_stream(_lib.DTYPE_CODES[dt], seed, 0, n, rows, cols, vmod, _p(r), _p(c), _p(v),
+                                             _stream()))
+    return r[:n], c[:n], v[:n]
+
+
+def csr_from_device_inserts(dims, row: torch.Tensor, col: torch.Tensor, v: torch.Tensor, stream=None):
+    """bsm_dev_csr_from_inserts on device tensors -> a finalised host Csr
+    whose device copy stays cached (Csr::insert x n, then finalise)."""
+    from .sparse import Csr, _raise_for
+    from .util import MatDim
+
+    lib = _lib.require_device()
+    d = MatDim.of(dims)
+    dt = np.dtype(str(v.dtype).replace("torch.", ""))
+    h = ctypes.c_void_p()
+    rc = lib.bsm_dev_csr_from_inserts(_lib.DTYPE_CODES[dt], d.rows, d.cols, v.numel(), _p(row), _p(col), _p(v),
+                                      ctypes.byref(h), _stream(stream))
+    _raise_for(rc)
+    return Csr._from_device(_lib.DeviceCsr(h.value))

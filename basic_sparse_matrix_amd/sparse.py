@@ -144,6 +144,24 @@ class Csr(GetDims):
         m.is_finalised = True
         return m
 
+    @classmethod
+    def from_inserts(cls, dims, row, col, v) -> "Csr":
+        """``insert(v[i], row[i], col[i])`` for every i, then ``finalise``
+        (sparse.rs:206-250), executed on the GPU (bsm_csr_from_inserts): the
+        zero skip, the running-max row rule of insert_unchecked and the
+        "big eek" panic behave exactly like the sequence of calls. The result
+        stays cached on the device for the hot-path methods."""
+        d = MatDim.of(dims)
+        v = np.asarray(v)
+        if v.dtype not in GPU_DTYPES:
+            raise TypeError(f"Csr<{v.dtype}> has no GPU path (supported: f64 f32 i32 u32 i64 u64)")
+        try:
+            dev = _lib.DeviceCsr.from_inserts(d.rows, d.cols, np.asarray(row), np.asarray(col), v)
+        except _lib.BsmError as e:
+            _raise_for(e.code)
+            raise
+        return cls._from_device(dev)
+
     # ------------------------------------------------------------ building
     def finalise(self) -> "Csr":
         """sparse.rs:206-219: pad row_index to rows+1 with nnz."""

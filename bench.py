@@ -84,6 +84,65 @@ def cpu_baseline(cfg_name, sample_rows):
     }
 
 
+def bench_x_cols(seed, k, n, fill, dtype=np.uint32):
+    """The reference bench's RHS (sparse_dense_mul.rs:23-29): k zero columns of
+    n, then `fill` writes of v % 255 at (col % k, row % n); later writes win."""
+    rng = np.random.default_rng(seed)
+    cols = [np.zeros(n, dtype=dtype) for _ in range(k)]
+    j = rng.integers(0, k, fill)
+    i = rng.integers(0, n, fill)
+    v = rng.integers(0, 255, fill)
+    for a, b, c in zip(j, i, v):
+        cols[a][b] = c
+    return cols
+
+
+def sd_mul_suite(iters=20):
+    """The reference's own criterion bench `sd_mul` (sparse_dense_mul.rs:6-35):
+    Csr<u32> 1000 x 1000 built by e random inserts (e = 100k .. 900k), times a
+    10-column Dense<u32> with e/100 random entries; throughput in criterion's
+    unit, elements = e per call. GPU: the public Csr.mul_dense call end to end
+    (X upload, nnz-balanced integer SpMM, compaction, download), the matrix
+    built on the device by the insert-sequence builder. CPU: the oracle's
+    restatement of mul_dense (1 thread) on the same matrix and RHS. The insert
+    stream is bsm_synth.h's SplitMix64 (StdRng is not vendored), same shape."""
+    from basic_sparse_matrix_amd import Dense
+    from basic_sparse_matrix_amd.device import csr_from_device_inserts, gen_insert_stream
+    from oracle import pyoracle as orc
+
+    for i in range(9):
+        e = 10000 * (i + 1) * 10
+        r, c, v = gen_insert_stream(SEED_A, e, 1000, 1000, 255, np.uint32)
+        a = csr_from_device_inserts((1000, 1000), r, c, v)
+        x_cols = bench_x_cols(SEED_X + e, 10, 1000, e // 100)
+        x = Dense.from_columns(x_cols)
+        for _ in range(3):
+            out = a.mul_dense(x)
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            out = a.mul_dense(x)
+            ts.append(time.perf_counter() - t0)
+        gpu_s = float(np.median(ts))
+        rp, ci, vv = np.asarray(a.row_index), np.asarray(a.col_index), np.asarray(a.v)
+        cts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            e_rp, e_ci, e_v = orc.mul_dense(1000, 1000, rp, ci, vv, x_cols)
+            cts.append(time.perf_counter() - t0)
+        cpu_s = float(np.median(cts))
+        ok = (np.array_equal(np.asarray(out.row_index, np.uint64), e_rp)
+              and np.array_equal(np.asarray(out.col_index, np.uint64), e_ci) and np.array_equal(np.asarray(out.v), e_v))
+        print(json.dumps({
+            "workload": "sd_mul (benches/sparse_dense_mul.rs:6-35)", "elements": e, "dtype": "u32",
+            "a_nnz": int(len(vv)), "longest_row": int(np.diff(rp.astype(np.int64)).max()), "k": 10,
+            "gpu_ms_per_call": round(gpu_s * 1e3, 4), "gpu_elements_per_s": round(e / gpu_s, 1),
+            "cpu_ms_per_call": round(cpu_s * 1e3, 4), "cpu_elements_per_s": round(e / cpu_s, 1),
+            "cpu_kind": "port (oracle mul_dense, 1 thread)", "gpu_over_cpu": round(cpu_s / gpu_s, 2),
+            "out_nnz": int(out.get_nnz()), "bit_exact_vs_oracle": bool(ok),
+        }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,7 +158,12 @@ def main():
                     help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
+    ap.add_argument("--sd-mul", action="store_true",
+                    help="run the reference's own sd_mul criterion shapes instead (one JSON line per size)")
     args = ap.parse_args()
+    if args.sd_mul:
+        sd_mul_suite()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -83,6 +83,16 @@ int bsm_set_device(int ordinal);
 int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz,
                    const uint64_t* row_ptr, const uint64_t* col_idx, const void* vals,
                    bsm_csr** out);
+/* Build a finalised Csr on the device from a SEQUENCE of Csr::insert(v[i],
+ * row[i], col[i]) calls followed by finalise (sparse.rs:206-250): zero
+ * values are skipped, an entry belongs to the running maximum of the rows
+ * inserted so far (insert_unchecked, sparse.rs:237-250), skipped rows get
+ * empty ranges, and finalise pads row_index. A kept row >= rows is the
+ * reference's finalise panic ("big eek", sparse.rs:210) -> BSM_ERR_PANIC;
+ * a kept col >= cols -> BSM_ERR_PANIC (the device Csr holds in-bounds
+ * columns). Host arrays of n entries. */
+int bsm_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                         const uint64_t* col, const void* vals, bsm_csr** out);
 int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz,
                   int* dtype);
 /* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz). */
@@ -128,6 +138,15 @@ int bsm_dev_gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_
 int bsm_dev_gen_entries(int dtype, uint64_t seed, uint64_t row0, uint64_t rows,
                         uint32_t n_cols, int value_kind, const int64_t* row_ptr,
                         int32_t* col, void* vals, void* stream);
+/* Insert stream shaped like the reference bench (sparse_dense_mul.rs:16-22;
+ * bsm_synth.h bsm_stream_draw): entries i0 .. i0+n-1 with row = draw % rows,
+ * col = draw % cols, v = draw % vmod (as dtype). Device arrays. */
+int bsm_dev_gen_insert_stream(int dtype, uint64_t seed, uint64_t i0, uint64_t n, uint64_t rows,
+                              uint64_t cols, uint64_t vmod, uint64_t* row, uint64_t* col, void* vals,
+                              void* stream);
+/* bsm_csr_from_inserts on device arrays (synchronous on `stream`). */
+int bsm_dev_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                             const uint64_t* col, const void* vals, bsm_csr** out, void* stream);
 /* Dense ROW-major n x k operand: X[r][j] = bsm_x_value(seed, row0 + r, j). */
 int bsm_dev_gen_dense(int dtype, uint64_t seed, uint64_t row0, uint64_t n, uint64_t k,
                       int value_kind, void* x, void* stream);

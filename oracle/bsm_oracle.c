@@ -133,6 +133,15 @@ void orc_gen_x_colmajor(uint64_t seed, uint64_t n_cols, uint64_t k, int value_ki
         for (uint64_t r = 0; r < n_cols; ++r) x[c * n_cols + r] = bsm_x_value(seed, r, c, value_kind);
 }
 
+void orc_gen_insert_stream(uint64_t seed, uint64_t n, uint64_t rows, uint64_t cols, uint64_t vmod,
+                           uint64_t* row, uint64_t* col, uint64_t* v) {
+    for (uint64_t i = 0; i < n; ++i) {
+        row[i] = bsm_stream_draw(seed, i, 0) % rows;
+        col[i] = bsm_stream_draw(seed, i, 1) % cols;
+        v[i] = bsm_stream_draw(seed, i, 2) % vmod;
+    }
+}
+
 uint64_t orc_gen_poisson2d(uint64_t g, uint64_t* row_ptr, uint64_t* col_idx, double* v) {
     uint64_t n = g * g, p = 0;
     for (uint64_t i = 0; i < n; ++i) {

@@ -61,6 +61,25 @@ enum {
                             uint64_t ri_len, const uint64_t* col_index, const T* v,        \
                             uint64_t nnz, uint64_t* t_row, uint64_t* t_col, T* t_v);
 
+/* ---- Construction: a sequence of Csr::insert calls then finalise ---------
+ * insert (sparse.rs:222-233) skips value == default; insert_unchecked
+ * (sparse.rs:237-250) appends and extends row_index only when `row` exceeds
+ * the rows recorded so far (running max); finalise (sparse.rs:206-220)
+ * panics ("big eek") when rows < row_index.len(), else pads to rows + 1.
+ * Output: out_row (rows+1), out_col/out_v (capacity n); ORC_ERR_PANIC on
+ * the finalise panic. */
+#define ORC_DECL_FROM_INSERTS(SUF, T)                                                      \
+    int orc_csr_from_inserts_##SUF(uint64_t rows, uint64_t n, const uint64_t* row,         \
+                                   const uint64_t* col, const T* v, uint64_t* out_row,     \
+                                   uint64_t* out_col, T* out_v, uint64_t* out_nnz);
+
+ORC_DECL_FROM_INSERTS(f64, double)
+ORC_DECL_FROM_INSERTS(f32, float)
+ORC_DECL_FROM_INSERTS(i32, int32_t)
+ORC_DECL_FROM_INSERTS(u32, uint32_t)
+ORC_DECL_FROM_INSERTS(i64, int64_t)
+ORC_DECL_FROM_INSERTS(u64, uint64_t)
+
 ORC_DECL_MUL_DENSE(f64, double)
 ORC_DECL_MUL_DENSE(f32, float)
 ORC_DECL_MUL_DENSE(i32, int32_t)
@@ -110,6 +129,10 @@ int orc_gen_entries(uint64_t seed, uint64_t r0, uint64_t r1, uint32_t n_cols,
 /* X column-major (k columns of n_cols) from seed. */
 void orc_gen_x_colmajor(uint64_t seed, uint64_t n_cols, uint64_t k, int value_kind,
                         double* x);
+/* Bench-shaped insert stream (bsm_synth.h bsm_stream_draw): row/col/v of
+ * entries [0, n) with the given moduli. */
+void orc_gen_insert_stream(uint64_t seed, uint64_t n, uint64_t rows, uint64_t cols, uint64_t vmod,
+                           uint64_t* row, uint64_t* col, uint64_t* v);
 /* 5-point 2D Poisson on a g x g grid, natural row-major ordering: diag 4,
  * neighbours -1 (Dirichlet). Sorted columns per row. Returns nnz. */
 uint64_t orc_gen_poisson2d(uint64_t g, uint64_t* row_ptr, uint64_t* col_idx, double* v);

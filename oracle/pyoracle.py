@@ -67,6 +67,25 @@ def _check(rc):
         raise OracleError(rc)
 
 
+def csr_from_inserts(rows, row, col, v):
+    """Csr::insert(v[i], row[i], col[i]) for every i, then finalise
+    (sparse.rs:206-250) -> (row_index u64 [rows+1], col u64, v)."""
+    v = np.ascontiguousarray(v)
+    dt = v.dtype
+    r, c = _u64(row), _u64(col)
+    n = len(v)
+    out_row = np.zeros(rows + 1, dtype=np.uint64)
+    out_col = np.zeros(max(1, n), dtype=np.uint64)
+    out_v = np.zeros(max(1, n), dtype=dt)
+    nnz = ctypes.c_uint64(0)
+    fn = getattr(lib(), "orc_csr_from_inserts_" + SUFFIX[dt])
+    rc = fn(ctypes.c_uint64(rows), ctypes.c_uint64(n), _p(r), _p(c), _p(v), _p(out_row), _p(out_col), _p(out_v),
+            ctypes.byref(nnz))
+    _check(rc)
+    m = nnz.value
+    return out_row, out_col[:m].copy(), out_v[:m].copy()
+
+
 def mul_dense(rows, cols, row_index, col_index, v, x_cols, x_rows=None):
     """Csr::mul_dense (sparse.rs:426-446). x_cols: list of k columns."""
     v = np.ascontiguousarray(v)
@@ -212,6 +231,16 @@ def gen_x_cols(seed, n_cols, k, value_kind=VAL_UNIFORM, dtype=np.float64):
     lib().orc_gen_x_colmajor(ctypes.c_uint64(seed), ctypes.c_uint64(n_cols), ctypes.c_uint64(k),
                              ctypes.c_int(value_kind), _p(x))
     return [x[j].astype(dtype) for j in range(k)]
+
+
+def gen_insert_stream(seed, n, rows=1000, cols=1000, vmod=255):
+    """Bench-shaped insert stream (bsm_synth.h bsm_stream_draw) -> row, col, v (u64)."""
+    r = np.zeros(max(1, n), dtype=np.uint64)
+    c = np.zeros(max(1, n), dtype=np.uint64)
+    v = np.zeros(max(1, n), dtype=np.uint64)
+    lib().orc_gen_insert_stream(ctypes.c_uint64(seed), ctypes.c_uint64(n), ctypes.c_uint64(rows),
+                                ctypes.c_uint64(cols), ctypes.c_uint64(vmod), _p(r), _p(c), _p(v))
+    return r[:n], c[:n], v[:n]
 
 
 def poisson2d(g):

@@ -123,3 +123,83 @@ def test_solve(orc, golden, band):
     x = orc.solve(n, rp, ci, v, b, band=band)
     # x_ref = [0.625, -0.1, 2.6999998, 0.5]: the f32 rounding of the chain
     assert _bits(x[0]) == _bits([f32(s) for s in g["x_cols"][0]])
+
+
+# ---- construction: a sequence of Csr::insert calls, then finalise ---------
+def from_data_inserts(rows):
+    """Csr::from_data (sparse.rs:193-203) is insert(val, i, j) over rows then columns."""
+    ins = [(v, i, j) for i, row in enumerate(rows) for j, v in enumerate(row)]
+    v, r, c = zip(*ins)
+    return np.asarray(r, dtype=np.uint64), np.asarray(c, dtype=np.uint64), np.asarray(v, dtype=np.int32)
+
+
+@pytest.mark.parametrize("name", ["example_mat_0", "example_mat_1", "example_mat_2", "csr_with_empty_row_top",
+                                  "csr_with_empty_row_middle"])
+def test_from_inserts_golden(orc, golden, name):
+    g = golden[name]
+    r, c, v = from_data_inserts(g["rows"])
+    o_rp, o_ci, o_v = orc.csr_from_inserts(len(g["rows"]), r, c, v)
+    assert o_rp.tolist() == g["row_index"]
+    assert o_ci.tolist() == g["col_index"]
+    assert o_v.tolist() == g["v"]
+
+
+def test_from_inserts_create_mat_by_insert(orc, golden):
+    g = golden["create_mat_by_insert"]
+    v, r, c = (np.asarray(a) for a in zip(*g["inserts"]))
+    rows, cols = g["dims"]
+    o_rp, o_ci, o_v = orc.csr_from_inserts(rows, r.astype(np.uint64), c.astype(np.uint64), v.astype(np.int32))
+    dense = np.zeros((rows, cols), dtype=np.int32)
+    for i in range(rows):
+        for e in range(int(o_rp[i]), int(o_rp[i + 1])):
+            dense[i, int(o_ci[e])] = o_v[e]
+    assert dense.tolist() == g["rows"]
+
+
+def test_from_inserts_finalise_panics(orc):
+    from oracle.pyoracle import OracleError, ORC_ERR_PANIC
+
+    r = np.array([0, 3], dtype=np.uint64)
+    c = np.array([0, 0], dtype=np.uint64)
+    with pytest.raises(OracleError) as e:
+        orc.csr_from_inserts(3, r, c, np.array([1, 1], dtype=np.int32))  # row 3 of 3 rows: "big eek"
+    assert e.value.code == ORC_ERR_PANIC
+    # a skipped (zero) insert never extends row_index, so no panic
+    rp, ci, v = orc.csr_from_inserts(3, r, c, np.array([1, 0], dtype=np.int32))
+    assert rp.tolist() == [0, 1, 1, 1] and v.tolist() == [1]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint32, np.int64])
+def test_from_inserts_matches_host_mirror(orc, dtype):
+    """The C restatement against the host mirror's literal insert loop
+    (basic_sparse_matrix_amd/sparse.py, sparse.rs:222-250), on streams with
+    zeros, repeated rows, decreasing rows and row gaps."""
+    from basic_sparse_matrix_amd.sparse import Csr
+
+    rng = np.random.default_rng(7)
+    n, rows, cols = 3000, 400, 50
+    r = np.sort(rng.integers(0, rows, n)).astype(np.uint64)
+    r[rng.random(n) < 0.3] = rng.integers(0, rows, int((rng.random(n) < 0.3).sum()) or 1)[0]  # stragglers
+    r[::7] = rng.integers(0, rows, len(r[::7]))
+    c = rng.integers(0, cols, n).astype(np.uint64)
+    v = rng.integers(-3, 4, n).astype(dtype)
+    if dtype == np.float64:
+        v[rng.random(n) < 0.05] = -0.0
+    m = Csr.new((rows, cols), dtype=dtype)
+    for a, b, x in zip(r, c, v):
+        m.insert(x, int(a), int(b))
+    m = m.finalise()
+    o_rp, o_ci, o_v = orc.csr_from_inserts(rows, r, c, v)
+    assert np.array_equal(np.asarray(m.row_index, dtype=np.uint64), o_rp)
+    assert np.array_equal(np.asarray(m.col_index, dtype=np.uint64), o_ci)
+    assert np.array_equal(np.asarray(m.v, dtype=dtype).view(np.uint8), o_v.view(np.uint8))
+
+
+def test_insert_stream_is_bench_shaped(orc):
+    """sparse_dense_mul.rs:16-22 shape: rows/cols/v in range; the running-max
+    rule leaves almost every entry in the last row."""
+    r, c, v = orc.gen_insert_stream(1000, 100_000)
+    assert r.max() < 1000 and c.max() < 1000 and v.max() < 255
+    rp, ci, vv = orc.csr_from_inserts(1000, r, c, v.astype(np.uint32))
+    lens = np.diff(rp.astype(np.int64))
+    assert lens[-1] > 0.8 * len(vv) and len(vv) == int((v != 0).sum())
