@@ -10,10 +10,12 @@ hand-written HIP kernels through the C-ABI in include/bsm.h
 from .dense import Dense
 from .dense_static import DenseS
 from .solver import backward_substitution, forward_substitution, solve
-from .sparse import Csr, CsrEntry
+from .sparse import COO, COOEntry, Csr, CsrEntry
 from .util import GetDims, MatDim, MatErr, MatErrKind, Panic
 
 __all__ = [
+    "COO",
+    "COOEntry",
     "Csr",
     "CsrEntry",
     "Dense",

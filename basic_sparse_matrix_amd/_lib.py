@@ -48,6 +48,7 @@ BSM_ERR_HIP = 5
 BSM_ERR_OOM = 6
 BSM_ERR_UNSUPPORTED = 7
 BSM_ERR_NO_DEVICE = 8
+BSM_ERR_OUT_OF_BOUNDS = 9
 
 # generator families (bsm_synth.h)
 ROWLEN_CONST, ROWLEN_UNIFORM, ROWLEN_BINOMIAL = 0, 1, 2
@@ -80,6 +81,7 @@ SIGNATURES = [
     ("bsm_set_device", _int, [_int]),
     ("bsm_csr_upload", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     ("bsm_csr_from_inserts", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    ("bsm_csr_from_coo", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     ("bsm_csr_shape", _int, [_vp, _u64p, _u64p, _u64p, ctypes.POINTER(_int)]),
     ("bsm_csr_download", _int, [_vp, _vp, _vp, _vp]),
     ("bsm_csr_free", None, [_vp]),
@@ -204,6 +206,22 @@ class DeviceCsr:
         vals = np.ascontiguousarray(vals)
         h = _vp()
         rc = lib.bsm_csr_from_inserts(code, rows, cols, vals.size, ptr(row), ptr(col), ptr(vals), ctypes.byref(h))
+        if rc != BSM_OK:
+            raise BsmError(rc, last_error())
+        return cls(h.value)
+
+    @classmethod
+    def from_coo(cls, rows, cols, row: np.ndarray, col: np.ndarray, vals: np.ndarray) -> "DeviceCsr":
+        """bsm_csr_from_coo: From<COO<T>> for Csr<T> (sparse.rs:56-66) on the device."""
+        lib = require_device()
+        code = DTYPE_CODES.get(vals.dtype)
+        if code is None:
+            raise TypeError(f"dtype {vals.dtype} has no GPU path")
+        row = np.ascontiguousarray(row, dtype=np.uint64)
+        col = np.ascontiguousarray(col, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals)
+        h = _vp()
+        rc = lib.bsm_csr_from_coo(code, rows, cols, vals.size, ptr(row), ptr(col), ptr(vals), ctypes.byref(h))
         if rc != BSM_OK:
             raise BsmError(rc, last_error())
         return cls(h.value)

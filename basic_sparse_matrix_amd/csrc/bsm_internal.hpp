@@ -180,6 +180,8 @@ int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* r
 // device construction from an insert sequence (kernels_build.hip)
 int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
                             const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s);
+int csr_from_coo_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                        const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s);
 int gen_insert_stream(int dtype, uint64_t seed, uint64_t i0, uint64_t n, uint64_t rows, uint64_t cols,
                       uint64_t vmod, uint64_t* row, uint64_t* col, void* vals, hipStream_t s);
 uint64_t spmm_panel_cols(int dtype, uint64_t n_cols, uint64_t k);  // 0 = single pass

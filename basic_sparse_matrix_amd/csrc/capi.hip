@@ -301,6 +301,25 @@ int bsm_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, co
     return csr_from_inserts_device(dtype, rows, cols, n, dr.as<uint64_t>(), dc.as<uint64_t>(), dv.p, out, s);
 }
 
+int bsm_csr_from_coo(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                     const uint64_t* col, const void* vals, bsm_csr** out) {
+    BSM_REQUIRE(out && (n == 0 || (row && col && vals)), BSM_ERR_INVALID, "null argument");
+    const size_t es = dtype_size(dtype);
+    BSM_REQUIRE(es, BSM_ERR_INVALID, "unknown dtype %d", dtype);
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf dr, dc, dv;
+    BSM_TRY(dr.alloc((n ? n : 1) * sizeof(uint64_t)));
+    BSM_TRY(dc.alloc((n ? n : 1) * sizeof(uint64_t)));
+    BSM_TRY(dv.alloc((n ? n : 1) * es));
+    if (n) {
+        BSM_HIP_TRY(hipMemcpyAsync(dr.p, row, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        BSM_HIP_TRY(hipMemcpyAsync(dc.p, col, n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        BSM_HIP_TRY(hipMemcpyAsync(dv.p, vals, n * es, hipMemcpyHostToDevice, s));
+    }
+    return csr_from_coo_device(dtype, rows, cols, n, dr.as<uint64_t>(), dc.as<uint64_t>(), dv.p, out, s);
+}
+
 int bsm_dev_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
                              const uint64_t* col, const void* vals, bsm_csr** out, void* stream) {
     return csr_from_inserts_device(dtype, rows, cols, n, row, col, vals, out, static_cast<hipStream_t>(stream));

@@ -17,6 +17,7 @@
 // row_index pushes produce, including the repeated entries of skipped rows.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include "bsm_internal.hpp"
@@ -76,6 +77,38 @@ __global__ __launch_bounds__(256) void insert_stream_gen(uint64_t seed, uint64_t
 }
 
 unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// From<COO>: sort key (row << cb) | col and entry index; err |= 1 outside dims
+__global__ __launch_bounds__(256) void coo_keys(uint64_t n, uint64_t rows, uint64_t cols, unsigned cb,
+                                                const uint64_t* __restrict__ row, const uint64_t* __restrict__ col,
+                                                uint64_t* __restrict__ key, uint64_t* __restrict__ idx,
+                                                unsigned* __restrict__ err) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t r = row[i], c = col[i];
+    if (r >= rows || c >= cols) atomicOr(err, 1u);
+    key[i] = ((r < rows ? r : 0) << cb) | (c < cols ? c : 0);
+    idx[i] = i;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void coo_gather(uint64_t n, const uint64_t* __restrict__ perm,
+                                                  const uint64_t* __restrict__ row, const uint64_t* __restrict__ col,
+                                                  const T* __restrict__ v, uint64_t* __restrict__ srow,
+                                                  uint64_t* __restrict__ scol, T* __restrict__ sv) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t j = perm[i];
+    srow[i] = row[j];
+    scol[i] = col[j];
+    sv[i] = v[j];
+}
+
+unsigned bits_for(uint64_t x) {  // bits to hold values < x
+    unsigned b = 0;
+    while (b < 64 && (x - 1) >> b) ++b;
+    return b;
+}
 
 }  // namespace
 
@@ -174,6 +207,59 @@ int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n,
     if ((rc = csr_analyse(m, s)) != BSM_OK) return fail(rc);  // synchronises
     *out = m;
     return BSM_OK;
+}
+
+// From<COO<T>> for Csr<T> (sparse.rs:56-66): a STABLE sort by (row, col)
+// (Rust's sort_by is stable; rocPRIM's LSD radix sort is too), then the
+// insert sequence of csr_from_inserts_device (zero skip; sorted rows make
+// the running maximum the row itself). Entries outside dims are COO::insert's
+// Err(OutOfBounds) (sparse.rs:45-53), which the caller normally reports
+// before ever building the COO.
+int csr_from_coo_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                        const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s) {
+    BSM_REQUIRE(out && (n == 0 || (row && col && vals)), BSM_ERR_INVALID, "null argument");
+    const size_t es = dtype_size(dtype);
+    BSM_REQUIRE(es, BSM_ERR_INVALID, "unknown dtype %d", dtype);
+    if (n == 0) return csr_from_inserts_device(dtype, rows, cols, 0, row, col, vals, out, s);
+    const unsigned cb = bits_for(cols), rb = bits_for(rows);
+    BSM_REQUIRE(cb + rb <= 64, BSM_ERR_UNSUPPORTED, "COO: rows x cols too large for a 64-bit sort key");
+    DBuf key, key_s, idx, idx_s, err, srow, scol, sv, tmp;
+    BSM_TRY(key.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(key_s.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(idx.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(idx_s.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(err.alloc(sizeof(unsigned)));
+    BSM_HIP_TRY(hipMemsetAsync(err.p, 0, sizeof(unsigned), s));
+    coo_keys<<<grid_of(n), 256, 0, s>>>(n, rows, cols, cb, row, col, key.as<uint64_t>(), idx.as<uint64_t>(),
+                                        err.as<unsigned>());
+    BSM_HIP_TRY(hipGetLastError());
+    unsigned bad = 0;
+    BSM_HIP_TRY(hipMemcpyAsync(&bad, err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    if (bad) {
+        set_error("COO entry outside dims %llu x %llu (MatErr::OutOfBounds, sparse.rs:47-49)",
+                  (unsigned long long)rows, (unsigned long long)cols);
+        return BSM_ERR_OUT_OF_BOUNDS;
+    }
+    const unsigned end_bit = cb + rb > 0 ? cb + rb : 1;
+    size_t tmp_bytes = 0;
+    BSM_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key.as<uint64_t>(), key_s.as<uint64_t>(),
+                                          idx.as<uint64_t>(), idx_s.as<uint64_t>(), (size_t)n, 0u, end_bit, s));
+    BSM_TRY(tmp.alloc(tmp_bytes ? tmp_bytes : 1));
+    BSM_HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tmp_bytes, key.as<uint64_t>(), key_s.as<uint64_t>(),
+                                          idx.as<uint64_t>(), idx_s.as<uint64_t>(), (size_t)n, 0u, end_bit, s));
+    BSM_TRY(srow.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(scol.alloc(n * sizeof(uint64_t)));
+    BSM_TRY(sv.alloc(n * es));
+    BSM_TRY(dispatch_dtype(dtype, [&]<typename T>() -> int {
+        coo_gather<T><<<grid_of(n), 256, 0, s>>>(n, idx_s.as<uint64_t>(), row, col, static_cast<const T*>(vals),
+                                                 srow.as<uint64_t>(), scol.as<uint64_t>(), sv.as<T>());
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    }));
+    // csr_from_inserts_device synchronises before returning, so the sorted
+    // temporaries stay alive for as long as its kernels read them
+    return csr_from_inserts_device(dtype, rows, cols, n, srow.as<uint64_t>(), scol.as<uint64_t>(), sv.p, out, s);
 }
 
 }  // namespace bsm

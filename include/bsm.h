@@ -60,7 +60,8 @@ typedef enum bsm_status {
     BSM_ERR_HIP = 5,         /* HIP runtime error */
     BSM_ERR_OOM = 6,         /* device allocation failed */
     BSM_ERR_UNSUPPORTED = 7, /* valid input outside what this build implements */
-    BSM_ERR_NO_DEVICE = 8    /* no usable gfx950 device */
+    BSM_ERR_NO_DEVICE = 8,   /* no usable gfx950 device */
+    BSM_ERR_OUT_OF_BOUNDS = 9 /* MatErr::OutOfBounds (util.rs:54; COO::insert, sparse.rs:45-53) */
 } bsm_status;
 
 /* Opaque device-resident CSR matrix (a finalised Csr<T>, sparse.rs:68-78). */
@@ -93,6 +94,14 @@ int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz,
  * columns). Host arrays of n entries. */
 int bsm_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
                          const uint64_t* col, const void* vals, bsm_csr** out);
+/* From<COO<T>> for Csr<T> (sparse.rs:56-66): the n COO entries (row[i],
+ * col[i], vals[i]) in insert order, stably sorted by (row, col) (Rust's
+ * sort_by is stable), then inserted (zero skip) and finalised. The
+ * reference's per-entry println! is not reproduced. An entry outside dims
+ * (COO::insert would have returned Err(OutOfBounds)) -> BSM_ERR_OUT_OF_BOUNDS.
+ * Host arrays. */
+int bsm_csr_from_coo(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
+                     const uint64_t* col, const void* vals, bsm_csr** out);
 int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz,
                   int* dtype);
 /* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz). */

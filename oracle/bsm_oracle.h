@@ -67,11 +67,17 @@ enum {
  * the rows recorded so far (running max); finalise (sparse.rs:206-220)
  * panics ("big eek") when rows < row_index.len(), else pads to rows + 1.
  * Output: out_row (rows+1), out_col/out_v (capacity n); ORC_ERR_PANIC on
- * the finalise panic. */
+ * the finalise panic.
+ * orc_csr_from_coo: From<COO<T>> for Csr<T> (sparse.rs:56-66), a stable sort
+ * by (row, col) then the same insert sequence; an entry outside dims is
+ * COO::insert's Err(OutOfBounds) (sparse.rs:45-53) -> ORC_ERR_PANIC. */
 #define ORC_DECL_FROM_INSERTS(SUF, T)                                                      \
     int orc_csr_from_inserts_##SUF(uint64_t rows, uint64_t n, const uint64_t* row,         \
                                    const uint64_t* col, const T* v, uint64_t* out_row,     \
-                                   uint64_t* out_col, T* out_v, uint64_t* out_nnz);
+                                   uint64_t* out_col, T* out_v, uint64_t* out_nnz);        \
+    int orc_csr_from_coo_##SUF(uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row, \
+                               const uint64_t* col, const T* v, uint64_t* out_row,          \
+                               uint64_t* out_col, T* out_v, uint64_t* out_nnz);
 
 ORC_DECL_FROM_INSERTS(f64, double)
 ORC_DECL_FROM_INSERTS(f32, float)

@@ -253,3 +253,21 @@ def poisson2d(g):
     v = np.zeros(cap, dtype=np.float64)
     m = nnz(ctypes.c_uint64(g), _p(rp), _p(ci), _p(v))
     return rp, ci[:m].copy(), v[:m].copy()
+
+
+def csr_from_coo(rows, cols, row, col, v):
+    """From<COO<T>> for Csr<T> (sparse.rs:56-66) -> (row_index, col, v)."""
+    v = np.ascontiguousarray(v)
+    dt = v.dtype
+    r, c = _u64(row), _u64(col)
+    n = len(v)
+    out_row = np.zeros(rows + 1, dtype=np.uint64)
+    out_col = np.zeros(max(1, n), dtype=np.uint64)
+    out_v = np.zeros(max(1, n), dtype=dt)
+    nnz = ctypes.c_uint64(0)
+    fn = getattr(lib(), "orc_csr_from_coo_" + SUFFIX[dt])
+    rc = fn(ctypes.c_uint64(rows), ctypes.c_uint64(cols), ctypes.c_uint64(n), _p(r), _p(c), _p(v), _p(out_row),
+            _p(out_col), _p(out_v), ctypes.byref(nnz))
+    _check(rc)
+    m = nnz.value
+    return out_row, out_col[:m].copy(), out_v[:m].copy()

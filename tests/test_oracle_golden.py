@@ -203,3 +203,28 @@ def test_insert_stream_is_bench_shaped(orc):
     rp, ci, vv = orc.csr_from_inserts(1000, r, c, v.astype(np.uint32))
     lens = np.diff(rp.astype(np.int64))
     assert lens[-1] > 0.8 * len(vv) and len(vv) == int((v != 0).sum())
+
+
+# ---- From<COO<T>> for Csr<T> ----------------------------------------------
+def test_coo_to_csr_golden(orc, golden):
+    g = golden["coo_to_csr"]  # sparse.rs:1443-1468
+    r, c, v = (np.asarray(a) for a in zip(*g["inserts"]))
+    rows, cols = g["dims"]
+    o_rp, o_ci, o_v = orc.csr_from_coo(rows, cols, r.astype(np.uint64), c.astype(np.uint64), v.astype(np.float64))
+    _, _, e_rp, e_ci, e_v = csr_of(g["rows"], np.float64)
+    assert np.array_equal(o_rp, e_rp) and np.array_equal(o_ci, e_ci) and np.array_equal(o_v, e_v)
+
+
+def test_coo_sort_is_stable(orc):
+    """sort_by is stable: duplicates of one (row, col) keep insert order, so
+    the Csr holds them in that order (and mul_dense sums them in it)."""
+    r = np.array([2, 0, 2, 0, 1, 0], dtype=np.uint64)
+    c = np.array([1, 3, 1, 0, 2, 3], dtype=np.uint64)
+    v = np.array([10, 20, 30, 40, 0, 60], dtype=np.int32)  # the 0 is skipped at insert
+    rp, ci, vv = orc.csr_from_coo(3, 4, r, c, v)
+    assert rp.tolist() == [0, 3, 3, 5]
+    assert ci.tolist() == [0, 3, 3, 1, 1] and vv.tolist() == [40, 20, 60, 10, 30]
+    from oracle.pyoracle import OracleError
+
+    with pytest.raises(OracleError):
+        orc.csr_from_coo(3, 3, r, c, v)  # col 3 of 3: COO::insert's Err(OutOfBounds)
