@@ -88,6 +88,9 @@ SIGNATURES = [
     ("bsm_csr_mul_dense", _int, [_vp, _u64, _u64, _pp, ctypes.POINTER(_vp)]),
     ("bsm_csr_mul_vector", _int, [_vp, _vp, _u64, _vp, _u64]),
     ("bsm_csr_transpose", _int, [_vp, ctypes.POINTER(_vp)]),
+    ("bsm_csr_add_sparse", _int, [_vp, _vp, ctypes.POINTER(_vp)]),
+    ("bsm_csr_sub_sparse", _int, [_vp, _vp, ctypes.POINTER(_vp)]),
+    ("bsm_csr_mul_sparse", _int, [_vp, _vp, ctypes.POINTER(_vp)]),
     ("bsm_csr_cholesky", _int, [_vp, ctypes.POINTER(_vp)]),
     ("bsm_forward_substitution", _int, [_vp, _u64, _u64, _pp, _pp]),
     ("bsm_backward_substitution", _int, [_vp, _u64, _u64, _pp, _pp]),

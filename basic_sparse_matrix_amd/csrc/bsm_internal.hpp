@@ -180,6 +180,9 @@ int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* r
 // device construction from an insert sequence (kernels_build.hip)
 int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
                             const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s);
+// sparse x sparse (kernels_sparse.hip); synchronous
+int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr** out, hipStream_t s);
+int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipStream_t s);
 int csr_from_coo_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
                         const uint64_t* col, const void* vals, bsm_csr** out, hipStream_t s);
 int gen_insert_stream(int dtype, uint64_t seed, uint64_t i0, uint64_t n, uint64_t rows, uint64_t cols,

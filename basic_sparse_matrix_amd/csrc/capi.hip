@@ -426,6 +426,24 @@ int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void
     return rc;
 }
 
+int bsm_csr_add_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out) {
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    return sparse_addsub_dispatch(a, b, false, out, s);
+}
+
+int bsm_csr_sub_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out) {
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    return sparse_addsub_dispatch(a, b, true, out, s);
+}
+
+int bsm_csr_mul_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out) {
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    return sparse_mul_dispatch(a, b, out, s);
+}
+
 int bsm_csr_transpose(const bsm_csr* a, bsm_csr** out) {
     BSM_REQUIRE(a && out, BSM_ERR_INVALID, "null argument");
     hipStream_t s;

@@ -440,6 +440,35 @@ class Csr(GetDims):
         _raise_for(lib.bsm_csr_transpose(dev.handle, ctypes.byref(out)))
         return Csr._from_device(_lib.DeviceCsr(out.value))
 
+    def _sparse_binary(self, rhs: "Csr", fn_name: str) -> "Csr":
+        if not isinstance(rhs, Csr) or rhs.dtype != self.dtype:
+            raise TypeError(f"{fn_name}: Csr<{self.dtype}> with Csr<{getattr(rhs, 'dtype', None)}>")
+        a, b = self._device(), rhs._device()
+        lib = _lib.require_device()
+        out = ctypes.c_void_p()
+        _raise_for(getattr(lib, fn_name)(a.handle, b.handle, ctypes.byref(out)))
+        return Csr._from_device(_lib.DeviceCsr(out.value))
+
+    def add_sparse(self, rhs: "Csr") -> "Csr":
+        """sparse.rs:484-540 on the GPU: the reference's per-row merge in
+        storage order, zero sums dropped; Err(IncorrectDimensions) when the
+        dims differ (checked here first, as the reference does)."""
+        if self.get_dims() != rhs.get_dims():
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        return self._sparse_binary(rhs, "bsm_csr_add_sparse")
+
+    def sub_sparse(self, rhs: "Csr") -> "Csr":
+        """sparse.rs:542-599 (rhs-only entries become T::default() - v)."""
+        if self.get_dims() != rhs.get_dims():
+            raise MatErr(MatErrKind.IncorrectDimensions)
+        return self._sparse_binary(rhs, "bsm_csr_sub_sparse")
+
+    def mul_sparse(self, rhs: "Csr") -> "Csr":
+        """sparse.rs:601-635 on the GPU: dims (self.rows, rhs.cols), no
+        dimension check, every entry the reference's merge of a self row with
+        a row of rhs.transpose()."""
+        return self._sparse_binary(rhs, "bsm_csr_mul_sparse")
+
     def pair_with_tranpose(self):
         """sparse.rs:320-323."""
         return self, self.transpose()

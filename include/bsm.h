@@ -121,6 +121,17 @@ int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void
                        uint64_t out_len);
 /* Csr::transpose (sparse.rs:296-318): stable CSR -> CSC. */
 int bsm_csr_transpose(const bsm_csr* a, bsm_csr** out);
+/* Csr::add_sparse (sparse.rs:484-540) / Csr::sub_sparse (sparse.rs:542-599):
+ * the reference's per-row two-pointer merge over the operands' entries in
+ * storage order (rhs-only entries of sub become T::default() - v), zero
+ * results dropped. Dims differ -> BSM_ERR_DIMENSIONS; 0 rows -> BSM_ERR_PANIC
+ * (the reference's row loop never ends). Same dtype required. */
+int bsm_csr_add_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out);
+int bsm_csr_sub_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out);
+/* Csr::mul_sparse (sparse.rs:601-635): dims (a.rows, b.cols), no dimension
+ * check; every result entry is the reference's merge of a's row (storage
+ * order) with row j of b.transpose(), kept when nonzero. */
+int bsm_csr_mul_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out);
 /* impl Csr<f32>::cholesky_decomp (sparse.rs:682-714); F64 is this build's
  * addition. Square check -> BSM_ERR_NON_SQUARE. */
 int bsm_csr_cholesky(const bsm_csr* a, bsm_csr** out);

@@ -79,6 +79,28 @@ enum {
                                const uint64_t* col, const T* v, uint64_t* out_row,          \
                                uint64_t* out_col, T* out_v, uint64_t* out_nnz);
 
+/* ---- add_sparse / sub_sparse (sparse.rs:484-599), mul_sparse (:601-635) --
+ * Inputs are finalised CSRs (row arrays of rows+1). add/sub: out capacity
+ * a_nnz + b_nnz; ORC_ERR_INCORRECT_DIMENSIONS on a dims mismatch,
+ * ORC_ERR_PANIC for rows == 0 (the reference's row loop never ends). mul:
+ * out capacity rows * b_cols. */
+#define ORC_DECL_SPARSE_OPS(SUF, T)                                                                 \
+    int orc_addsub_sparse_##SUF(int sub, uint64_t rows, uint64_t cols, const uint64_t* a_row,        \
+                                const uint64_t* a_col, const T* a_v, uint64_t b_rows, uint64_t b_cols, \
+                                const uint64_t* b_row, const uint64_t* b_col, const T* b_v,          \
+                                uint64_t* out_row, uint64_t* out_col, T* out_v, uint64_t* out_nnz);  \
+    int orc_mul_sparse_##SUF(uint64_t rows, uint64_t cols, const uint64_t* a_row, const uint64_t* a_col, \
+                             const T* a_v, uint64_t b_rows, uint64_t b_cols, const uint64_t* b_row,    \
+                             const uint64_t* b_col, const T* b_v, uint64_t* out_row,                  \
+                             uint64_t* out_col, T* out_v, uint64_t* out_nnz);
+
+ORC_DECL_SPARSE_OPS(f64, double)
+ORC_DECL_SPARSE_OPS(f32, float)
+ORC_DECL_SPARSE_OPS(i32, int32_t)
+ORC_DECL_SPARSE_OPS(u32, uint32_t)
+ORC_DECL_SPARSE_OPS(i64, int64_t)
+ORC_DECL_SPARSE_OPS(u64, uint64_t)
+
 ORC_DECL_FROM_INSERTS(f64, double)
 ORC_DECL_FROM_INSERTS(f32, float)
 ORC_DECL_FROM_INSERTS(i32, int32_t)

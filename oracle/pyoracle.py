@@ -271,3 +271,38 @@ def csr_from_coo(rows, cols, row, col, v):
     _check(rc)
     m = nnz.value
     return out_row, out_col[:m].copy(), out_v[:m].copy()
+
+
+def _sparse_op(name, sub, a, b, cap):
+    (ar, ac, arp, aci, av), (br, bc, brp, bci, bv) = a, b
+    av = np.ascontiguousarray(av)
+    dt = av.dtype
+    bv = np.ascontiguousarray(bv, dtype=dt)
+    rows_out = ar
+    out_row = np.zeros(rows_out + 1, dtype=np.uint64)
+    out_col = np.zeros(max(1, cap), dtype=np.uint64)
+    out_v = np.zeros(max(1, cap), dtype=dt)
+    nnz = ctypes.c_uint64(0)
+    fn = getattr(lib(), name + SUFFIX[dt])
+    args = [ctypes.c_uint64(ar), ctypes.c_uint64(ac), _p(_u64(arp)), _p(_u64(aci)), _p(av), ctypes.c_uint64(br),
+            ctypes.c_uint64(bc), _p(_u64(brp)), _p(_u64(bci)), _p(bv), _p(out_row), _p(out_col), _p(out_v),
+            ctypes.byref(nnz)]
+    rc = fn(ctypes.c_int(sub), *args) if sub is not None else fn(*args)
+    _check(rc)
+    m = nnz.value
+    return out_row, out_col[:m].copy(), out_v[:m].copy()
+
+
+def add_sparse(a, b):
+    """Csr::add_sparse (sparse.rs:484-540). a, b: (rows, cols, row_index, col, v)."""
+    return _sparse_op("orc_addsub_sparse_", 0, a, b, len(a[4]) + len(b[4]))
+
+
+def sub_sparse(a, b):
+    """Csr::sub_sparse (sparse.rs:542-599)."""
+    return _sparse_op("orc_addsub_sparse_", 1, a, b, len(a[4]) + len(b[4]))
+
+
+def mul_sparse(a, b):
+    """Csr::mul_sparse (sparse.rs:601-635): dims (a.rows, b.cols)."""
+    return _sparse_op("orc_mul_sparse_", None, a, b, a[0] * b[1])

@@ -1,0 +1,124 @@
+"""GPU parity of the sparse x sparse operations:
+Csr::add_sparse / sub_sparse (src/sparse.rs:484-599) and Csr::mul_sparse
+(src/sparse.rs:601-635), against the reference's unit tests and the CPU
+oracle's literal restatement (oracle/, pinned in test_oracle_golden.py).
+Inputs include the reference benches' shapes (benches/sparse_dense_mul.rs
+ss_add, benches/sparse_sparse_mul.rs ss_mul: random insert order, so rows
+with unsorted and repeated columns), where the merge semantics matter.
+The bar is bit-exact.
+"""
+
+import numpy as np
+import pytest
+
+from basic_sparse_matrix_amd import Csr, MatErr, MatErrKind, Panic
+from test_gpu_spmm import assert_csr_bits
+
+pytestmark = pytest.mark.gpu
+
+
+def arrays(m: Csr):
+    return (m.dims.rows, m.dims.cols, np.asarray(m.row_index, np.uint64), np.asarray(m.col_index, np.uint64),
+            np.asarray(m.v))
+
+
+def test_add_sub_golden(golden):
+    for name, op in [("add_sparse", Csr.add_sparse), ("sub_sparse", Csr.sub_sparse)]:
+        g = golden[name]
+        assert op(Csr.from_data(g["a"]), Csr.from_data(g["b"])) == Csr.from_data(g["c"]), name
+
+
+def test_mul_sparse_golden(golden):
+    g = golden["sparse_multiplication"]
+    a = Csr.from_data(g["a"])
+    assert a.mul_sparse(a.transpose()) == Csr.from_data(g["c"])
+
+
+def test_errors():
+    a = Csr.from_data([[1, 2]])
+    with pytest.raises(MatErr) as e:
+        a.add_sparse(Csr.from_data([[1], [2]]))
+    assert e.value.kind == MatErrKind.IncorrectDimensions
+    with pytest.raises(MatErr):
+        a.sub_sparse(Csr.from_data([[1], [2]]))
+    with pytest.raises(Panic, match="big eek"):  # a 0-row Csr cannot even be finalised (sparse.rs:209-211)
+        Csr.new((0, 3)).finalise()
+    # mul_sparse has no dimension check: a (1 x 2) times a (1 x 2)
+    out = a.mul_sparse(Csr.from_data([[3, 4]]))
+    assert out.get_dims().rows == 1 and out.get_dims().cols == 2
+
+
+def sorted_random(rng, rows, cols, density, dtype):
+    if np.dtype(dtype).kind == "f":
+        d = rng.uniform(-2, 2, (rows, cols)).astype(dtype)
+    else:
+        d = rng.integers(1, 9, (rows, cols)).astype(dtype)
+    d[rng.random((rows, cols)) >= density] = 0
+    return Csr.from_data(d.tolist(), dtype=dtype)
+
+
+def unsorted_random(rng, e, rows, cols, dtype, seed_shift=0):
+    """Bench-shaped: e inserts in random (row, col) order -> running-max rows,
+    unsorted and repeated columns inside rows (sparse.rs:237-250)."""
+    r = rng.integers(0, rows, e).astype(np.uint64)
+    c = rng.integers(0, cols, e).astype(np.uint64)
+    if np.dtype(dtype).kind == "f":
+        v = rng.uniform(-3, 3, e).astype(dtype)
+    else:
+        v = rng.integers(0, 255, e).astype(dtype)
+    return Csr.from_inserts((rows, cols), r, c, v)
+
+
+DTYPES = [np.float64, np.float32, np.int32, np.uint32, np.int64, np.uint64]
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("kind", ["sorted", "unsorted"])
+def test_add_sub_vs_oracle(orc, dtype, kind):
+    rng = np.random.default_rng(11)
+    if kind == "sorted":
+        a, b = sorted_random(rng, 120, 90, 0.1, dtype), sorted_random(rng, 120, 90, 0.1, dtype)
+    else:
+        a, b = unsorted_random(rng, 20_000, 300, 200, dtype), unsorted_random(rng, 20_000, 300, 200, dtype)
+    assert_csr_bits(a.add_sparse(b), *orc.add_sparse(arrays(a), arrays(b)))
+    assert_csr_bits(a.sub_sparse(b), *orc.sub_sparse(arrays(a), arrays(b)))
+    assert_csr_bits(b.sub_sparse(a), *orc.sub_sparse(arrays(b), arrays(a)))
+
+
+def test_sub_exact_cancellation(orc):
+    """a - a: every stored value cancels exactly and is dropped (insert's zero
+    skip); rhs-only entries are T::default() - v."""
+    rng = np.random.default_rng(2)
+    a = sorted_random(rng, 50, 40, 0.2, np.float64)
+    z = a.sub_sparse(a)
+    assert z.get_nnz() == 0 and np.asarray(z.row_index).tolist() == [0] * 51
+    b = Csr.new((50, 40), dtype=np.float64).finalise()
+    assert_csr_bits(b.sub_sparse(a), *orc.sub_sparse(arrays(b), arrays(a)))
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(60, 45, 70), (200, 300, 150), (1, 1, 1)])
+def test_mul_sparse_sorted_vs_oracle(orc, dtype, shape):
+    rng = np.random.default_rng(sum(shape))
+    m, k, n = shape
+    a, b = sorted_random(rng, m, k, 0.08, dtype), sorted_random(rng, k, n, 0.08, dtype)
+    assert_csr_bits(a.mul_sparse(b), *orc.mul_sparse(arrays(a), arrays(b)))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint32, np.int64])
+@pytest.mark.parametrize("e", [1_000, 20_000, 100_000])
+def test_mul_sparse_bench_shape_vs_oracle(orc, dtype, e):
+    """ss_mul (sparse_sparse_mul.rs:6-37) shape at e inserts per operand:
+    1000 x 1000, random insert order (unsorted, repeated columns)."""
+    rng = np.random.default_rng(e)
+    a = unsorted_random(rng, e, 1000, 1000, dtype)
+    b = unsorted_random(rng, e, 1000, 1000, dtype)
+    assert_csr_bits(a.mul_sparse(b), *orc.mul_sparse(arrays(a), arrays(b)))
+
+
+def test_mul_sparse_rectangular_mismatch(orc):
+    """No dimension check in the reference: a.cols != b.rows still merges."""
+    rng = np.random.default_rng(9)
+    a = sorted_random(rng, 30, 50, 0.2, np.int32)
+    b = sorted_random(rng, 20, 40, 0.2, np.int32)
+    assert_csr_bits(a.mul_sparse(b), *orc.mul_sparse(arrays(a), arrays(b)))

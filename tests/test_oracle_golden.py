@@ -228,3 +228,38 @@ def test_coo_sort_is_stable(orc):
 
     with pytest.raises(OracleError):
         orc.csr_from_coo(3, 3, r, c, v)  # col 3 of 3: COO::insert's Err(OutOfBounds)
+
+
+# ---- add_sparse / sub_sparse / mul_sparse (sparse.rs:484-635) --------------
+def test_add_sub_sparse_golden(orc, golden):
+    for name, fn in [("add_sparse", orc.add_sparse), ("sub_sparse", orc.sub_sparse)]:
+        g = golden[name]
+        a, b = csr_of(g["a"], np.int32), csr_of(g["b"], np.int32)
+        o = fn(a, b)
+        e = csr_of(g["c"], np.int32)
+        assert np.array_equal(o[0], e[2]) and np.array_equal(o[1], e[3]) and np.array_equal(o[2], e[4]), name
+    from oracle.pyoracle import OracleError, ORC_ERR_INCORRECT_DIMENSIONS
+
+    with pytest.raises(OracleError) as ex:
+        orc.add_sparse(csr_of([[1, 2]], np.int32), csr_of([[1], [2]], np.int32))
+    assert ex.value.code == ORC_ERR_INCORRECT_DIMENSIONS
+
+
+def test_mul_sparse_golden(orc, golden):
+    g = golden["sparse_multiplication"]
+    a = csr_of(g["a"], np.int32)
+    t_rp, t_ci, t_v = orc.transpose(*a)
+    b = (a[1], a[0], t_rp, t_ci, t_v)
+    o = orc.mul_sparse(a, b)
+    e = csr_of(g["c"], np.int32)
+    assert np.array_equal(o[0], e[2]) and np.array_equal(o[1], e[3]) and np.array_equal(o[2], e[4])
+
+
+def test_mul_sparse_matches_dense_product(orc):
+    """Sorted, duplicate-free rows: the literal merge equals the dense product."""
+    rng = np.random.default_rng(5)
+    A = (rng.random((40, 30)) < 0.2) * rng.integers(-5, 6, (40, 30))
+    B = (rng.random((30, 25)) < 0.2) * rng.integers(-5, 6, (30, 25))
+    o = orc.mul_sparse(csr_of(A, np.int64), csr_of(B, np.int64))
+    e = csr_of(A @ B, np.int64)
+    assert np.array_equal(o[0], e[2]) and np.array_equal(o[1], e[3]) and np.array_equal(o[2], e[4])
