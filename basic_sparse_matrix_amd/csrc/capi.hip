@@ -78,7 +78,7 @@ int csr_analyse(bsm_csr* m, hipStream_t s) {
     uint64_t h[3] = {0, 0, 0};
     BSM_HIP_TRY(hipMemcpyAsync(h, out.p, sizeof(h), hipMemcpyDeviceToHost, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
-    BSM_REQUIRE(h[2] == 0, BSM_ERR_PANIC, "column index out of bounds in %llu row(s)",
+    BSM_REQUIRE(h[2] == 0, BSM_ERR_PANIC, "column index out of bounds in %llu entries",
                 (unsigned long long)h[2]);
     m->max_row_len = h[0];
     m->rows_sorted = (h[1] == 0);

@@ -10,6 +10,16 @@
 // entry is T::default() - v), each output through the zero-skipping insert.
 // One thread per row runs that merge twice: once to count the kept outputs
 // (then an exclusive scan gives row_ptr), once to write them.
+// Long rows (the benches' running-max rule piles ~all entries into one row,
+// with columns in random order) are cut into independent pieces first. Let
+// M be the largest column of the two rows: the merge never passes an M on
+// one side before pairing it with the next M of the other side (every other
+// value is smaller), so the k-th M of the self row pairs with the k-th M of
+// the rhs row, and the stretches between consecutive pairs merge on their
+// own, in order. Piece k = (self stretch k, rhs stretch k, the k-th M pair);
+// the last piece is the two tails (standard merge, M left over on at most one
+// side). Each piece is one thread's sequential merge; results are identical
+// to the whole-row merge (checked against the literal oracle).
 //
 // mul: the reference visits every (row, col) pair of the result and merges
 // the self row (storage order) with row `col` of rhs.transpose(); val starts
@@ -29,6 +39,8 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
 
+#include <vector>
+
 #include "bsm_internal.hpp"
 
 namespace bsm {
@@ -43,15 +55,14 @@ unsigned bits_for(uint64_t x) {  // bits to hold values < x
 }
 
 // ---- add / sub -------------------------------------------------------------
-// The merge of row r; emit(col, value) for every output the reference
-// inserts (zero results are dropped by the caller, like insert).
+// The reference's merge of self entries [ia, ea) with rhs entries [ib, eb);
+// emit(col, value) for every output it inserts (zero results are dropped by
+// the caller, like insert).
 template <typename T, bool SUB, typename F>
-__device__ __forceinline__ void merge_row(int64_t r, const int64_t* __restrict__ arp, const int32_t* __restrict__ acol,
-                                          const T* __restrict__ av, const int64_t* __restrict__ brp,
-                                          const int32_t* __restrict__ bcol, const T* __restrict__ bv, F&& emit) {
+__device__ __forceinline__ void merge_range(int64_t ia, int64_t ea, int64_t ib, int64_t eb,
+                                            const int32_t* __restrict__ acol, const T* __restrict__ av,
+                                            const int32_t* __restrict__ bcol, const T* __restrict__ bv, F&& emit) {
     using A = Arith<T>;
-    int64_t ia = arp[r], ib = brp[r];
-    const int64_t ea = arp[r + 1], eb = brp[r + 1];
     while (ia < ea || ib < eb) {
         if (ia < ea && ib < eb) {
             const int32_t ca = acol[ia], cb = bcol[ib];
@@ -76,16 +87,28 @@ __device__ __forceinline__ void merge_row(int64_t r, const int64_t* __restrict__
     }
 }
 
+constexpr int64_t PIECE_CAP = 2048;  // entries per side staged in LDS by piece_merge
+constexpr int64_t LONG_ROW = 2048;  // la + lb above this: cut the row into pieces (wave merges)
+
+__device__ __forceinline__ bool is_long(const int64_t* arp, const int64_t* brp, int64_t r) {
+    return (arp[r + 1] - arp[r]) + (brp[r + 1] - brp[r]) > LONG_ROW;
+}
+
 template <typename T, bool SUB>
 __global__ __launch_bounds__(256) void addsub_count(int64_t rows, const int64_t* __restrict__ arp,
                                                     const int32_t* __restrict__ acol, const T* __restrict__ av,
                                                     const int64_t* __restrict__ brp, const int32_t* __restrict__ bcol,
-                                                    const T* __restrict__ bv, int32_t* __restrict__ cnt) {
+                                                    const T* __restrict__ bv, int32_t* __restrict__ cnt,
+                                                    int32_t* __restrict__ long_flag) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
+    const bool lg = is_long(arp, brp, r);
+    long_flag[r] = lg ? 1 : 0;
     int32_t n = 0;
-    merge_row<T, SUB>(r, arp, acol, av, brp, bcol, bv, [&](int32_t, T v) { n += Arith<T>::nz(v) ? 1 : 0; });
-    cnt[r] = n;
+    if (!lg)
+        merge_range<T, SUB>(arp[r], arp[r + 1], brp[r], brp[r + 1], acol, av, bcol, bv,
+                            [&](int32_t, T v) { n += Arith<T>::nz(v) ? 1 : 0; });
+    cnt[r] = n;  // long rows: filled from their pieces
 }
 
 template <typename T, bool SUB>
@@ -95,15 +118,343 @@ __global__ __launch_bounds__(256) void addsub_fill(int64_t rows, const int64_t* 
                                                    const T* __restrict__ bv, const int64_t* __restrict__ orp,
                                                    int32_t* __restrict__ ocol, T* __restrict__ ov) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= rows) return;
+    if (r >= rows || is_long(arp, brp, r)) return;
     int64_t p = orp[r];
-    merge_row<T, SUB>(r, arp, acol, av, brp, bcol, bv, [&](int32_t c, T v) {
+    merge_range<T, SUB>(arp[r], arp[r + 1], brp[r], brp[r + 1], acol, av, bcol, bv, [&](int32_t c, T v) {
         if (Arith<T>::nz(v)) {
             ocol[p] = c;
             ov[p] = v;
             ++p;
         }
     });
+}
+
+// long rows ------------------------------------------------------------------
+struct Piece {
+    int64_t a0, a1, b0, b1;  // the two stretches
+    int64_t pa, pb;          // the M pair that closes the piece (-1: none, the tails)
+    int64_t row;
+};
+
+// Long-row setup, chunk-parallel: a long row's two sides are cut into
+// chunks of LR_CHUNK entries (listed on the host from the rows' extents).
+constexpr int64_t LR_CHUNK = 16384;
+
+struct LrChunk {
+    int64_t l;     // long-row index
+    int64_t side;  // 0: self row, 1: rhs row
+    int64_t b, e;  // entry range
+    int64_t off;   // occurrences of M in the earlier chunks of the same row side
+};
+
+// rank of `flag` within a 256-thread block, and the block total
+__device__ __forceinline__ int block_rank256(bool flag, int* wsum, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t m = __ballot(flag);
+    const int before = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+    __syncthreads();
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    return off + before;
+}
+
+__global__ __launch_bounds__(256) void long_extents(int64_t n_long, const int64_t* __restrict__ long_rows,
+                                                    const int64_t* __restrict__ arp, const int64_t* __restrict__ brp,
+                                                    int64_t* __restrict__ ext) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n_long) return;
+    const int64_t r = long_rows[l];
+    ext[4 * l + 0] = arp[r];
+    ext[4 * l + 1] = arp[r + 1];
+    ext[4 * l + 2] = brp[r];
+    ext[4 * l + 3] = brp[r + 1];
+}
+
+// MAX: mval[l] = max column over the chunks of row l; else the count of
+// mval[l] in each chunk
+template <bool MAX>
+__global__ __launch_bounds__(256) void chunk_reduce(const LrChunk* __restrict__ chunks, const int32_t* __restrict__ acol,
+                                                    const int32_t* __restrict__ bcol, int32_t* __restrict__ mval,
+                                                    int64_t* __restrict__ ccnt) {
+    __shared__ int red[256];
+    const LrChunk ch = chunks[blockIdx.x];
+    const int32_t* col = ch.side ? bcol : acol;
+    const int t = threadIdx.x;
+    const int M = MAX ? 0 : mval[ch.l];
+    int v = MAX ? -1 : 0;
+    for (int64_t e = ch.b + t; e < ch.e; e += 256) v = MAX ? max(v, col[e]) : v + (col[e] == M);
+    red[t] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s) red[t] = MAX ? max(red[t], red[t + s]) : red[t] + red[t + s];
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (MAX) atomicMax(&mval[ch.l], red[0]);
+        else ccnt[blockIdx.x] = red[0];
+    }
+}
+
+// the first and last piece of each long row, and every piece's row
+__global__ __launch_bounds__(256) void long_piece_init(int64_t n_long, const int64_t* __restrict__ long_rows,
+                                                       const int64_t* __restrict__ ext,
+                                                       const int64_t* __restrict__ pstart, Piece* __restrict__ pieces,
+                                                       int64_t* __restrict__ first_piece) {
+    const int64_t l = blockIdx.x;
+    const int64_t p0 = pstart[l], c = pstart[l + 1] - p0 - 1;
+    Piece* pc = pieces + p0;
+    if (threadIdx.x == 0) {
+        pc[0].a0 = ext[4 * l + 0];
+        pc[0].b0 = ext[4 * l + 2];
+        pc[c].a1 = ext[4 * l + 1];
+        pc[c].b1 = ext[4 * l + 3];
+        pc[c].pa = pc[c].pb = -1;
+    }
+    for (int64_t k = threadIdx.x; k <= c; k += blockDim.x) {
+        pc[k].row = long_rows[l];
+        first_piece[p0 + k] = p0;
+    }
+}
+
+// the k-th M of a side (k < c) closes piece k and opens piece k + 1
+__global__ __launch_bounds__(256) void chunk_pieces(const LrChunk* __restrict__ chunks, const int32_t* __restrict__ acol,
+                                                    const int32_t* __restrict__ bcol, const int32_t* __restrict__ mval,
+                                                    const int64_t* __restrict__ pstart, Piece* __restrict__ pieces) {
+    __shared__ int wsum[4];
+    const LrChunk ch = chunks[blockIdx.x];
+    const int32_t* col = ch.side ? bcol : acol;
+    const int M = mval[ch.l];
+    const int64_t p0 = pstart[ch.l], c = pstart[ch.l + 1] - p0 - 1;
+    Piece* pc = pieces + p0;
+    int64_t base = ch.off;
+    for (int64_t e0 = ch.b; e0 < ch.e && base < c; e0 += 256) {
+        const int64_t e = e0 + threadIdx.x;
+        const bool f = e < ch.e && col[e] == M;
+        int tot;
+        const int64_t k = base + block_rank256(f, wsum, &tot);
+        if (f && k < c) {
+            if (ch.side) {
+                pc[k].b1 = e;
+                pc[k].pb = e;
+                pc[k + 1].b0 = e + 1;
+            } else {
+                pc[k].a1 = e;
+                pc[k].pa = e;
+                pc[k + 1].a0 = e + 1;
+            }
+        }
+        base += tot;
+    }
+}
+
+__device__ __forceinline__ int32_t rl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ float rl(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint64_t rl(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int64_t rl(int64_t v, int l) { return (int64_t)rl((uint64_t)v, l); }
+__device__ __forceinline__ double rl(double v, int l) {
+    return __longlong_as_double((long long)rl((uint64_t)__double_as_longlong(v), l));
+}
+
+// One WAVE per piece. The merge itself is uniform scalar control flow: both
+// stretches are read 64 entries at a time into a lane window (next window
+// prefetched), the current entries come out with v_readlane, and the kept
+// outputs collect one per lane until 64 are stored at once. Outputs go to a
+// scratch slot at a0 + b0 (pieces' slots never overlap: a piece emits at
+// most its two lengths plus one pair); piece_copy moves them into place.
+template <typename T, bool SUB>
+__global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ pieces, const int32_t* __restrict__ acol,
+                                                  const T* __restrict__ av, const int32_t* __restrict__ bcol,
+                                                  const T* __restrict__ bv, int32_t* __restrict__ tcol,
+                                                  T* __restrict__ tval, int32_t* __restrict__ pcnt) {
+    using A = Arith<T>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char piece_sm[];
+    int32_t* sac = reinterpret_cast<int32_t*>(piece_sm);
+    int32_t* sbc = sac + PIECE_CAP;
+    T* sav = reinterpret_cast<T*>(sbc + PIECE_CAP);
+    T* sbv = sav + PIECE_CAP;
+    const int lane = threadIdx.x;
+    const Piece pc = pieces[blockIdx.x];
+    const int64_t ea = pc.a1, eb = pc.b1;
+    int64_t ia = pc.a0, ib = pc.b0, wa = pc.a0, wb = pc.b0;
+    // stage both stretches in LDS when they fit: the windows then refill from
+    // LDS instead of waiting on global memory every 64 steps
+    const bool staged = ea - pc.a0 <= PIECE_CAP && eb - pc.b0 <= PIECE_CAP;
+    if (staged) {
+        for (int64_t i = lane; i < ea - pc.a0; i += 64) {
+            sac[i] = acol[pc.a0 + i];
+            sav[i] = av[pc.a0 + i];
+        }
+        for (int64_t i = lane; i < eb - pc.b0; i += 64) {
+            sbc[i] = bcol[pc.b0 + i];
+            sbv[i] = bv[pc.b0 + i];
+        }
+        __syncthreads();
+    }
+    auto load = [&](bool side_b, int64_t base, int32_t& c, T& x) {
+        const int64_t s0 = side_b ? pc.b0 : pc.a0, end = side_b ? eb : ea;
+        const int64_t e = base + lane < end ? base + lane : (end > s0 ? end - 1 : s0);
+        if (staged) {
+            c = side_b ? sbc[e - s0] : sac[e - s0];
+            x = side_b ? sbv[e - s0] : sav[e - s0];
+        } else {
+            c = side_b ? bcol[e] : acol[e];
+            x = side_b ? bv[e] : av[e];
+        }
+    };
+    int32_t caw, can, cbw, cbn;
+    T vaw, van, vbw, vbn;
+    if (ea > pc.a0) { load(false, wa, caw, vaw); load(false, wa + 64, can, van); }
+    if (eb > pc.b0) { load(true, wb, cbw, vbw); load(true, wb + 64, cbn, vbn); }
+    int64_t o = pc.a0 + pc.b0;
+    int nbuf = 0;
+    int32_t cnt = 0, oc = 0;
+    T ov = A::zero();
+    auto emit = [&](int32_t c, T v) {
+        if (A::nz(v)) {
+            if (lane == nbuf) {
+                oc = c;
+                ov = v;
+            }
+            ++cnt;
+            if (++nbuf == 64) {
+                tcol[o + lane] = oc;
+                tval[o + lane] = ov;
+                o += 64;
+                nbuf = 0;
+            }
+        }
+    };
+    while (ia < ea && ib < eb) {
+        if (ia - wa == 64) {
+            wa += 64;
+            caw = can;
+            vaw = van;
+            if (wa + 64 < ea) load(false, wa + 64, can, van);
+        }
+        if (ib - wb == 64) {
+            wb += 64;
+            cbw = cbn;
+            vbw = vbn;
+            if (wb + 64 < eb) load(true, wb + 64, cbn, vbn);
+        }
+        const int32_t ca = rl(caw, (int)(ia - wa)), cb = rl(cbw, (int)(ib - wb));
+        if (ca > cb) {
+            const T x = rl(vbw, (int)(ib - wb));
+            emit(cb, SUB ? A::sub(A::zero(), x) : x);
+            ++ib;
+        } else if (ca < cb) {
+            emit(ca, rl(vaw, (int)(ia - wa)));
+            ++ia;
+        } else {
+            const T x = rl(vaw, (int)(ia - wa)), y = rl(vbw, (int)(ib - wb));
+            emit(ca, SUB ? A::sub(x, y) : A::add(x, y));
+            ++ia;
+            ++ib;
+        }
+    }
+    // one side is exhausted: the rest of the other side goes out in order,
+    // 64 entries per step (ballot compaction of the kept ones)
+    if (ia < ea || ib < eb) {
+        if (lane < nbuf) {
+            tcol[o + lane] = oc;
+            tval[o + lane] = ov;
+        }
+        o += nbuf;
+        nbuf = 0;
+        const bool side_b = ib < eb;
+        const int64_t s0 = side_b ? ib : ia, s1 = side_b ? eb : ea;
+        const int32_t* col = side_b ? bcol : acol;
+        const T* val = side_b ? bv : av;
+        for (int64_t base = s0; base < s1; base += 64) {
+            const int64_t e = base + lane;
+            const bool valid = e < s1;
+            T x = valid ? val[e] : A::zero();
+            if (SUB && side_b) x = A::sub(A::zero(), x);
+            const bool keep = valid && A::nz(x);
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const int r = __popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+                tcol[o + r] = col[e];
+                tval[o + r] = x;
+            }
+            o += __popcll(m);
+            cnt += __popcll(m);
+        }
+    }
+    if (pc.pa >= 0) {
+        const T x = av[pc.pa], y = bv[pc.pb];
+        emit(acol[pc.pa], SUB ? A::sub(x, y) : A::add(x, y));
+    }
+    if (lane < nbuf) {
+        tcol[o + lane] = oc;
+        tval[o + lane] = ov;
+    }
+    if (lane == 0) pcnt[blockIdx.x] = cnt;
+}
+
+// one wave per piece: scratch slot -> the output rows
+template <typename T>
+__global__ __launch_bounds__(64) void piece_copy(const Piece* __restrict__ pieces, const int32_t* __restrict__ pcnt,
+                                                 const int64_t* __restrict__ poff,
+                                                 const int64_t* __restrict__ first_piece,
+                                                 const int64_t* __restrict__ orp, const int32_t* __restrict__ tcol,
+                                                 const T* __restrict__ tval, int32_t* __restrict__ ocol,
+                                                 T* __restrict__ ov) {
+    const int64_t p = blockIdx.x;
+    const Piece pc = pieces[p];
+    const int64_t src = pc.a0 + pc.b0, dst = orp[pc.row] + (poff[p] - poff[first_piece[p]]);
+    const int32_t n = pcnt[p];
+    for (int32_t i = threadIdx.x; i < n; i += 64) {
+        ocol[dst + i] = tcol[src + i];
+        ov[dst + i] = tval[src + i];
+    }
+}
+
+// output count of each long row = the sum of its pieces' counts
+__global__ __launch_bounds__(256) void long_row_totals(int64_t n_long, const int64_t* __restrict__ long_rows,
+                                                       const int64_t* __restrict__ pstart,
+                                                       const int64_t* __restrict__ poff, int32_t* __restrict__ cnt) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n_long) return;
+    cnt[long_rows[l]] = (int32_t)(poff[pstart[l + 1]] - poff[pstart[l]]);
+}
+
+template <typename T, bool SUB>
+__global__ __launch_bounds__(256) void piece_fill(int64_t n, const Piece* __restrict__ pieces,
+                                                  const int32_t* __restrict__ acol, const T* __restrict__ av,
+                                                  const int32_t* __restrict__ bcol, const T* __restrict__ bv,
+                                                  const int64_t* __restrict__ poff, const int64_t* __restrict__ first_piece,
+                                                  const int64_t* __restrict__ orp, int32_t* __restrict__ ocol,
+                                                  T* __restrict__ ov) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const Piece pc = pieces[p];
+    int64_t q = orp[pc.row] + (poff[p] - poff[first_piece[p]]);
+    auto put = [&](int32_t c, T v) {
+        if (Arith<T>::nz(v)) {
+            ocol[q] = c;
+            ov[q] = v;
+            ++q;
+        }
+    };
+    merge_range<T, SUB>(pc.a0, pc.a1, pc.b0, pc.b1, acol, av, bcol, bv, put);
+    if (pc.pa >= 0) put(acol[pc.pa], SUB ? Arith<T>::sub(av[pc.pa], bv[pc.pb]) : Arith<T>::add(av[pc.pa], bv[pc.pb]));
+}
+
+__global__ __launch_bounds__(256) void compact_flags(int64_t rows, const int32_t* __restrict__ flag,
+                                                     const int64_t* __restrict__ pos, int64_t* __restrict__ list) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < rows && flag[r]) list[pos[r]] = r;
 }
 
 // ---- mul -------------------------------------------------------------------
@@ -217,40 +568,118 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                 "%s on a matrix with 0 rows: the reference's row loop never terminates (sparse.rs:%s)",
                 sub ? "sub_sparse" : "add_sparse", sub ? "593-596" : "533-537");
     const uint64_t rows = a->rows;
-    DBuf cnt, ws;
+    DBuf cnt, lflag, lpos, ws;
     CsrGuard g;
     BSM_TRY(cnt.alloc(rows * sizeof(int32_t)));
+    BSM_TRY(lflag.alloc(rows * sizeof(int32_t)));
+    BSM_TRY(lpos.alloc((rows + 1) * sizeof(int64_t)));
     BSM_TRY(ws.alloc(scan_workspace_bytes(rows)));
     DBuf orp;
     BSM_TRY(orp.alloc((rows + 1) * sizeof(int64_t)));
-    auto run = [&]<typename T>() -> int {
+    auto run = [&]<typename T, bool SUB>() -> int {
         const T* av = static_cast<const T*>(a->vals);
         const T* bv = static_cast<const T*>(b->vals);
-        if (sub)
-            addsub_count<T, true><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr,
-                                                                 b->col, bv, cnt.as<int32_t>());
-        else
-            addsub_count<T, false><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr,
-                                                                  b->col, bv, cnt.as<int32_t>());
+        addsub_count<T, SUB><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr, b->col,
+                                                           bv, cnt.as<int32_t>(), lflag.as<int32_t>());
         BSM_HIP_TRY(hipGetLastError());
+        // long rows: list, pieces, piece counts
+        BSM_TRY(exclusive_scan_i32_to_i64(lflag.as<int32_t>(), lpos.as<int64_t>(), rows, ws.p, ws.bytes, s));
+        int64_t n_long = 0;
+        BSM_HIP_TRY(hipMemcpyAsync(&n_long, lpos.as<int64_t>() + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        DBuf long_rows, mval, pstart, pieces, pcnt, poff, first, ws2, tcol, tval;
+        int64_t n_pieces = 0;
+        if (n_long) {
+            BSM_TRY(long_rows.alloc(n_long * sizeof(int64_t)));
+            BSM_TRY(mval.alloc(n_long * sizeof(int32_t)));
+            BSM_TRY(pstart.alloc((n_long + 1) * sizeof(int64_t)));
+            DBuf ext;
+            BSM_TRY(ext.alloc(4 * n_long * sizeof(int64_t)));
+            compact_flags<<<grid_of(rows), 256, 0, s>>>((int64_t)rows, lflag.as<int32_t>(), lpos.as<int64_t>(),
+                                                        long_rows.as<int64_t>());
+            long_extents<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), a->row_ptr, b->row_ptr,
+                                                         ext.as<int64_t>());
+            BSM_HIP_TRY(hipGetLastError());
+            std::vector<int64_t> hx(4 * n_long);
+            BSM_HIP_TRY(hipMemcpyAsync(hx.data(), ext.p, hx.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            BSM_HIP_TRY(hipStreamSynchronize(s));
+            std::vector<LrChunk> hc;
+            for (int64_t l = 0; l < n_long; ++l)
+                for (int64_t side = 0; side < 2; ++side)
+                    for (int64_t b0 = hx[4 * l + 2 * side]; b0 < hx[4 * l + 2 * side + 1]; b0 += LR_CHUNK)
+                        hc.push_back({l, side, b0, std::min(b0 + LR_CHUNK, hx[4 * l + 2 * side + 1]), 0});
+            const int64_t n_chunks = (int64_t)hc.size();
+            DBuf chunks, ccnt;
+            BSM_TRY(chunks.alloc((n_chunks ? n_chunks : 1) * sizeof(LrChunk)));
+            BSM_TRY(ccnt.alloc((n_chunks ? n_chunks : 1) * sizeof(int64_t)));
+            BSM_HIP_TRY(hipMemsetAsync(mval.p, 0xff, n_long * sizeof(int32_t), s));  // -1
+            std::vector<int64_t> hcnt(n_chunks);
+            if (n_chunks) {
+                BSM_HIP_TRY(hipMemcpyAsync(chunks.p, hc.data(), n_chunks * sizeof(LrChunk), hipMemcpyHostToDevice, s));
+                chunk_reduce<true><<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col,
+                                                                      mval.as<int32_t>(), nullptr);
+                chunk_reduce<false><<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col,
+                                                                       mval.as<int32_t>(), ccnt.as<int64_t>());
+                BSM_HIP_TRY(hipGetLastError());
+                BSM_HIP_TRY(hipMemcpyAsync(hcnt.data(), ccnt.p, n_chunks * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+                BSM_HIP_TRY(hipStreamSynchronize(s));  // hc (host) is read by the copy above
+            }
+            // M pairs per row: min of the two sides' counts; chunk offsets
+            std::vector<int64_t> cnt_side(2 * n_long, 0), ps(n_long + 1, 0);
+            for (int64_t i = 0; i < n_chunks; ++i) {
+                hc[i].off = cnt_side[2 * hc[i].l + hc[i].side];
+                cnt_side[2 * hc[i].l + hc[i].side] += hcnt[i];
+            }
+            for (int64_t l = 0; l < n_long; ++l) ps[l + 1] = ps[l] + std::min(cnt_side[2 * l], cnt_side[2 * l + 1]) + 1;
+            n_pieces = ps[n_long];
+            BSM_HIP_TRY(hipMemcpyAsync(pstart.p, ps.data(), (n_long + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            BSM_TRY(pieces.alloc(n_pieces * sizeof(Piece)));
+            BSM_TRY(pcnt.alloc(n_pieces * sizeof(int32_t)));
+            BSM_TRY(poff.alloc((n_pieces + 1) * sizeof(int64_t)));
+            BSM_TRY(first.alloc(n_pieces * sizeof(int64_t)));
+            BSM_TRY(ws2.alloc(scan_workspace_bytes(n_pieces)));
+            long_piece_init<<<(unsigned)n_long, 256, 0, s>>>(n_long, long_rows.as<int64_t>(), ext.as<int64_t>(),
+                                                             pstart.as<int64_t>(), pieces.as<Piece>(),
+                                                             first.as<int64_t>());
+            if (n_chunks) {
+                BSM_HIP_TRY(hipMemcpyAsync(chunks.p, hc.data(), n_chunks * sizeof(LrChunk), hipMemcpyHostToDevice, s));
+                chunk_pieces<<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col, mval.as<int32_t>(),
+                                                                pstart.as<int64_t>(), pieces.as<Piece>());
+            }
+            BSM_HIP_TRY(hipGetLastError());
+            BSM_HIP_TRY(hipStreamSynchronize(s));  // ps / hc (host) are read by the copies above
+            BSM_TRY(tcol.alloc((a->nnz + b->nnz + 1) * sizeof(int32_t)));
+            BSM_TRY(tval.alloc((a->nnz + b->nnz + 1) * sizeof(T)));
+            BSM_REQUIRE(n_pieces < (1ll << 31), BSM_ERR_UNSUPPORTED, "too many pieces");
+            piece_merge<T, SUB><<<(unsigned)n_pieces, 64, 2 * PIECE_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(pieces.as<Piece>(), a->col, av, b->col, bv,
+                                                                  tcol.as<int32_t>(), tval.as<T>(), pcnt.as<int32_t>());
+            BSM_HIP_TRY(hipGetLastError());
+            BSM_TRY(exclusive_scan_i32_to_i64(pcnt.as<int32_t>(), poff.as<int64_t>(), n_pieces, ws2.p, ws2.bytes, s));
+            long_row_totals<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), pstart.as<int64_t>(),
+                                                             poff.as<int64_t>(), cnt.as<int32_t>());
+            BSM_HIP_TRY(hipGetLastError());
+        }
         BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), orp.as<int64_t>(), rows, ws.p, ws.bytes, s));
         int64_t nnz = 0;
         BSM_HIP_TRY(hipMemcpyAsync(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, (uint64_t)nnz));
         BSM_HIP_TRY(hipMemcpyAsync(g.m->row_ptr, orp.p, (rows + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-        if (sub)
-            addsub_fill<T, true><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr,
-                                                                b->col, bv, orp.as<int64_t>(), g.m->col,
-                                                                static_cast<T*>(g.m->vals));
-        else
-            addsub_fill<T, false><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr,
-                                                                 b->col, bv, orp.as<int64_t>(), g.m->col,
-                                                                 static_cast<T*>(g.m->vals));
+        addsub_fill<T, SUB><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr, b->col,
+                                                          bv, orp.as<int64_t>(), g.m->col, static_cast<T*>(g.m->vals));
         BSM_HIP_TRY(hipGetLastError());
+        if (n_pieces) {
+            piece_copy<T><<<(unsigned)n_pieces, 64, 0, s>>>(pieces.as<Piece>(), pcnt.as<int32_t>(), poff.as<int64_t>(),
+                                                            first.as<int64_t>(), orp.as<int64_t>(), tcol.as<int32_t>(),
+                                                            tval.as<T>(), g.m->col, static_cast<T*>(g.m->vals));
+            BSM_HIP_TRY(hipGetLastError());
+        }
+        BSM_HIP_TRY(hipStreamSynchronize(s));  // the piece buffers die with this scope
         return BSM_OK;
     };
-    BSM_TRY(dispatch_dtype(a->dtype, run));
+    BSM_TRY(dispatch_dtype(a->dtype, [&]<typename T>() -> int {
+        return sub ? run.template operator()<T, true>() : run.template operator()<T, false>();
+    }));
     BSM_TRY(csr_analyse(g.m, s));  // synchronises
     *out = g.release();
     return BSM_OK;

@@ -591,24 +591,37 @@ int launch_transpose_tiles(const T* in, T* out, uint64_t in_rows, uint64_t in_co
 // what mul_vector's transpose-based sum uses, sparse.rs:474-479).
 // out3 = {max_row_len, unsorted_rows, bad_col (col >= cols or < 0)}.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void analyse_rows(const int64_t* __restrict__ rp,
-                                                    const int32_t* __restrict__ col, int64_t rows,
-                                                    int64_t cols, unsigned long long* out3) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
-    if (row >= rows) return;
-    const int64_t a = rp[row], b = rp[row + 1];
-    bool unsorted = false, bad = false;
-    for (int64_t e = a + lane; e < b; e += WAVE) {
-        const int32_t c = col[e];
-        if (c < 0 || c >= cols) bad = true;
-        if (e > a && col[e - 1] > c) unsorted = true;
-    }
-    const bool any_uns = __any(unsorted), any_bad = __any(bad);
-    if (lane == 0) {
+// Matrix analysis, nnz-parallel (a wave per row serialised on the benches'
+// one-huge-row matrices): per row the length (max) and a row-start bit;
+// per entry the column bound and a descent against the previous entry of
+// the same row (not a row start). out3 = {max row length, descents (> 0:
+// some row is unsorted), out-of-bounds columns}.
+__global__ __launch_bounds__(256) void analyse_row_starts(const int64_t* __restrict__ rp, int64_t rows,
+                                                          unsigned* __restrict__ start_bits,
+                                                          unsigned long long* __restrict__ out3) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int64_t a = rp[r], b = rp[r + 1];
+    if (b > a) {
         atomicMax(&out3[0], (unsigned long long)(b - a));
-        if (any_uns) atomicAdd(&out3[1], 1ull);
-        if (any_bad) atomicAdd(&out3[2], 1ull);
+        atomicOr(&start_bits[a >> 5], 1u << (a & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void analyse_entries(const int32_t* __restrict__ col, int64_t nnz, int64_t cols,
+                                                       const unsigned* __restrict__ start_bits,
+                                                       unsigned long long* __restrict__ out3) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false, desc = false;
+    if (e < nnz) {
+        const int32_t c = col[e];
+        bad = c < 0 || c >= cols;
+        desc = e > 0 && !((start_bits[e >> 5] >> (e & 31)) & 1u) && col[e - 1] > c;
+    }
+    const uint64_t mb = __ballot(bad), md = __ballot(desc);
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        if (md) atomicAdd(&out3[1], (unsigned long long)__popcll(md));
+        if (mb) atomicAdd(&out3[2], (unsigned long long)__popcll(mb));
     }
 }
 
@@ -1036,9 +1049,19 @@ int analyse_dispatch(const int64_t* rp, const int32_t* col, uint64_t rows, uint6
                      uint64_t* d_out3, hipStream_t s) {
     BSM_HIP_TRY(hipMemsetAsync(d_out3, 0, 3 * sizeof(uint64_t), s));
     if (rows == 0) return BSM_OK;
-    analyse_rows<<<grid1d(rows, 4), 256, 0, s>>>(rp, col, (int64_t)rows, (int64_t)cols,
-                                                 reinterpret_cast<unsigned long long*>(d_out3));
+    int64_t nnz = 0;
+    BSM_HIP_TRY(hipMemcpyAsync(&nnz, rp + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    DBuf bits;
+    const uint64_t words = (uint64_t)nnz / 32 + 1;
+    BSM_TRY(bits.alloc(words * sizeof(unsigned)));
+    BSM_HIP_TRY(hipMemsetAsync(bits.p, 0, words * sizeof(unsigned), s));
+    auto out3 = reinterpret_cast<unsigned long long*>(d_out3);
+    analyse_row_starts<<<grid1d(rows, 256), 256, 0, s>>>(rp, (int64_t)rows, bits.as<unsigned>(), out3);
+    if (nnz > 0)
+        analyse_entries<<<grid1d((uint64_t)nnz, 256), 256, 0, s>>>(col, nnz, (int64_t)cols, bits.as<unsigned>(), out3);
     BSM_HIP_TRY(hipGetLastError());
+    BSM_HIP_TRY(hipStreamSynchronize(s));  // bits dies here
     return BSM_OK;
 }
 

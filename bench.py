@@ -97,50 +97,86 @@ def bench_x_cols(seed, k, n, fill, dtype=np.uint32):
     return cols
 
 
-def sd_mul_suite(iters=20):
-    """The reference's own criterion bench `sd_mul` (sparse_dense_mul.rs:6-35):
-    Csr<u32> 1000 x 1000 built by e random inserts (e = 100k .. 900k), times a
-    10-column Dense<u32> with e/100 random entries; throughput in criterion's
-    unit, elements = e per call. GPU: the public Csr.mul_dense call end to end
-    (X upload, nnz-balanced integer SpMM, compaction, download), the matrix
-    built on the device by the insert-sequence builder. CPU: the oracle's
-    restatement of mul_dense (1 thread) on the same matrix and RHS. The insert
-    stream is bsm_synth.h's SplitMix64 (StdRng is not vendored), same shape."""
+def _time_call(fn, iters, warm=3):
+    for _ in range(warm):
+        out = fn()
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return out, float(np.median(ts))
+
+
+def _same(out, ref):
+    e_rp, e_ci, e_v = ref
+    return bool(np.array_equal(np.asarray(out.row_index, np.uint64), e_rp)
+                and np.array_equal(np.asarray(out.col_index, np.uint64), e_ci)
+                and np.array_equal(np.asarray(out.v), e_v))
+
+
+def ref_bench_suite(iters=20, which=("sd_mul", "ss_add", "ss_mul")):
+    """The reference's own criterion benches, one JSON line per size:
+      sd_mul (sparse_dense_mul.rs:6-35): Csr<u32> 1000 x 1000 from e random
+        inserts x a 10-column Dense<u32> with e/100 random entries;
+      ss_add (sparse_dense_mul.rs:37-67): two such Csr<u32>, add_sparse;
+      ss_mul (sparse_sparse_mul.rs:6-37): two such Csr<u32>, mul_sparse.
+    criterion's throughput unit is elements = e per call. GPU: the public
+    Csr call end to end (uploads, kernels, download), the matrices built on
+    the device by the insert-sequence builder. CPU: the oracle's restatement
+    of the same call (1 thread) on the same inputs, which is also the check
+    (bit_exact_vs_oracle). The insert streams come from bsm_synth.h's
+    SplitMix64 (StdRng is not vendored), with the benches' shapes."""
     from basic_sparse_matrix_amd import Dense
     from basic_sparse_matrix_amd.device import csr_from_device_inserts, gen_insert_stream
     from oracle import pyoracle as orc
 
-    for i in range(9):
-        e = 10000 * (i + 1) * 10
-        r, c, v = gen_insert_stream(SEED_A, e, 1000, 1000, 255, np.uint32)
-        a = csr_from_device_inserts((1000, 1000), r, c, v)
-        x_cols = bench_x_cols(SEED_X + e, 10, 1000, e // 100)
-        x = Dense.from_columns(x_cols)
-        for _ in range(3):
-            out = a.mul_dense(x)
-        ts = []
-        for _ in range(iters):
-            t0 = time.perf_counter()
-            out = a.mul_dense(x)
-            ts.append(time.perf_counter() - t0)
-        gpu_s = float(np.median(ts))
-        rp, ci, vv = np.asarray(a.row_index), np.asarray(a.col_index), np.asarray(a.v)
-        cts = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            e_rp, e_ci, e_v = orc.mul_dense(1000, 1000, rp, ci, vv, x_cols)
-            cts.append(time.perf_counter() - t0)
-        cpu_s = float(np.median(cts))
-        ok = (np.array_equal(np.asarray(out.row_index, np.uint64), e_rp)
-              and np.array_equal(np.asarray(out.col_index, np.uint64), e_ci) and np.array_equal(np.asarray(out.v), e_v))
-        print(json.dumps({
-            "workload": "sd_mul (benches/sparse_dense_mul.rs:6-35)", "elements": e, "dtype": "u32",
-            "a_nnz": int(len(vv)), "longest_row": int(np.diff(rp.astype(np.int64)).max()), "k": 10,
-            "gpu_ms_per_call": round(gpu_s * 1e3, 4), "gpu_elements_per_s": round(e / gpu_s, 1),
-            "cpu_ms_per_call": round(cpu_s * 1e3, 4), "cpu_elements_per_s": round(e / cpu_s, 1),
-            "cpu_kind": "port (oracle mul_dense, 1 thread)", "gpu_over_cpu": round(cpu_s / gpu_s, 2),
-            "out_nnz": int(out.get_nnz()), "bit_exact_vs_oracle": bool(ok),
-        }), flush=True)
+    def build(seed, e):
+        r, c, v = gen_insert_stream(seed, e, 1000, 1000, 255, np.uint32)
+        return csr_from_device_inserts((1000, 1000), r, c, v)
+
+    def arrays(m):
+        return (1000, 1000, np.asarray(m.row_index, np.uint64), np.asarray(m.col_index, np.uint64),
+                np.asarray(m.v))
+
+    sizes = {
+        "sd_mul": [10000 * (i + 1) * 10 for i in range(9)],
+        "ss_add": [10000 * (i + 1) * 10 for i in range(9)],
+        "ss_mul": [i * 50 for i in [1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 10000]],
+    }
+    cite = {"sd_mul": "benches/sparse_dense_mul.rs:6-35", "ss_add": "benches/sparse_dense_mul.rs:37-67",
+            "ss_mul": "benches/sparse_sparse_mul.rs:6-37"}
+    for name in which:
+        for e in sizes[name]:
+            a = build(SEED_A, e)
+            if name == "sd_mul":
+                x_cols = bench_x_cols(SEED_X + e, 10, 1000, e // 100)
+                x = Dense.from_columns(x_cols)
+                out, gpu_s = _time_call(lambda: a.mul_dense(x), iters)
+                ra = arrays(a)
+                cpu = lambda: orc.mul_dense(1000, 1000, ra[2], ra[3], ra[4], x_cols)  # noqa: E731
+                extra = {"k": 10, "longest_row": int(np.diff(ra[2].astype(np.int64)).max())}
+            else:
+                b = build(SEED_X, e)
+                op = a.add_sparse if name == "ss_add" else a.mul_sparse
+                out, gpu_s = _time_call(lambda: op(b), iters if name == "ss_add" or e <= 100_000 else 5)
+                ra, rb = arrays(a), arrays(b)
+                cpu_fn = orc.add_sparse if name == "ss_add" else orc.mul_sparse
+                cpu = lambda: cpu_fn(ra, rb)  # noqa: E731
+                extra = {"b_nnz": int(b.get_nnz())}
+            cts = []
+            for _ in range(3 if name != "ss_mul" or e <= 100_000 else 1):
+                t0 = time.perf_counter()
+                ref = cpu()
+                cts.append(time.perf_counter() - t0)
+            cpu_s = float(np.median(cts))
+            print(json.dumps({
+                "workload": f"{name} ({cite[name]})", "elements": e, "dtype": "u32", "a_nnz": int(a.get_nnz()),
+                **extra, "gpu_ms_per_call": round(gpu_s * 1e3, 4), "gpu_elements_per_s": round(e / gpu_s, 1),
+                "cpu_ms_per_call": round(cpu_s * 1e3, 4), "cpu_elements_per_s": round(e / cpu_s, 1),
+                "cpu_kind": "port (oracle restatement, 1 thread)", "gpu_over_cpu": round(cpu_s / gpu_s, 2),
+                "out_nnz": int(out.get_nnz()), "bit_exact_vs_oracle": _same(out, ref),
+            }), flush=True)
 
 
 def main():
@@ -158,11 +194,12 @@ def main():
                     help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
-    ap.add_argument("--sd-mul", action="store_true",
-                    help="run the reference's own sd_mul criterion shapes instead (one JSON line per size)")
+    ap.add_argument("--ref-benches", default=None,
+                    help="comma list of the reference's own criterion benches to run instead "
+                         "(sd_mul,ss_add,ss_mul; one JSON line per size)")
     args = ap.parse_args()
-    if args.sd_mul:
-        sd_mul_suite()
+    if args.ref_benches:
+        ref_bench_suite(which=tuple(args.ref_benches.split(",")))
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

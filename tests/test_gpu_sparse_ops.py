@@ -122,3 +122,31 @@ def test_mul_sparse_rectangular_mismatch(orc):
     a = sorted_random(rng, 30, 50, 0.2, np.int32)
     b = sorted_random(rng, 20, 40, 0.2, np.int32)
     assert_csr_bits(a.mul_sparse(b), *orc.mul_sparse(arrays(a), arrays(b)))
+
+
+@pytest.mark.parametrize("case", ["both_have_max", "rhs_lacks_max", "unequal_max_counts", "one_side_empty",
+                                  "sorted_long"])
+def test_add_sub_long_rows_vs_oracle(orc, case):
+    """Rows above the piece threshold (8192 entries) are cut at the pairs of
+    the row maximum; every way the maximum can be distributed stays exact."""
+    rng = np.random.default_rng(len(case))
+    n, cols = 30_000, 500
+    ca = rng.integers(0, cols, n)
+    cb = rng.integers(0, cols, n)
+    if case == "rhs_lacks_max":
+        cb = np.minimum(cb, cols - 2)
+    if case == "unequal_max_counts":
+        ca[rng.random(n) < 0.05] = cols - 1
+    if case == "sorted_long":
+        ca, cb = np.sort(ca), np.sort(cb)
+    if case == "one_side_empty":
+        cb = cb[:0]
+    va = rng.integers(-3, 4, len(ca)).astype(np.int64)
+    vb = rng.integers(-3, 4, len(cb)).astype(np.int64)
+    va[va == 0] = 1
+    vb[vb == 0] = 2
+    a = Csr.from_csr_arrays((2, cols), np.array([0, 5, len(ca)], np.uint64), ca.astype(np.uint64), va)
+    b = Csr.from_csr_arrays((2, cols), np.array([0, min(3, len(cb)), len(cb)], np.uint64), cb.astype(np.uint64), vb)
+    for op, ref in [(Csr.add_sparse, orc.add_sparse), (Csr.sub_sparse, orc.sub_sparse)]:
+        assert_csr_bits(op(a, b), *ref(arrays(a), arrays(b)))
+        assert_csr_bits(op(b, a), *ref(arrays(b), arrays(a)))
