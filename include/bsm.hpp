@@ -156,6 +156,7 @@ inline std::optional<MatErr> status(int rc) {
         case BSM_OK: return std::nullopt;
         case BSM_ERR_DIMENSIONS: return MatErr::IncorrectDimensions;
         case BSM_ERR_NON_SQUARE: return MatErr::NonSquareMatrix;
+        case BSM_ERR_OUT_OF_BOUNDS: return MatErr::OutOfBounds;
         case BSM_ERR_PANIC: throw Panic(bsm_last_error());
         default: throw DeviceError(rc, bsm_last_error());
     }
@@ -239,6 +240,41 @@ struct CsrEntry {
     bool operator==(const CsrEntry& o) const {
         return *v == *o.v && col_index == o.col_index && row_index == o.row_index;
     }
+};
+
+template <class T>
+class Csr;
+
+/// sparse.rs:7-33: a COO entry, ordered by row then col.
+template <class T>
+struct COOEntry {
+    size_t row = 0, col = 0;
+    T value{};
+};
+
+/// sparse.rs:35-54: an unordered entry list with a bounds-checked insert;
+/// Csr<T>::from(coo) is `From<COO<T>> for Csr<T>` (sparse.rs:56-66).
+template <class T>
+class COO {
+public:
+    static COO with_capacity(MatDim dims, size_t capacity) {
+        COO c;
+        c.dims_ = dims;
+        c.entries_.reserve(capacity);
+        return c;
+    }
+    /// sparse.rs:45-53: Err(OutOfBounds) unless row < rows and col < cols.
+    Result<void> insert(COOEntry<T> e) {
+        if (dims_.rows <= e.row || dims_.cols <= e.col) return MatErr::OutOfBounds;
+        entries_.push_back(e);
+        return {};
+    }
+    const std::vector<COOEntry<T>>& entries() const { return entries_; }
+    MatDim dims() const { return dims_; }
+
+private:
+    std::vector<COOEntry<T>> entries_;
+    MatDim dims_;
 };
 
 template <class T>
@@ -416,6 +452,24 @@ public:
         return from_device(detail::Handle(out, detail::HandleFree{}));
     }
 
+    /// sparse.rs:484-540: the per-row merge in storage order, zero sums dropped.
+    Result<Csr> add_sparse(const Csr& rhs) const requires detail::GpuScalar<T> {
+        if (dims_ != rhs.dims_) return MatErr::IncorrectDimensions;  // :485-487
+        return binary(rhs, bsm_csr_add_sparse);
+    }
+    /// sparse.rs:542-599 (rhs-only entries become T::default() - v).
+    Result<Csr> sub_sparse(const Csr& rhs) const requires detail::GpuScalar<T> {
+        if (dims_ != rhs.dims_) return MatErr::IncorrectDimensions;  // :543-546
+        return binary(rhs, bsm_csr_sub_sparse);
+    }
+    /// sparse.rs:601-635: dims (rows, rhs.cols), no dimension check.
+    Result<Csr> mul_sparse(const Csr& rhs) const requires detail::GpuScalar<T> {
+        return binary(rhs, bsm_csr_mul_sparse);
+    }
+    /// `From<COO<T>> for Csr<T>` (sparse.rs:56-66): stable sort by (row, col),
+    /// then the zero-skipping insert sequence and finalise (on the GPU).
+    static Csr from(const class COO<T>& coo) requires detail::GpuScalar<T>;
+
     /// Derived PartialEq over the seven fields of sparse.rs:68-78.
     bool operator==(const Csr& o) const {
         return dims_ == o.dims_ && v_ == o.v_ && col_index_ == o.col_index_ && row_index_ == o.row_index_ &&
@@ -489,6 +543,15 @@ private:
         return from_device(detail::Handle(out, detail::HandleFree{}));
     }
 
+    Result<Csr> binary(const Csr& rhs, int (*fn)(const bsm_csr*, const bsm_csr*, bsm_csr**)) const {
+        auto a = device();
+        auto b = rhs.device();
+        bsm_csr* out = nullptr;
+        if (auto e = detail::status(fn(a.get(), b.get(), &out))) return *e;
+        return from_device(detail::Handle(out, detail::HandleFree{}));
+    }
+
+public:
     static Csr from_device(detail::Handle h) {
         uint64_t rows = 0, cols = 0, nnz = 0;
         int dt = 0;
@@ -505,6 +568,7 @@ private:
         return m;
     }
 
+private:
     MatDim dims_;
     std::vector<T> v_;
     std::vector<size_t> col_index_;
@@ -513,6 +577,23 @@ private:
     size_t iter_v_index_ = 0, iter_row_index_ = 0;
     mutable detail::Handle dev_;
 };
+
+template <class T>
+Csr<T> Csr<T>::from(const COO<T>& coo) requires detail::GpuScalar<T> {
+    const auto& es = coo.entries();
+    std::vector<uint64_t> r(es.size()), c(es.size());
+    std::vector<T> v(es.size());
+    for (size_t i = 0; i < es.size(); ++i) {
+        r[i] = es[i].row;
+        c[i] = es[i].col;
+        v[i] = es[i].value;
+    }
+    bsm_csr* out = nullptr;
+    if (auto e = detail::status(bsm_csr_from_coo(detail::dtype_of<T>::value, coo.dims().rows, coo.dims().cols,
+                                                 es.size(), r.data(), c.data(), v.data(), &out)))
+        throw Panic(std::string("COO entry out of bounds: ") + to_string(*e));
+    return from_device(detail::Handle(out, detail::HandleFree{}));
+}
 
 // ----------------------------------------------------------------- lib.rs
 namespace detail {

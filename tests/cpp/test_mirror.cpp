@@ -213,6 +213,40 @@ GPU_TEST(solve_test) {  // lib.rs:119-138
 }
 
 // ------------------------------------------- seeded parity vs the oracle
+GPU_TEST(add_sparse) {  // sparse.rs:1181-1207
+    auto a = Csr<int32_t>::from_data(Rows<int32_t>{{5, 6, 7, 8, 9}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 1}, {1, 0, 0, 0, 0}});
+    auto b = Csr<int32_t>::from_data(Rows<int32_t>{{9, 8, 7, 6, 5}, {0, 0, 0, 0, 0}, {1, 0, 0, 0, 0}, {1, 0, 0, 0, 0}});
+    CHECK(a.add_sparse(b).unwrap() == Csr<int32_t>::from_data(Rows<int32_t>{
+                                          {14, 14, 14, 14, 14}, {0, 0, 0, 0, 0}, {1, 0, 0, 0, 1}, {2, 0, 0, 0, 0}}));
+    CHECK(a.add_sparse(Csr<int32_t>::from_data(Rows<int32_t>{{1}})) == MatErr::IncorrectDimensions);
+}
+
+GPU_TEST(sub_sparse) {  // sparse.rs:1210-1236
+    auto a = Csr<int32_t>::from_data(Rows<int32_t>{{5, 6, 7, 8, 9}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 1}, {1, 0, 0, 0, 0}});
+    auto b = Csr<int32_t>::from_data(Rows<int32_t>{{9, 8, 7, 6, 5}, {0, 0, 0, 0, 0}, {1, 0, 0, 0, 0}, {1, 0, 0, 0, 0}});
+    CHECK(a.sub_sparse(b).unwrap() == Csr<int32_t>::from_data(Rows<int32_t>{
+                                          {-4, -2, 0, 2, 4}, {0, 0, 0, 0, 0}, {-1, 0, 0, 0, 1}, {0, 0, 0, 0, 0}}));
+}
+
+GPU_TEST(sparse_multiplication) {  // sparse.rs:1284-1301 (round 3)
+    auto a = Csr<int32_t>::from_data(Rows<int32_t>{{0}, {1}, {1}});
+    auto b = a.transpose();
+    CHECK(a.mul_sparse(b).unwrap() == Csr<int32_t>::from_data(Rows<int32_t>{{0, 0, 0}, {0, 1, 1}, {0, 1, 1}}));
+}
+
+GPU_TEST(coo_to_csr) {  // sparse.rs:1443-1468
+    auto coo = bsm::COO<double>::with_capacity({5, 6}, 8);
+    const std::vector<bsm::COOEntry<double>> es = {{0, 0, 1.0}, {1, 1, 2.0}, {1, 2, 3.0}, {2, 2, 4.0}, {2, 3, 5.0},
+                                                   {3, 3, 6.0}, {3, 4, 7.0}, {4, 4, 8.0}, {4, 5, 9.0}};
+    for (auto e : es) coo.insert(e).unwrap();
+    CHECK(Csr<double>::from(coo) == Csr<double>::from_data(Rows<double>{{1.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                                                                        {0.0, 2.0, 3.0, 0.0, 0.0, 0.0},
+                                                                        {0.0, 0.0, 4.0, 5.0, 0.0, 0.0},
+                                                                        {0.0, 0.0, 0.0, 6.0, 7.0, 0.0},
+                                                                        {0.0, 0.0, 0.0, 0.0, 8.0, 9.0}}));
+    CHECK(coo.insert({5, 0, 1.0}) == MatErr::OutOfBounds);
+}
+
 GPU_TEST(mul_dense_f64_k32_vs_oracle) {
     const uint64_t rows = 1500, cols = 700, k = 32;
     std::vector<uint64_t> rp(rows + 1);
