@@ -107,6 +107,9 @@ template <typename F> int dispatch_dtype(int dt, F&& f) {
 // ---------------------------------------------------------------------------
 int current_device(int* dev);
 int ctx_stream(hipStream_t* s);  // stream of the calling thread's device
+// Small device -> host read through a pinned bounce buffer, synchronous on s
+// (a pageable hipMemcpyAsync costs ~19 us; this is a few).
+hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s);
 
 // RAII device buffer for host-path temporaries.
 struct DBuf {

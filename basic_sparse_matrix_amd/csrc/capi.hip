@@ -6,6 +6,9 @@
 #include <mutex>
 #include <vector>
 
+#include <algorithm>
+#include <cstring>
+
 #include "bsm_internal.hpp"
 
 namespace bsm {
@@ -86,25 +89,76 @@ int csr_analyse(bsm_csr* m, hipStream_t s) {
     return BSM_OK;
 }
 
+// Pinned host staging for small transfers: a copy from pageable memory costs
+// ~19 us per hipMemcpyAsync on the box, so small operands are packed into one
+// pinned buffer and moved with one copy (profiles/r01_z_api_overhead.log).
+// One buffer per thread (the library's calls are synchronous per thread).
+constexpr size_t PIN_MAX = 32ull << 20;
+static void* pinned(size_t bytes) {
+    static thread_local void* buf = nullptr;
+    static thread_local size_t cap = 0;
+    if (bytes > cap) {
+        if (buf) (void)hipHostFree(buf);
+        buf = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 1 << 20);
+        if (hipHostMalloc(&buf, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        cap = want;
+    }
+    return buf;
+}
+
+hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s) {
+    static thread_local void* bounce = nullptr;
+    if (bytes > 4096) {
+        hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s);
+        return e != hipSuccess ? e : hipStreamSynchronize(s);
+    }
+    if (!bounce) {
+        hipError_t e = hipHostMalloc(&bounce, 4096, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            bounce = nullptr;
+            return e;
+        }
+    }
+    hipError_t e = hipMemcpyAsync(bounce, dev, bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) std::memcpy(host, bounce, bytes);
+    return e;
+}
+
 // Upload k host columns (each n values) into a device ROW-major n x k array.
 static int upload_columns(int dtype, uint64_t n, uint64_t k, const void* const* cols, DBuf& out,
                           hipStream_t s) {
     const size_t es = dtype_size(dtype);
     BSM_TRY(out.alloc(n * k * es));
     if (n == 0 || k == 0) return BSM_OK;
+    for (uint64_t j = 0; j < k; ++j)
+        BSM_REQUIRE(cols[j] != nullptr, BSM_ERR_INVALID, "null column pointer %llu", (unsigned long long)j);
+    if (n * k * es <= PIN_MAX) {
+        if (char* pin = static_cast<char*>(pinned(n * k * es))) {  // pack row-major on the host, one copy
+            if (k == 1) {
+                std::memcpy(pin, cols[0], n * es);
+            } else {
+                for (uint64_t j = 0; j < k; ++j) {
+                    const char* c = static_cast<const char*>(cols[j]);
+                    for (uint64_t r = 0; r < n; ++r) std::memcpy(pin + (r * k + j) * es, c + r * es, es);
+                }
+            }
+            BSM_HIP_TRY(hipMemcpyAsync(out.p, pin, n * k * es, hipMemcpyHostToDevice, s));
+            BSM_HIP_TRY(hipStreamSynchronize(s));  // the pinned buffer is reused by the next call
+            return BSM_OK;
+        }
+    }
     if (k == 1) {
-        BSM_REQUIRE(cols[0] != nullptr, BSM_ERR_INVALID, "null column pointer");
         BSM_HIP_TRY(hipMemcpyAsync(out.p, cols[0], n * es, hipMemcpyHostToDevice, s));
         return BSM_OK;
     }
     DBuf staging;
     BSM_TRY(staging.alloc(n * k * es));
-    for (uint64_t j = 0; j < k; ++j) {
-        BSM_REQUIRE(cols[j] != nullptr, BSM_ERR_INVALID, "null column pointer %llu",
-                    (unsigned long long)j);
+    for (uint64_t j = 0; j < k; ++j)
         BSM_HIP_TRY(hipMemcpyAsync(static_cast<char*>(staging.p) + j * n * es, cols[j], n * es,
                                    hipMemcpyHostToDevice, s));
-    }
     BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, staging.p, out.p, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // staging dies here
     return BSM_OK;
@@ -173,9 +227,7 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     BSM_TRY(exclusive_scan_i32_to_i64(row_nnz.as<int32_t>(), out_rp.as<int64_t>(), rows, ws.p,
                                       ws.bytes, s));
     int64_t out_nnz = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t),
-                               hipMemcpyDeviceToHost, s));
-    BSM_HIP_TRY(hipStreamSynchronize(s));
+    BSM_HIP_TRY(read_dev(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t), s));
     r = new bsm_csr();
     r->dtype = a->dtype;
     r->device = a->device;
@@ -344,21 +396,35 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
     hipStream_t s;
     BSM_TRY(ctx_stream(&s));
-    std::vector<int64_t> rp64(m->rows + 1);
-    std::vector<int32_t> c32(m->nnz);
-    BSM_HIP_TRY(hipMemcpyAsync(rp64.data(), m->row_ptr, (m->rows + 1) * sizeof(int64_t),
-                               hipMemcpyDeviceToHost, s));
+    const size_t es = dtype_size(m->dtype);
+    const size_t rp_b = (m->rows + 1) * sizeof(int64_t), col_b = m->nnz * sizeof(int32_t), val_b = m->nnz * es;
+    char* pin = rp_b + col_b + val_b <= PIN_MAX ? static_cast<char*>(pinned(rp_b + col_b + val_b)) : nullptr;
+    std::vector<int64_t> rp_v;
+    std::vector<int32_t> c_v;
+    int64_t* rp64;
+    int32_t* c32;
+    char* vdst = static_cast<char*>(vals);
+    if (pin) {  // small: three copies into one pinned buffer, one sync
+        rp64 = reinterpret_cast<int64_t*>(pin);
+        c32 = reinterpret_cast<int32_t*>(pin + rp_b);
+        vdst = pin + rp_b + col_b;
+    } else {
+        rp_v.resize(m->rows + 1);
+        c_v.resize(m->nnz);
+        rp64 = rp_v.data();
+        c32 = c_v.data();
+    }
+    BSM_HIP_TRY(hipMemcpyAsync(rp64, m->row_ptr, rp_b, hipMemcpyDeviceToHost, s));
     if (m->nnz) {
-        BSM_HIP_TRY(hipMemcpyAsync(c32.data(), m->col, m->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        if (vals)
-            BSM_HIP_TRY(hipMemcpyAsync(vals, m->vals, m->nnz * dtype_size(m->dtype),
-                                       hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipMemcpyAsync(c32, m->col, col_b, hipMemcpyDeviceToHost, s));
+        if (vals) BSM_HIP_TRY(hipMemcpyAsync(vdst, m->vals, val_b, hipMemcpyDeviceToHost, s));
     }
     BSM_HIP_TRY(hipStreamSynchronize(s));
     if (row_ptr)
         for (uint64_t r = 0; r <= m->rows; ++r) row_ptr[r] = (uint64_t)rp64[r];
     if (col_idx)
         for (uint64_t e = 0; e < m->nnz; ++e) col_idx[e] = (uint64_t)c32[e];
+    if (pin && vals && val_b) std::memcpy(vals, vdst, val_b);
     return BSM_OK;
 }
 

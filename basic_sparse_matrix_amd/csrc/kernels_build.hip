@@ -145,7 +145,7 @@ int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n,
     BSM_TRY(rc);
     BSM_TRY(exclusive_scan_i32_to_i64(flag.as<int32_t>(), pos.as<int64_t>(), n, ws.p, ws.bytes, s));
     int64_t nnz = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&nnz, pos.as<int64_t>() + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&nnz, pos.as<int64_t>() + n, sizeof(int64_t), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     // 2. scatter the kept entries, then the running maximum of their rows
     bsm_csr* m = nullptr;
@@ -186,10 +186,9 @@ int csr_from_inserts_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n,
     // 3. checks: finalise's "big eek" (a kept row >= rows) and column bounds
     int64_t last_row = -1;
     unsigned bad_col = 0;
-    if (nnz && hipMemcpyAsync(&last_row, erow.as<int64_t>() + nnz - 1, sizeof(int64_t), hipMemcpyDeviceToHost,
-                              s) != hipSuccess)
+    if (nnz && read_dev(&last_row, erow.as<int64_t>() + nnz - 1, sizeof(int64_t), s) != hipSuccess)
         return fail(BSM_ERR_HIP);
-    if (hipMemcpyAsync(&bad_col, err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (read_dev(&bad_col, err.p, sizeof(unsigned), s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return fail(BSM_ERR_HIP);
     if (nnz && (uint64_t)last_row >= rows) {
@@ -234,7 +233,7 @@ int csr_from_coo_device(int dtype, uint64_t rows, uint64_t cols, uint64_t n, con
                                         err.as<unsigned>());
     BSM_HIP_TRY(hipGetLastError());
     unsigned bad = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&bad, err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&bad, err.p, sizeof(unsigned), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     if (bad) {
         set_error("COO entry outside dims %llu x %llu (MatErr::OutOfBounds, sparse.rs:47-49)",

@@ -1373,7 +1373,7 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
                     ph[0] / nbd, ph[1] / nbd, ph[2] / nbd, ph[3] / nbd, ph[4] / nbd);
     }
     int st = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&st, status, sizeof(int), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     BSM_REQUIRE(!(st & ST_TIMEOUT), BSM_ERR_HIP, "cholesky: tile-row hand-off timed out");
     BSM_REQUIRE(!(st & ST_NOT_PD), BSM_ERR_UNSUPPORTED,
@@ -1395,7 +1395,7 @@ int band_to_csr_host(const Band& bd, int dtype, bsm_csr** out, hipStream_t s) {
     BSM_HIP_TRY(hipGetLastError());
     BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), rp.as<int64_t>(), n, ws.p, ws.bytes, s));
     int64_t nnz = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&nnz, rp.as<int64_t>() + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&nnz, rp.as<int64_t>() + n, sizeof(int64_t), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     auto* m = new bsm_csr();
     m->dtype = dtype;
@@ -1484,7 +1484,7 @@ int solve_dispatch_trsv(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, co
             BSM_HIP_TRY(hipGetLastError());
         }
         int h = 0;
-        BSM_HIP_TRY(hipMemcpyAsync(&h, st.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(read_dev(&h, st.p, sizeof(int), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         BSM_REQUIRE(!(h & ST_EMPTY_ROW), BSM_ERR_PANIC,
                     "called `Option::unwrap()` on a `None` value: empty row (lib.rs:41 / :60)");

@@ -585,7 +585,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
         // long rows: list, pieces, piece counts
         BSM_TRY(exclusive_scan_i32_to_i64(lflag.as<int32_t>(), lpos.as<int64_t>(), rows, ws.p, ws.bytes, s));
         int64_t n_long = 0;
-        BSM_HIP_TRY(hipMemcpyAsync(&n_long, lpos.as<int64_t>() + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(read_dev(&n_long, lpos.as<int64_t>() + rows, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         DBuf long_rows, mval, pstart, pieces, pcnt, poff, first, ws2, tcol, tval;
         int64_t n_pieces = 0;
@@ -661,7 +661,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
         }
         BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), orp.as<int64_t>(), rows, ws.p, ws.bytes, s));
         int64_t nnz = 0;
-        BSM_HIP_TRY(hipMemcpyAsync(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, (uint64_t)nnz));
         BSM_HIP_TRY(hipMemcpyAsync(g.m->row_ptr, orp.p, (rows + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
@@ -709,7 +709,7 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
     }
     BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), off.as<int64_t>(), nnz_a, ws.p, ws.bytes, s));
     int64_t total = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&total, off.as<int64_t>() + nnz_a, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&total, off.as<int64_t>() + nnz_a, sizeof(int64_t), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     BSM_REQUIRE(total < (int64_t)UINT32_MAX, BSM_ERR_UNSUPPORTED,
                 "mul_sparse: %lld expanded products (limit 2^32)", (long long)total);
@@ -737,7 +737,7 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
         BSM_TRY(tmp2.alloc(ub ? ub : 1));
         BSM_HIP_TRY(rocprim::unique(tmp2.p, ub, keys_s.as<uint64_t>(), keys.as<uint64_t>(), n_dev.as<uint64_t>(),
                                     (size_t)total, rocprim::equal_to<uint64_t>(), s));
-        BSM_HIP_TRY(hipMemcpyAsync(&n_cand, n_dev.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(read_dev(&n_cand, n_dev.p, sizeof(uint64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
     }
     // 3. the merge per candidate, 4. keep the nonzero ones
@@ -758,7 +758,7 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
             BSM_HIP_TRY(hipGetLastError());
         }
         BSM_TRY(exclusive_scan_i32_to_i64(keep.as<int32_t>(), pos.as<int64_t>(), n_cand, ws2.p, ws2.bytes, s));
-        BSM_HIP_TRY(hipMemcpyAsync(&nnz, pos.as<int64_t>() + n_cand, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(read_dev(&nnz, pos.as<int64_t>() + n_cand, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         BSM_TRY(csr_alloc(&g.m, a->dtype, rows, cols, (uint64_t)nnz));
         BSM_TRY(orow.alloc((nnz ? nnz : 1) * sizeof(int64_t)));

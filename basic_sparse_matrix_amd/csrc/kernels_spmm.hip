@@ -980,7 +980,7 @@ int spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* rp, const int32_t* 
         BSM_HIP_TRY(hipGetLastError());
     }
     unsigned bad = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&bad, flag.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&bad, flag.p, sizeof(unsigned), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     *usable = bad == 0;
     return BSM_OK;
@@ -1050,7 +1050,7 @@ int analyse_dispatch(const int64_t* rp, const int32_t* col, uint64_t rows, uint6
     BSM_HIP_TRY(hipMemsetAsync(d_out3, 0, 3 * sizeof(uint64_t), s));
     if (rows == 0) return BSM_OK;
     int64_t nnz = 0;
-    BSM_HIP_TRY(hipMemcpyAsync(&nnz, rp + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(read_dev(&nnz, rp + rows, sizeof(int64_t), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     DBuf bits;
     const uint64_t words = (uint64_t)nnz / 32 + 1;
