@@ -68,3 +68,29 @@ def unpad_blocks(y_gathered, bounds, pad_rows: int):
         return y_gathered[: int(b[-1])]  # only the last block can be short
     parts = [y_gathered[g * pad_rows: g * pad_rows + int(b[g + 1] - b[g])] for g in range(world)]
     return torch.cat(parts, dim=0)
+
+
+def partition_rows_cyclic(rows: int, world: int, chunks: int):
+    """Block-cyclic row partition for an all-gather overlapped with compute.
+
+    The rows are cut into `chunks` rounds of world*cr consecutive rows
+    (cr = ceil(rows / (chunks*world))); in round c rank g owns rows
+    [c*world*cr + g*cr, ... + cr), clipped to `rows`. Round c of every rank
+    is finished by the same SpMM launch, and the equal-count all-gather of
+    round c lands contiguously, already in global row order, at rows
+    [c*world*cr, (c+1)*world*cr) of the gathered buffer: no reordering copy,
+    and only the last round holds padding (rows >= `rows`, never read).
+
+    Returns (cr, [[(row0, nrows) for c in range(chunks)] for g in range(world)]);
+    nrows may be 0 for trailing pieces."""
+    if world < 1 or chunks < 1:
+        raise ValueError("world and chunks must be >= 1")
+    cr = -(-rows // (chunks * world)) if rows else 0
+    pieces = []
+    for g in range(world):
+        mine = []
+        for c in range(chunks):
+            r0 = c * world * cr + g * cr
+            mine.append((min(r0, rows), max(0, min(rows, r0 + cr) - r0)))
+        pieces.append(mine)
+    return cr, pieces

@@ -6,10 +6,13 @@ Workload (BASELINE.json north_star target / configs[3]): A = 10M x 10M
 synthetic random CSR, 1000 nnz per row (0.01 % density, nnz = 1e10), f64,
 times a dense 10M x 32 f64 RHS. It fits one MI355X (A 120 GB + X/Y 5 GB of
 288 GB HBM), so N=1 runs the whole matrix on one GPU. For N > 1 the rows are
-split into N contiguous, equal-nnz blocks (one process per GPU); X is
-replicated (every rank generates the same X from its seed -- no transfer) and
-the dense result Y is assembled on every rank with an RCCL all-gather over
-xGMI, as north_star specifies. Total work is fixed as N grows ("strong").
+split block-cyclically (one process per GPU): `--chunks` rounds of N equal
+row blocks, rank g owning block g of every round (equal rows = equal nnz). X
+is replicated (every rank generates the same X from its seed -- no transfer)
+and the dense result Y is assembled on every rank with RCCL all-gathers over
+xGMI, as north_star specifies: one async all-gather per round, issued as soon
+as that round's SpMM is enqueued, so it overlaps the next round's SpMM and
+lands in global row order. Total work is fixed as N grows ("strong").
 
 One step = the hot path of Csr::mul_dense (src/sparse.rs:426-446) over the
 whole matrix: SpMM kernel (Y block) -> [all-gather of Y blocks] ->
@@ -189,6 +192,8 @@ def main():
     ap.add_argument("--cpu-sample-rows", type=int, default=5000)
     ap.add_argument("--panel-cols", type=int, default=None,
                     help="column-panel width of the SpMM schedule (default: the library's choice; 0 = one pass)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="rounds of the block-cyclic row partition (0: 1 at N=1, 4 at N>1)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
@@ -220,34 +225,39 @@ def main():
     from basic_sparse_matrix_amd import _lib
     from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
 
-    from basic_sparse_matrix_amd.distributed import padded_block_rows, partition_rows_even
+    from basic_sparse_matrix_amd.distributed import partition_rows_cyclic
 
     rows, n_cols, nnz_r, k = CONFIGS[args.config]
-    # contiguous row blocks, equal rows (= equal nnz: constant row length);
-    # padded to a common size for the equal-count all-gather
-    bounds = partition_rows_even(rows, world)
-    per = padded_block_rows(bounds)
-    row0 = int(bounds[rank])
-    my_rows = int(bounds[rank + 1]) - row0
+    # block-cyclic row partition (equal rows = equal nnz: constant row length):
+    # `chunks` rounds, each finished by its own SpMM launch and all-gathered
+    # asynchronously while the next round computes (N > 1)
+    chunks = args.chunks if args.chunks else (1 if world == 1 else 4)
+    cr, pieces = partition_rows_cyclic(rows, world, chunks)
+    mine = pieces[rank]
+    my_rows = sum(n for _, n in mine)
 
     t0 = time.perf_counter()
-    blk = DeviceCsrBlock.generate(SEED_A, row0, my_rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r,
-                                  _lib.VAL_UNIFORM, np.float64, device=dev)
+    blks = [DeviceCsrBlock.generate(SEED_A, r0, n, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r, _lib.VAL_UNIFORM,
+                                    np.float64, device=dev) for r0, n in mine]
+    my_nnz = sum(b.nnz for b in blks)
     x = gen_dense(SEED_X, 0, n_cols, k, device=dev)
-    y_local = torch.empty((per, k), dtype=torch.float64, device=dev)
-    nnz_local = torch.zeros(per, dtype=torch.int32, device=dev)
+    y_local = torch.empty((chunks, cr, k), dtype=torch.float64, device=dev)
+    nnz_local = torch.zeros((chunks, cr), dtype=torch.int32, device=dev)
     if world > 1:
-        y_full = torch.empty((per * world, k), dtype=torch.float64, device=dev)
-        nnz_full = torch.empty(per * world, dtype=torch.int32, device=dev)
+        y_full = torch.empty((chunks * world * cr, k), dtype=torch.float64, device=dev)
+        nnz_full = torch.zeros(chunks * world * cr, dtype=torch.int32, device=dev)
     else:
-        y_full, nnz_full = y_local, nnz_local
+        y_full, nnz_full = y_local.view(chunks * cr, k), nnz_local.view(chunks * cr)
     comp = Compactor(rows, k, np.float64, device=dev)
     torch.cuda.synchronize()
-    log(f"rank {rank}: rows [{row0},{row0 + my_rows}) nnz {blk.nnz:,} generated in {time.perf_counter() - t0:.1f} s")
+    log(f"rank {rank}: {my_rows:,} rows in {chunks} round(s) of {cr:,}, nnz {my_nnz:,} generated in "
+        f"{time.perf_counter() - t0:.1f} s")
     # column-panel plan: built once per matrix (like the matrix itself, outside
     # the timed region; its cost is reported as plan_ms)
     t0 = time.perf_counter()
-    panel_cols = blk.plan(k, args.panel_cols)
+    panel_cols = 0
+    for b in blks:
+        panel_cols = b.plan(k, args.panel_cols)
     torch.cuda.synchronize()
     plan_ms = (time.perf_counter() - t0) * 1e3
     n_passes = -(-n_cols // panel_cols) if panel_cols else 1
@@ -258,16 +268,23 @@ def main():
     ev_c0 = torch.cuda.Event(enable_timing=True)
     ev_c1 = torch.cuda.Event(enable_timing=True)
     kern_ms, comm_ms, comp_ms = [], [], []
+    round_rows = world * cr
 
     def step(timed):
         if timed:
             ev_k0.record()
-        blk.spmm(x, y_local[:my_rows], nnz_local[:my_rows])
+        works = []
+        for c, b in enumerate(blks):
+            b.spmm(x, y_local[c, :b.rows], nnz_local[c, :b.rows])
+            if world > 1:  # RCCL all-gather of this round's Y rows (+ nnz counts), overlapped with the next
+                works.append(dist.all_gather_into_tensor(y_full[c * round_rows:(c + 1) * round_rows], y_local[c],
+                                                         async_op=True))
+                works.append(dist.all_gather_into_tensor(nnz_full[c * round_rows:(c + 1) * round_rows],
+                                                         nnz_local[c], async_op=True))
         if timed:
             ev_k1.record()
-        if world > 1:  # RCCL all-gather of the dense Y blocks (+ their nnz counts)
-            dist.all_gather_into_tensor(y_full, y_local)
-            dist.all_gather_into_tensor(nnz_full, nnz_local)
+        for w in works:
+            w.wait()
         if timed:
             ev_c0.record()
         comp(y_full[:rows], nnz_full[:rows])
@@ -321,7 +338,7 @@ def main():
     # roofline of the dominant kernel (the SpMM: n_passes launches of the
     # panelled kernel, bracketed together by the HIP events): algorithmic
     # bytes of THIS rank's SpMM over its measured average duration
-    b_launch = b_alg(my_rows, n_cols, blk.nnz, k)
+    b_launch = b_alg(my_rows, n_cols, my_nnz, k)
     achieved = b_launch / (float(np.mean(kern_ms)) / 1e3) / 1e9
     if rank == 0:
         cpu = None
@@ -358,7 +375,8 @@ def main():
                             f"f64; step = SpMM + {'RCCL all-gather of Y + ' if world > 1 else ''}compaction "
                             f"to Csr",
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
-                "parallelism": f"row-block x{world}" + (" + all-gather" if world > 1 else ""),
+                "parallelism": f"row-block x{world}" + (f" (block-cyclic, {chunks} rounds) + overlapped all-gather"
+                                                         if world > 1 else ""),
                 "panel_cols": panel_cols, "passes": n_passes, "plan_ms": round(plan_ms, 1),
             },
             "nnz_per_s": round(nnz_total / (elapsed / args.steps), 1),

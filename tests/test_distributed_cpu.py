@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from basic_sparse_matrix_amd.distributed import (all_gather_blocks, padded_block_rows, partition_rows_by_nnz,
-                                                 partition_rows_even, unpad_blocks)
+                                                 partition_rows_cyclic, partition_rows_even, unpad_blocks)
 
 
 def _free_port():
@@ -58,6 +58,65 @@ def _worker(rank, world, port, even, result_q):
         result_q.put(bool(np.array_equal(y_full.numpy().view(np.uint64), ref.view(np.uint64))))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _worker_cyclic(rank, world, port, chunks, rows, result_q):
+    """bench.py's overlapped schedule: one async all-gather per round of the
+    block-cyclic partition, issued right after that round's rows are done,
+    straight into the gathered buffer (no reordering)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import pyoracle as orc
+
+    n_cols, k = 700, 4
+    rp, ci, v = orc.gen_csr(1000, rows, n_cols, orc.ROWLEN_UNIFORM, 0, 30)
+    x_cols = orc.gen_x_cols(1001, n_cols, k)
+    cr, pieces = partition_rows_cyclic(rows, world, chunks)
+    y_local = torch.full((chunks, cr, k), float("nan"), dtype=torch.float64)
+    y_full = torch.empty((chunks * world * cr, k), dtype=torch.float64)
+    works = []
+    for c, (r0, n) in enumerate(pieces[rank]):
+        if n:
+            y_local[c, :n] = torch.from_numpy(_dense_y(orc, rows, n_cols, rp, ci, v, x_cols, r0, r0 + n))
+        works.append(dist.all_gather_into_tensor(y_full[c * world * cr:(c + 1) * world * cr], y_local[c],
+                                                 async_op=True))
+    for w in works:
+        w.wait()
+    if rank == 0:
+        ref = _dense_y(orc, rows, n_cols, rp, ci, v, x_cols, 0, rows)
+        result_q.put(bool(np.array_equal(y_full[:rows].numpy().view(np.uint64), ref.view(np.uint64))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks,rows", [(2, 4, 1000), (3, 4, 997), (2, 3, 5), (3, 1, 601)])
+def test_block_cyclic_overlapped_allgather_matches_single(world, chunks, rows):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, chunks, rows, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
+
+
+def test_partition_cyclic_covers_rows_once():
+    for rows, world, chunks in [(10_000_000, 8, 4), (997, 3, 4), (5, 2, 3), (0, 2, 2), (7, 8, 1)]:
+        cr, pieces = partition_rows_cyclic(rows, world, chunks)
+        owner = np.full(rows, -1)
+        for g in range(world):
+            for c, (r0, n) in enumerate(pieces[g]):
+                assert n <= cr
+                if n:
+                    assert r0 == c * world * cr + g * cr  # gathered position == global row
+                    assert np.all(owner[r0:r0 + n] == -1)
+                    owner[r0:r0 + n] = g
+        assert np.all(owner >= 0)
+    cr, pieces = partition_rows_cyclic(10_000_000, 8, 4)
+    assert cr == 312_500 and all(n == cr for mine in pieces for _, n in mine)
 
 
 @pytest.mark.parametrize("world,even", [(2, True), (2, False), (3, False)])
