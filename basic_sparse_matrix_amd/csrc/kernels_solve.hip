@@ -91,6 +91,63 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// Lane j of each 16-lane row to the whole row (DPP row_newbcast:j, gfx90a+; the
+// one DPP form 64-bit data may use): a VALU move, no LDS, no SGPR.
+template <int J> __device__ __forceinline__ int rowbcast_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, false);
+}
+template <int J> __device__ __forceinline__ double rowbcast(double v) {
+    return __hiloint2double(rowbcast_i<J>(__double2hiint(v)), rowbcast_i<J>(__double2loint(v)));
+}
+template <int J> __device__ __forceinline__ float rowbcast(float v) {
+    return __int_as_float(rowbcast_i<J>(__float_as_int(v)));
+}
+
+// Factor the 16 x 16 diagonal block of row-block i0 (wave 0; lane r < 16 is
+// row i0 + r): q[j] = the row's accumulated sum for column i0 + j (dacc[r][j]),
+// a[j] = A[i0 + r][i0 + j] (dA[r][j]). All 16 columns unrolled, straight-line:
+// lane r keeps its row in registers, the pivot comes from lane t and L[j][t]
+// for the updates from lane j (v_readlane). Per element the reference's order
+// (sparse.rs:689-708): sum in ascending k, sqrt pivot, (1/L[t][t]) * (A - sum).
+// Stores L and R = 1 / L[t][t] write-through; the caller drains and publishes.
+template <typename T>
+__device__ __forceinline__ void diag_factor16(const T (*dacc)[17], const T (*dA)[17], T* xl, int i0, int64_t n,
+                                              int64_t b, int64_t ld, T* CB, T* R, int* status, int c) {
+    using A = Arith<T>;
+    constexpr int NB = 16;
+    // opaque lane index: otherwise the per-step masks and store offsets (functions of the lane
+    // and b only) are hoisted out of the caller's loop and kept, in spilled registers, for good
+    asm volatile("" : "+v"(c));
+    const int r = c & (NB - 1);
+    const bool live = i0 + r < n;
+    T q[NB], a[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        q[j] = live ? dacc[r][j] : A::zero();
+        a[j] = live ? dA[r][j] : (r == j ? (T)1 : A::zero());
+    }
+    auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
+        const T v = A::sub(a[t], q[t]);
+        const T piv = pow_half(rowbcast<t>(v));
+        const T rt = div_rn((T)1, piv);
+        const T x = r == t ? piv : A::mul(rt, v);  // L[i0 + r][i0 + t] for r >= t
+        if (c == 0 && i0 + t < n && (!(piv > A::zero()) || isinf(piv))) atomicOr(status, ST_NOT_PD);
+        if (c < NB && r >= t && live && r - t <= b) st_sc1(&CB[(int64_t)(i0 + t) * ld + (r - t)], x);
+        if (c == t && live) st_sc1(&R[i0 + t], rt);
+        // L[j][t] of the other rows by DPP row broadcast (q[t + 1] first: the next pivot's)
+        [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+            ((q[t + 1 + js] = A::add(q[t + 1 + js], A::mul(x, rowbcast<t + 1 + js>(x)))), ...);
+        }(std::make_integer_sequence<int, NB - 1 - t>{});
+        // materialise the sums now: left to itself the compiler sinks every add to
+        // the step that reads it, keeping all x alive and putting t adds on the chain
+#pragma unroll
+        for (int j = t + 1; j < NB; ++j) asm volatile("" : "+v"(q[j]));
+    };
+    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+        (step(std::integral_constant<int, ts>{}), ...);
+    }(std::make_integer_sequence<int, NB>{});
+}
+
 // ---------------------------------------------------------------------------
 // band construction
 // ---------------------------------------------------------------------------
@@ -602,6 +659,219 @@ __global__ __launch_bounds__(1024 / RW) void band_chol3(int64_t n, int64_t b, in
             trace[3 * I + 2] = wall_clock64();
             for (int ph = 0; ph < 5; ++ph) atomicAdd(&trace[3 * TRACE_TILES + 2 + ph], (unsigned long long)tph[ph]);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// band_chol4: tile-event schedule. Row-block I = rows [16 I, 16 I + 16), one
+// 1024-thread workgroup per CU (wave w = row i0 + w); column
+// tile K = columns [16 K, 16 K + 16). Accumulators as in band_chol3 (lane c
+// of slot m holds column jb + c + 64 m, jb = 16 K0 aligned down), so tile K
+// sits in lanes 16 e .. 16 e + 15 of slot m with 16 (K - K0) = 64 m + 16 e.
+// Per off-diagonal tile K (ascending):
+//   T  (needs row-block K complete): stage the 16 x 16 diagonal tile of K and
+//      1/L[k][k]; each wave solves its row across the tile's 16 columns
+//      (x_t = R_t (A - acc_t), acc_{t'} += x_t L[t'][t] in-tile), stores them
+//      write-through and the workgroup publishes fprog[I] = K + 1 (tiles <= K
+//      final) -- the only work on the row-blocks' critical chain;
+//   U  (needs fprog[J] > K for the row-blocks J in (K, I) -- one vector poll):
+//      stage column tile K of the rows in between and add its 16 terms to
+//      every later accumulator, and
+//      to the diagonal-block accumulators from the other rows' x (LDS).
+// Then the 16 x 16 diagonal block (wave 0, diag_factor16) and fprog[I] = I+1.
+// Unlike band_chol3 (which advances column by column behind its predecessor
+// and pays a staging round + barrier per 4 columns on the chain), a
+// row-block's bulk updates run as soon as the tiles they need exist; only
+// T of the last tile + the diagonal block sit between two completions.
+// Operation order per element = the reference's (ascending k, no FMA).
+// ---------------------------------------------------------------------------
+constexpr int C4_TB = 16;
+constexpr int C4_NT = 1024;  // 16 waves, one row each
+
+__global__ __launch_bounds__(256) void band_chol4_init(int64_t n_tiles, int64_t b, int* __restrict__ fprog) {
+    const int64_t J = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (J >= n_tiles) return;
+    const int64_t lo = C4_TB * J - b;
+    fprog[J] = (int)((lo > 0 ? lo : 0) / C4_TB);  // tiles before the band: structurally zero
+}
+
+template <typename T, int M>
+__global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
+                                                    T* __restrict__ R, int* __restrict__ fprog,
+                                                    int* __restrict__ status, int64_t n_tiles,
+                                                    unsigned long long* __restrict__ trace) {
+    using A = Arith<T>;
+    constexpr int CS = 64 + 64 * M;  // [64 zero pad][column tile K of rows k0+16 ...]
+    __shared__ T colK[C4_TB][CS];
+    __shared__ T dTl[C4_TB][64];          // [t][lane lb + t + u] = L[k0 + t + u][k0 + t], 1 <= u <= 15 - t; else 0
+    __shared__ T rT[C4_TB];               // 1 / L[k0 + t][k0 + t]
+    __shared__ T aK[C4_TB][C4_TB];        // aK[r][t] = A[i0 + r][k0 + t]
+    __shared__ T hist[C4_TB][C4_TB + 1];  // hist[t][r] = L[i0 + r][k0 + t]
+    __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
+    __shared__ T xl[16];
+    __shared__ long long tph[16];  // BSM_CHOL_TRACE phase clocks (thread 0)
+    const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
+    for (int q = tid; q < C4_TB * 64; q += C4_NT) colK[q >> 6][q & 63] = A::zero();
+    const int ib = (int)b;
+    auto poll_all = [&](int jlo, int jhi, int need) {  // wave 0: fprog[J] >= need for J in [jlo, jhi)
+        const int J = jlo + c;
+        bool ok = J >= jhi;
+        long long spins = 0;
+        while (true) {
+            if (!ok) ok = __hip_atomic_load(&fprog[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+            if (__all(ok)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > SPIN_LIMIT ||
+                ((spins & 1023) == 0 &&
+                 (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
+                if (c == 0) atomicOr(status, ST_TIMEOUT);
+                break;
+            }
+        }
+    };
+    for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
+        const int i0 = (int)(I * C4_TB);
+        const int K0 = (i0 - ib > 0 ? i0 - ib : 0) / C4_TB, jb = C4_TB * K0;
+        const bool live = i0 + w < n;
+        // diagnostic phase clocks (BSM_CHOL_TRACE), thread 0: [0..6) every off-diagonal tile but the
+        // last, [6..12) the last one (K = I - 1), [12..15) the diagonal block
+        long long tlast = 0;
+        const bool tr0 = trace && tid == 0;
+        if (tr0) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) tph[q] = 0;
+            tlast = clock64();
+        }
+        auto mark = [&](bool last, int ph) {  // ph: a constant
+            if (tr0) {
+                const long long t = clock64();
+                if (last) tph[6 + ph] += t - tlast;
+                else tph[ph] += t - tlast;
+                tlast = t;
+            }
+        };
+        T acc[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[m] = A::zero();
+        T accT = A::zero();
+        const T aT = (c < C4_TB && c <= w && w - c <= ib && live) ? CB[(int64_t)(i0 + c) * ld + (w - c)] : A::zero();
+        auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
+#pragma unroll 1
+            for (int e = 0; e < 4; ++e) {
+                const int K = K0 + 4 * m + e;
+                if (K >= (int)I) return;
+                const int k0 = C4_TB * K, lb = 16 * e;
+                const bool lastK = K == (int)I - 1;
+                // ---------------- T: this row-block's tile K
+                if (w == 0) poll_all(K, K + 1, K + 1);
+                mark(lastK, 0);
+                __syncthreads();
+                {  // the diagonal tile of K, laid out per lane of the slot: one element per thread
+                    const int t = w, u = c - lb - t;
+                    T v = A::zero();
+                    if (u >= 1 && t + u <= 15 && u <= ib) v = ld_sc1(CB + (int64_t)(k0 + t) * ld + u);
+                    dTl[t][c] = v;
+                }
+                if (tid < 256) {
+                    const int rr = tid >> 4, t = tid & 15, d = i0 + rr - k0 - t;
+                    T v = A::zero();
+                    if (d <= ib && i0 + rr < n) v = CB[(int64_t)(k0 + t) * ld + d];
+                    aK[rr][t] = v;
+                } else if (tid < 256 + C4_TB) {
+                    rT[tid - 256] = ld_sc1(&R[k0 + tid - 256]);
+                }
+                __syncthreads();
+                mark(lastK, 1);
+                // lane t holds 1/L[k0+t][k0+t] and A[i][k0+t] (v_readlane), lane l its column's
+                // diagonal-tile values: nothing on the step chain waits for LDS
+                T myR = rT[c & 15], myA = aK[w][c & 15];
+                T xv = A::zero();
+#pragma unroll
+                for (int t = 0; t < C4_TB; ++t) {
+                    // keep the step's v_readlanes in the step (hoisted, they exhaust the SGPRs)
+                    asm volatile("" : "+v"(myR), "+v"(myA));
+                    const T dv = dTl[t][c];
+                    const T s = readlane_t(acc[m], lb + t);
+                    const T x = A::mul(readlane_t(myR, t), A::sub(readlane_t(myA, t), s));
+                    acc[m] = A::add(acc[m], A::mul(x, dv));
+                    if (c == t) xv = x;
+                }
+                if (c < C4_TB) {
+                    hist[c][w] = xv;
+                    const int d = i0 + w - k0 - c;
+                    if (d <= ib && live) st_sc1(&CB[(int64_t)(k0 + c) * ld + d], xv);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                mark(lastK, 2);
+                // publish F(I, K) at once: the row-blocks below wait on it in their U phase (a
+                // publication behind this row-block's own U wait would chain the hand-offs)
+                __syncthreads();
+                if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lastK) {  // no rows in between: the diagonal-block sums of this tile
+                    mark(true, 4);
+                    if (c < C4_TB) {
+                        T hc[C4_TB];
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t) hc[t] = hist[t][c];
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t) accT = A::add(accT, A::mul(readlane_t(xv, t), hc[t]));
+                    }
+                    mark(true, 5);
+                    return;
+                }
+                // ---------------- U: column tile K of the rows between, once they have it
+                mark(lastK, 3);
+                if (w == 0) poll_all(K + 1, (int)I, K + 1);
+                __syncthreads();
+                const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
+                if (tid < cnt) {
+                    // element (t, row k0 + 16 + tid) at base + t (ld - 1); reads past the band
+                    // (d > b) stay inside the allocation (band_pad) and are replaced by 0
+                    const T* base = CB + (int64_t)k0 * ld + C4_TB + tid;
+                    T v[C4_TB];
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + tid] = C4_TB + tid - t <= ib ? v[t] : A::zero();
+                }
+                __syncthreads();
+                mark(lastK, 4);
+#pragma unroll 1
+                for (int t = 0; t < C4_TB; ++t) {
+                    const T x = hist[t][w];
+                    const T* col = &colK[t][64 + c - lb - C4_TB];  // col[64 (mm - m)]: column jb + c + 64 mm
+#pragma unroll
+                    for (int mm = m; mm < M; ++mm)
+                        if (jb + 64 * mm < i0) acc[mm] = A::add(acc[mm], A::mul(x, col[64 * (mm - m)]));
+                    if (c < C4_TB) accT = A::add(accT, A::mul(x, hist[t][c]));
+                }
+                mark(lastK, 5);
+            }
+        };
+        [&]<int... ms>(std::integer_sequence<int, ms...>) __attribute__((always_inline)) {
+            (window(std::integral_constant<int, ms>{}), ...);
+        }(std::make_integer_sequence<int, M>{});
+        // ---------------- the 16 x 16 diagonal block (wave 0)
+        if (c < TR) {
+            dacc[w][c] = accT;
+            dA[w][c] = aT;
+        }
+        __syncthreads();
+        mark(false, 12);
+        if (tid < 64) {
+            diag_factor16<T>(dacc, dA, xl, i0, n, b, ld, CB, R, status, c);
+            mark(false, 13);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mark(false, 14);
+            if (tr0) {
+#pragma unroll
+                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
+                atomicAdd(&trace[15], 1ull);
+                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));  // non-last tiles
+            }
+        }
+        __syncthreads();  // dacc / dA / LDS tiles reused by the next row-block
     }
 }
 
@@ -1290,6 +1560,26 @@ int launch_chol3(Band& bd, int* progress, int* status, hipStream_t s, unsigned l
     return BSM_OK;
 }
 
+template <typename T, int M>
+int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
+    const int64_t n_tiles = (bd.n + C4_TB - 1) / C4_TB;
+    int dev = 0, cus = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    int per_cu = 0;
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol4<T, M>, C4_NT, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol4 does not fit a CU");
+    band_chol4_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
+    BSM_HIP_TRY(hipGetLastError());
+    int64_t grid = (int64_t)cus * per_cu;  // every workgroup resident: row-blocks wait on lower ones only
+    if (grid > n_tiles) grid = n_tiles;
+    if (grid < 1) grid = 1;
+    band_chol4<T, M><<<(unsigned)grid, C4_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
+                                                     n_tiles, trace);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
 template <typename T>
 int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     int64_t bw = 0;
@@ -1330,7 +1620,17 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     // band_chol3 indexes the band with 32-bit offsets
     const bool fits32 = (int64_t)a->rows * (bw + 1) + band_pad(bw + 1) < ((int64_t)1 << 31);
     const bool v1 = (cv && atoi(cv) == 1) || bw > 64 * 16 || !fits32;
-    if (!v1) {
+    // default band_chol4 (tile events); BSM_CHOL_VARIANT = 0 band_chol3, 1 band_chol (A/B)
+    const bool v4 = (!cv || atoi(cv) == 4) && bw + C4_TB - 1 <= 64 * 16;
+    if (v4) {
+        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
+        const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
+        if (w4 <= 64) rc = launch_chol4<T, 1>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 128) rc = launch_chol4<T, 2>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 256) rc = launch_chol4<T, 4>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 512) rc = launch_chol4<T, 8>(bd, prog.as<int>(), status, s, tr);
+        else rc = launch_chol4<T, 16>(bd, prog.as<int>(), status, s, tr);
+    } else if (!v1) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));  // R[n .. n+63]: dummy store / staging targets
         if (bw <= 64) rc = launch_chol3<T, 1>(bd, prog.as<int>(), status, s, tr);
         else if (bw <= 128) rc = launch_chol3<T, 2>(bd, prog.as<int>(), status, s, tr);
@@ -1343,7 +1643,20 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s, tr);
     else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s, tr);
     BSM_TRY(rc);
-    if (tracing) {
+    if (tracing && v4) {
+        std::vector<unsigned long long> h(17);
+        BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        const double nb = h[15] ? (double)h[15] : 1.0, nt = h[16] ? (double)h[16] : 1.0;
+        fprintf(stderr,
+                "[bsm chol4 trace] row-blocks %llu; cycles per tile (non-last): pollT %.0f stageT %.0f trsm %.0f "
+                "publish %.0f pollU+stageU %.0f update %.0f; last tile: pollT %.0f stageT %.0f trsm %.0f (-%.0f) "
+                "publish %.0f diag-sums %.0f; diagonal block: barrier %.0f factor %.0f publish %.0f; per "
+                "row-block: non-last tiles %.0f\n",
+                h[15], h[0] / nt, h[1] / nt, h[2] / nt, h[3] / nt, h[4] / nt, h[5] / nt, h[6] / nb, h[7] / nb,
+                h[8] / nb, h[9] / nb, h[10] / nb, h[11] / nb, h[12] / nb, h[13] / nb, h[14] / nb,
+                (double)(h[0] + h[1] + h[2] + h[3] + h[4] + h[5]) / nb);
+    } else if (tracing) {
         std::vector<unsigned long long> h(3 * TRACE_TILES + 8);
         BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));

@@ -103,7 +103,7 @@ def csr_arrays(dense):
     return rp, nzc.astype(np.uint64), dense[nzr, nzc]
 
 
-@pytest.mark.parametrize("chol_variant", ["0", "1"])  # band_chol3 / band_chol
+@pytest.mark.parametrize("chol_variant", ["0", "1", "4"])  # band_chol3 / band_chol / band_chol4
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("n,density", [(1, 1.0), (7, 0.5), (33, 0.2), (64, 0.05), (150, 0.1), (300, 0.02)])
 def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, chol_variant):
@@ -156,6 +156,42 @@ def test_csr_triangular_solves_vs_oracle(orc, dtype):
     ex = orc.backward_substitution(n, urp, uci, uv, ey)
     for j in range(3):
         assert bits(x.get_col(j)).tolist() == bits(ex[j]).tolist()
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("g", [5, 17, 40, 63, 100])
+def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
+    """Every Cholesky kernel (BSM_CHOL_VARIANT 0 = band_chol3, 1 = band_chol,
+    4 = band_chol4) gives the band oracle's factor bit for bit, including
+    bandwidths that are not a multiple of the 16-row tiles and last
+    row-blocks that are cut short."""
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    v = v.astype(dtype)
+    expect = orc.cholesky(n, n, rp, ci, v, band=True)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    for variant in ("0", "1", "4"):
+        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
+        assert_csr_exact(A.cholesky_decomp(), *expect)
+
+
+def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
+    """250,000 unknowns, bandwidth 500: band_chol4 and band_chol3 factors are
+    identical bit for bit (both are pinned to the oracle at smaller sizes)."""
+    from oracle import pyoracle as orc
+
+    g = 500
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    out = {}
+    for variant in ("0", "4"):
+        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
+        L = A.cholesky_decomp()
+        out[variant] = (np.asarray(L.row_index), np.asarray(L.col_index), bits(np.asarray(L.v)))
+        del L
+    for a, b in zip(out["0"], out["4"]):
+        assert np.array_equal(a, b)
 
 
 def test_poisson_250_bit_exact_solve_f64(orc):
