@@ -76,6 +76,24 @@ template <> __device__ __forceinline__ float div_rn(float a, float b) {
     return __double2float_rn(__ddiv_rn((double)a, (double)b));
 }
 
+// a / b correctly rounded with b's reciprocal y = RN(1/b) computed off the
+// chain (Markstein: q = RN(a y), r = a - b q exactly by FMA, RN(q + r y) =
+// RN(a / b) when y = RN(1/b) and nothing underflows or overflows). 28 instead
+// of 76 cycles of dependent latency (scripts/micro/div_latency.hip); checked
+// against IEEE division on 4e8 random pairs, significands near all-ones
+// included. Outside |a| in [2^-900, 2^900] (zeros, subnormals, inf, NaN) the
+// IEEE division is used (wave-uniform branch, out of line).
+__device__ __forceinline__ double div_by(double a, double b, double y) {
+    const double aa = fabs(a);
+    if (__builtin_expect(__all(aa >= 0x1p-900 && aa <= 0x1p900), 1)) {
+        const double q = __dmul_rn(a, y);
+        const double r = __fma_rn(-q, b, a);
+        return __fma_rn(r, y, q);
+    }
+    return __ddiv_rn(a, b);
+}
+__device__ __forceinline__ float div_by(float a, float b, float) { return div_rn(a, b); }
+
 constexpr int BH_RING = 4096;        // x ring (power of two > b)
 // zero elements after the band: whole-segment reads of the last rows
 // (band_backward_hop) and band_chol3's unclamped staging of columns up to
@@ -968,28 +986,101 @@ constexpr int FW2_RING = 4096;  // y ring (power of two >= b + NW * 64 + 64)
 
 // NW waves, FW2_PF far-term loads in flight per lane: the waiting waves'
 // bytes in flight are what hides the HBM latency of the row-wise band reads
-template <typename T, int NW, int FW2_PF>
+//
+// NH > 0: the far terms are split off. Per RHS column the grid holds one
+// solving workgroup (role 0) and NH helper workgroups. For block blk a helper
+// wave forms the PREFIX P[i] = sum_{j < i0 - FW3_NEAR} L[i][j] y[j] of each
+// row's ascending sum, reading y as the solver publishes it (gfront, per
+// block). The solver's wave starts the row's sum from P and adds the last
+// FW3_NEAR columns and the triangle itself. Same terms, same order: the
+// result is bit-identical. The L band (8 B per nonzero) is then read by
+// NH + 1 CUs instead of one. Hand-offs: write-through (sc1) stores, drained,
+// then a relaxed agent-scope flag; sc1 loads on the reading side
+// (MI355X_MICROARCH.md "Valid forms", row 1).
+constexpr int FW3_NEAR = 192;  // columns left of the block that the solving wave adds itself
+constexpr int FW3_HELPERS = 16;  // helper workgroups per RHS column
+
+template <typename T, int NW, int FW2_PF, int NH = 0>
 __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
                                                          const T* __restrict__ B, T* __restrict__ Y,
-                                                         unsigned long long* __restrict__ trace) {
+                                                         unsigned long long* __restrict__ trace,
+                                                         T* __restrict__ P = nullptr, int* __restrict__ pflag = nullptr,
+                                                         int* __restrict__ gfront = nullptr,
+                                                         int* __restrict__ status = nullptr) {
     using A = Arith<T>;
     __shared__ T yr[FW2_RING];
     __shared__ T tri[2][64][64];  // tri[buf][t][l] = L[i0 + l][i0 + t]
     __shared__ int frontier;      // y[0 .. frontier) are final in yr
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const T* bc = B + (int64_t)blockIdx.x * n;
-    T* yc = Y + (int64_t)blockIdx.x * n;
+    const int64_t colx = blockIdx.x / (1 + NH);
+    const int role = (int)(blockIdx.x % (1 + NH));
+    const T* bc = B + colx * n;
+    T* yc = Y + colx * n;
+    const int64_t nblk = (n + 63) / 64;
+    const int64_t pad_off = n * ld;  // band_pad zeros follow the band
+    if constexpr (NH > 0) {
+        P += colx * nblk * 64;
+        pflag += colx * nblk;
+        gfront += colx;
+        if (role > 0) {  // ---- helper: prefixes of the rows' sums, block by block
+            const uint32_t stride = (uint32_t)(ld - 1);  // L[i][jj] = CB[i + jj * (ld - 1)]
+            int64_t gf = 0;
+            for (int64_t blk = (int64_t)(role - 1) * NW + w; blk < nblk; blk += (int64_t)NH * NW) {
+                const int64_t i0 = blk * 64, i = i0 + lane;
+                const bool live = i < n;
+                const int64_t j0 = i0 - b > 0 ? i0 - b : 0, jn = i0 - FW3_NEAR;
+                if (jn <= j0) continue;  // the solving wave forms the whole sum
+                constexpr int HB = 32;  // terms per batch: one round trip for its L and y loads
+                const long long h0 = trace ? clock64() : 0;
+                long long hw = 0;
+                T s = A::zero();
+                for (int64_t j = j0; j < jn; j += HB) {
+                    const int64_t je = j + HB < jn ? j + HB : jn;
+                    long long spins = 0;
+                    const long long hw0 = trace && gf < je ? clock64() : 0;
+                    if (trace && gf < je) hw -= hw0;
+                    while (gf < je) {  // y[0 .. je) published (polled only when the cached value is short)
+                        gf = __hip_atomic_load(gfront, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (gf >= je) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > SPIN_LIMIT) {
+                            if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                            gf = INT64_MAX;
+                        }
+                    }
+                    if (trace && hw0) hw += clock64();
+                    T lv[HB], yv[HB];
+#pragma unroll
+                    for (int q = 0; q < HB; ++q) {  // out of band / past je: a zero of the padding
+                        const int64_t jj = j + q;
+                        const bool ok = live & (jj < je) & (i - jj <= b);
+                        lv[q] = CB[(ok ? i : pad_off) + (int64_t)((uint64_t)(ok ? (uint32_t)jj : 0u) * stride)];
+                        yv[q] = ld_sc1(&yc[jj < je ? jj : je - 1]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < HB; ++q) s = A::add(s, j + q < je ? A::mul(lv[q], yv[q]) : A::zero());
+                }
+                if (live) st_sc1(&P[i], s);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(&pflag[blk], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (trace && lane == 0) {
+                    atomicAdd(&trace[5], (unsigned long long)(clock64() - h0));
+                    atomicAdd(&trace[6], (unsigned long long)hw);
+                    atomicAdd(&trace[7], 1ull);
+                }
+            }
+            return;
+        }
+    }
     if (threadIdx.x == 0) frontier = 0;
     __syncthreads();
     // LDS atomics on the __shared__ counter itself (a volatile generic
     // pointer compiles to flat_* accesses, and a flat store is waited on
     // with vmcnt(0) together with the global y store)
     auto fr_load = [&]() -> int64_t { return __hip_atomic_load(&frontier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    const int64_t nblk = (n + 63) / 64;
-    const int64_t pad_off = n * ld;  // band_pad zeros follow the band
     // diagnostic (BSM_FW_TRACE): cycles per block in the far phase, waiting
     // for the previous block, and solving the block -- summed over blocks
-    long long t_far = 0, t_wait = 0, t_step = 0, t_spin = 0;
+    long long t_far = 0, t_wait = 0, t_step = 0, t_spin = 0, t_pwait = 0;
     for (int64_t blk = w; blk < nblk; blk += NW) {
         const long long c0 = trace ? clock64() : 0;
         const int64_t i0 = blk * 64, i = i0 + lane;
@@ -1001,12 +1092,21 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
         // t). Staged once block blk - 2 is solved: tri[buf] was block blk - 2's
         // and block blk - 1 (being solved meanwhile) uses the other buffer.
         bool staged = false;
-        auto stage_tri = [&]() {
-            for (int t = 0; t < 64; ++t) {
-                const int64_t a = (i0 + t) * ld + (lane - t);
-                const bool ok = live && lane > t && lane - t <= b;
-                const T v = CB[ok ? a : 0];
-                tri[buf][t][lane] = ok ? v : A::zero();
+        auto stage_tri = [&]() {  // 16 loads in flight at a time (a load-store loop waits per row)
+#pragma unroll 1
+            for (int h = 0; h < 64; h += 16) {
+                T v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int t = h + q;
+                    const bool ok = live && lane > t && lane - t <= b;
+                    v[q] = CB[ok ? (i0 + t) * ld + (lane - t) : 0];
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int t = h + q;
+                    tri[buf][t][lane] = (live && lane > t && lane - t <= b) ? v[q] : A::zero();
+                }
             }
             staged = true;
         };
@@ -1025,6 +1125,13 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
         // out-of-band terms (j < i - b) are +0 products
         T s = A::zero();
         int64_t j = i0 - b > 0 ? i0 - b : 0;
+        bool from_helper = false;  // the prefix [j, i0 - FW3_NEAR) comes from a helper
+        if constexpr (NH > 0) {
+            if (i0 - FW3_NEAR > j) {
+                from_helper = true;
+                j = i0 - FW3_NEAR;
+            }
+        }
         // L[i][jj], or a zero of the band's padding outside the band / past
         // the matrix: the ADDRESS is selected, the load is unconditional (a
         // load under a branch costs a vmcnt(0) per term)
@@ -1045,6 +1152,21 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
         for (int q = 0; q < FW2_PF; ++q) {
             pa[q] = lfar(j + q);
             pb[q] = lfar(j + FW2_PF + q);
+        }
+        if constexpr (NH > 0) {
+            if (from_helper) {  // after the first loads of the near terms are in flight
+                const long long cp = trace ? clock64() : 0;
+                long long spins = 0;
+                while (__hip_atomic_load(&pflag[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > SPIN_LIMIT) {
+                        if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                        break;
+                    }
+                }
+                s = live ? ld_sc1(&P[i]) : A::zero();
+                if (trace) t_pwait += clock64() - cp;
+            }
         }
         auto batch = [&](T (&pf)[FW2_PF]) {
             const int64_t need = j + FW2_PF < i0 ? j + FW2_PF : i0;
@@ -1070,19 +1192,45 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
         const long long c1 = trace ? clock64() : 0;
         wait_frontier(i0);  // block blk - 1 solved (and the triangle staged)
         const long long c2 = trace ? clock64() : 0;
-        // the block: one row per step
+        // the block: one row per step. The solving wave runs at raised priority
+        // (the other waves stream far terms on the same SIMDs)
         const int nb = (int)(n - i0 < 64 ? n - i0 : 64);
-        for (int t = 0; t < nb; ++t) {
+        const T rl = div_rn((T)1, lii);  // for div_by: off the chain
+        __builtin_amdgcn_s_setprio(3);
+        auto row = [&](int t) __attribute__((always_inline)) {
             const T lt = tri[buf][t][lane];  // read before the division: off the chain
-            const T yv = div_rn(A::sub(bi, s), lii);
+            const T yv = div_by(A::sub(bi, s), lii, rl);
             const T y = readlane_t(yv, t);
             if (lane == t) {
                 yr[(i0 + t) & (FW2_RING - 1)] = y;
-                yc[i0 + t] = y;
-                // y is in LDS before the frontier moves (LDS ops of one lane complete in order)
-                __hip_atomic_store(&frontier, (int)(i0 + t + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if constexpr (NH > 0) st_sc1(&yc[i0 + t], y);  // read by the helpers on other CUs
+                else yc[i0 + t] = y;
+                // y is in LDS before the frontier moves: LDS ops of one wave are performed
+                // in order, so a relaxed store suffices (a release would wait for the y stores)
+                __hip_atomic_store(&frontier, (int)(i0 + t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if (lane > t) s = A::add(s, A::mul(lt, y));
+        };
+        if (nb == 64) {
+#pragma unroll 8
+            for (int t = 0; t < 64; ++t) row(t);
+        } else {
+            for (int t = 0; t < nb; ++t) row(t);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if constexpr (NH > 0) {
+            // publish the block's y to the helpers: this wave's stores drained, and only
+            // after the previous block's wave has published (its stores are not ours to drain)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            long long spins = 0;
+            while (__hip_atomic_load(gfront, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT) {
+                    if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                    break;
+                }
+            }
+            if (lane == 0) __hip_atomic_store(gfront, (int)(i0 + nb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (trace) {
             const long long c3 = clock64();
@@ -1096,6 +1244,7 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
         atomicAdd(&trace[1], (unsigned long long)t_wait);
         atomicAdd(&trace[2], (unsigned long long)t_step);
         atomicAdd(&trace[3], (unsigned long long)t_spin);
+        atomicAdd(&trace[4], (unsigned long long)t_pwait);
     }
 }
 
@@ -1888,8 +2037,8 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
             DBuf ftr;
             unsigned long long* ftp = nullptr;
             if (getenv("BSM_FW_TRACE")) {
-                BSM_TRY(ftr.alloc(4 * sizeof(unsigned long long)));
-                BSM_HIP_TRY(hipMemsetAsync(ftr.p, 0, 4 * sizeof(unsigned long long), s));
+                BSM_TRY(ftr.alloc(8 * sizeof(unsigned long long)));
+                BSM_HIP_TRY(hipMemsetAsync(ftr.p, 0, 8 * sizeof(unsigned long long), s));
                 ftp = ftr.as<unsigned long long>();
             }
             if ((fv && atoi(fv) == 1) || bd.b + 16 * 64 + 64 > FW2_RING)
@@ -1901,19 +2050,38 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
             else if (fv && atoi(fv) == 3)
                 band_forward2<T, 16, 8><<<(unsigned)k, 1024, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
                                                                      bc.as<T>(), yc.as<T>(), ftp);
-            else
+            else if ((fv && atoi(fv) == 4) || bd.b <= FW3_NEAR || k * (1 + FW3_HELPERS) > 256)
                 band_forward2<T, 8, 24><<<(unsigned)k, 512, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
                                                                     bc.as<T>(), yc.as<T>(), ftp);
+            else {  // default: the far prefixes on FW3_HELPERS helper workgroups per column
+                const uint64_t nblk = (n + 63) / 64;
+                DBuf pbuf, flags;
+                BSM_TRY(pbuf.alloc(k * nblk * 64 * sizeof(T)));
+                BSM_TRY(flags.alloc((k * nblk + k + 1) * sizeof(int)));
+                BSM_HIP_TRY(hipMemsetAsync(flags.p, 0, (k * nblk + k + 1) * sizeof(int), s));
+                int* pflag = flags.as<int>();
+                int* gfront = pflag + k * nblk;
+                int* fst = gfront + k;
+                band_forward2<T, 8, 8, FW3_HELPERS><<<(unsigned)(k * (1 + FW3_HELPERS)), 512, 0, s>>>(
+                    (int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), bc.as<T>(), yc.as<T>(), ftp, pbuf.as<T>(), pflag, gfront,
+                    fst);
+                BSM_HIP_TRY(hipGetLastError());
+                int st = 0;
+                BSM_HIP_TRY(read_dev(&st, fst, sizeof(int), s));
+                BSM_HIP_TRY(hipStreamSynchronize(s));
+                BSM_REQUIRE(!(st & ST_TIMEOUT), BSM_ERR_HIP, "forward: helper hand-off timed out");
+            }
             BSM_HIP_TRY(hipGetLastError());
             if (ftp) {
-                unsigned long long h[4];
+                unsigned long long h[8];
                 BSM_HIP_TRY(hipMemcpyAsync(h, ftp, sizeof(h), hipMemcpyDeviceToHost, s));
                 BSM_HIP_TRY(hipStreamSynchronize(s));
-                const double nb = (double)((n + 63) / 64) * (double)k;
+                const double nb = (double)((n + 63) / 64) * (double)k, hb = h[7] ? (double)h[7] : 1.0;
                 fprintf(stderr,
                         "[bsm fw trace] cycles per 64-row block: far phase %.0f (of which waiting for the "
-                        "frontier %.0f), wait %.0f, solve %.0f\n",
-                        h[0] / nb, h[3] / nb, h[1] / nb, h[2] / nb);
+                        "frontier %.0f, for the helper prefix %.0f), wait %.0f, solve %.0f; helper blocks %llu: "
+                        "%.0f cycles each, %.0f of them waiting for y\n",
+                        h[0] / nb, h[3] / nb, h[4] / nb, h[1] / nb, h[2] / nb, h[7], h[5] / hb, h[6] / hb);
             }
             BSM_TRY(launch_backward<T>(n, k, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(), xc.as<T>(), s));
         }

@@ -194,6 +194,29 @@ def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_forward_helper_prefixes_vs_oracle(orc, monkeypatch, dtype):
+    """Bandwidth 200 > FW3_NEAR: the default forward solve takes the far
+    prefixes of the rows' sums from helper workgroups; with 3 RHS columns
+    (three solver/helper groups) the solution equals the single-workgroup
+    kernel (BSM_FW_VARIANT=4) and the band oracle bit for bit."""
+    g = 200
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    v = v.astype(dtype)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    b = orc.gen_x_cols(1004, n, 3, dtype=dtype)
+    ex = orc.solve(n, rp, ci, v, b, band=True)
+    got = {}
+    for fv in ("0", "4"):
+        monkeypatch.setenv("BSM_FW_VARIANT", fv)
+        x = solve(A, Dense.from_columns(b))
+        got[fv] = [bits(x.get_col(j)).tolist() for j in range(3)]
+    for j in range(3):
+        assert got["0"][j] == bits(ex[j]).tolist()
+        assert got["4"][j] == got["0"][j]
+
+
 def test_poisson_250_bit_exact_solve_f64(orc):
     """62,500 unknowns, bandwidth 250: GPU solve == band oracle bit for bit."""
     g = 250
