@@ -1642,6 +1642,217 @@ __global__ __launch_bounds__(64) void csr_backward(int64_t n, const int64_t* __r
     }
 }
 
+// ---------------------------------------------------------------------------
+// Blocked band solves (bsm_solve_blocked): the same L L^T x = b as solve
+// (lib.rs:11-24), with the sums REASSOCIATED. Not bit-exact with the
+// reference; within its f64 tolerance (relative error of a backward-stable
+// solve, tests/test_gpu_solver_blocked.py). The rows are cut into 64-row
+// blocks I. Forward (L y = b):
+//     y_I = Linv_I (b_I - sum_{J <= I-2} L_{I,J} y_J) - MF_I y_{I-1},
+//     Linv_I = L_{I,I}^-1,  MF_I = Linv_I L_{I,I-1};
+// backward (L^T x = y):
+//     x_I = Linv_I^T (y_I - sum_{J >= I+2} L_{J,I}^T x_J) - MB_I^T x_{I+1},
+//     MB_I = L_{I+1,I} Linv_I.
+// Linv, MF, MB depend on L only (blk_prep, fully parallel). In the solve the
+// far sums run ahead on many workgroups; the serial chain per block is one
+// 64 x 64 matrix-vector product (MF_I or MB_I) in one wave, against the N*b
+// dependent adds of the reference order (band_backward_reg).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __fma_rn(a, b, c); }
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __fmaf_rn(a, b, c); }
+
+// M[q * 64 + l] layouts (one 64 x 64 matrix per block, 4096 elements):
+//   G[I]  = Linv_I[l][q]   (forward:  u[l] = sum_q Linv[l][q] r[q])
+//   H[I]  = Linv_I[q][l]   (backward: u[l] = sum_q Linv[q][l] r[q])
+//   MF[I] = MF_I[l][q],  MB[I] = MB_I[q][l]
+template <typename T>
+__global__ __launch_bounds__(256) void blk_prep(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                T* __restrict__ G, T* __restrict__ H, T* __restrict__ MF,
+                                                T* __restrict__ MB) {
+    __shared__ T Ls[64][65];  // Ls[r][c] = L[i0 + r][i0 + c] (r >= c); identity rows past n
+    __shared__ T Xs[64][65];  // Linv
+    __shared__ T As[64][65];  // the neighbouring block, then the product
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t I = blockIdx.x, i0 = I * 64, nb64 = (n + 63) / 64;
+    const int64_t o = I * 4096;
+    for (int e = tid; e < 4096; e += 256) {  // r fastest: a column's rows are contiguous in CB
+        const int r = e & 63, c = e >> 6;
+        const int64_t i = i0 + r;
+        T v = (T)0;
+        if (r == c) v = i < n ? CB[i * ld] : (T)1;
+        else if (r > c && i < n && r - c <= b) v = CB[(i0 + c) * ld + (r - c)];
+        Ls[r][c] = v;
+    }
+    __syncthreads();
+    if (w == 0) {  // lane l forms column l of the inverse: L x = e_l, rows ascending
+        T x[64];
+#pragma unroll
+        for (int r = 0; r < 64; ++r) {
+            T acc = (T)0;
+#pragma unroll
+            for (int t = 0; t < r; ++t) acc = fma_t(Ls[r][t], x[t], acc);
+            x[r] = ((r == lane ? (T)1 : (T)0) - acc) / Ls[r][r];
+        }
+#pragma unroll
+        for (int r = 0; r < 64; ++r) Xs[r][lane] = x[r];
+    }
+    __syncthreads();
+    for (int e = tid; e < 4096; e += 256) {
+        const int q = e >> 6, l = e & 63;
+        G[o + e] = Xs[l][q];
+        H[o + e] = Xs[q][l];
+    }
+    if (I > 0) {  // MF = Linv L_{I,I-1}: As[t][c] = L[i0 + t][i0 - 64 + c]
+        for (int e = tid; e < 4096; e += 256) {
+            const int t = e & 63, c = e >> 6;
+            const int64_t i = i0 + t;
+            As[t][c] = (i < n && t + 64 - c <= b) ? CB[(i0 - 64 + c) * ld + (t + 64 - c)] : (T)0;
+        }
+        __syncthreads();
+        T acc[16];
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) acc[rr] = (T)0;
+        for (int t = 0; t < 64; ++t) {
+            const T a = As[t][lane];
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) acc[rr] = fma_t(Xs[16 * w + rr][t], a, acc[rr]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) As[16 * w + rr][lane] = acc[rr];  // MF[r][c]
+        __syncthreads();
+        for (int e = tid; e < 4096; e += 256) MF[o + e] = As[e & 63][e >> 6];
+        __syncthreads();
+    }
+    if (I + 1 < nb64) {  // MB = L_{I+1,I} Linv: As[a][t] = L[i0 + 64 + a][i0 + t]
+        for (int e = tid; e < 4096; e += 256) {
+            const int a = e & 63, t = e >> 6;
+            const int64_t i = i0 + 64 + a;
+            As[a][t] = (i < n && a + 64 - t <= b) ? CB[(i0 + t) * ld + (a + 64 - t)] : (T)0;
+        }
+        __syncthreads();
+        T acc[16];
+#pragma unroll
+        for (int aa = 0; aa < 16; ++aa) acc[aa] = (T)0;
+        for (int t = 0; t < 64; ++t) {
+            const T xv = Xs[t][lane];
+#pragma unroll
+            for (int aa = 0; aa < 16; ++aa) acc[aa] = fma_t(As[16 * w + aa][t], xv, acc[aa]);
+        }
+#pragma unroll
+        for (int aa = 0; aa < 16; ++aa) MB[o + (16 * w + aa) * 64 + lane] = acc[aa];
+    }
+}
+
+// One 64-row block per ticket; tickets are taken in dependency order (per RHS
+// column, FWD: blocks ascending, else descending), so a workgroup only waits
+// on blocks already held by running workgroups. Y: padded solution columns
+// (nb64 * 64 each), flags[col * nb64 + I] = 1 once block I of Y is final
+// (write-through stores, drained, then a relaxed agent-scope flag; sc1 loads
+// on the reading side: MI355X_MICROARCH.md "Valid forms", row 1).
+template <typename T, bool FWD>
+__global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
+                                                const T* __restrict__ Minv, const T* __restrict__ Madj,
+                                                const T* __restrict__ rhs, int64_t rhs_stride, T* __restrict__ Y,
+                                                int* __restrict__ flags, int* __restrict__ ticket,
+                                                int* __restrict__ status, int64_t k) {
+    __shared__ T red[4][64];
+    __shared__ T rv[64];
+    __shared__ int64_t tk;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nb64 = (n + 63) / 64, NP = nb64 * 64, pad_off = n * ld;
+    auto wait_flag = [&](const int* f) {
+        long long spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > SPIN_LIMIT) {
+                if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                return;
+            }
+        }
+    };
+    for (;;) {
+        if (threadIdx.x == 0) tk = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int64_t t = tk;
+        if (t >= nb64 * k) break;
+        const int64_t col = t % k, step = t / k;
+        const int64_t I = FWD ? step : nb64 - 1 - step, i0 = I * 64, i = i0 + lane;
+        T* Yc = Y + col * NP;
+        int* fl = flags + col * nb64;
+        const bool has_adj = FWD ? I > 0 : I + 1 < nb64;
+        // x-independent operands first: this wave's slice of Linv, wave 0's coupling matrix
+        T minv[16], madj[64];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) minv[q] = Minv[I * 4096 + (16 * w + q) * 64 + lane];
+        if (w == 0 && has_adj) {
+#pragma unroll
+            for (int q = 0; q < 64; ++q) madj[q] = Madj[I * 4096 + q * 64 + lane];
+        }
+        // far blocks: FWD columns [max(0, i0 - b), i0 - 64), else [i0 + 128, i0 + 63 + b];
+        // wave w takes columns 16w .. 16w + 15 of each, lane = row
+        T acc = (T)0;
+        int64_t J0, J1;  // in the order their solutions complete
+        if (FWD) {
+            J0 = (i0 - b > 0 ? i0 - b : 0) / 64;
+            J1 = I - 2;
+        } else {
+            const int64_t jl = i0 + 63 + b < n - 1 ? i0 + 63 + b : n - 1;
+            J0 = jl / 64;
+            J1 = I + 2;
+        }
+        for (int64_t J = J0; FWD ? J <= J1 : J >= J1; J += FWD ? 1 : -1) {
+            T lv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t j = J * 64 + 16 * w + q;
+                // L[i][j] (FWD) or L[j][i]: in the band and the matrix, else a zero of the padding
+                const bool ok = FWD ? (i < n) & (i - j <= b) : (j < n) & (j - i <= b);
+                const int64_t idx = FWD ? j * ld + (i - j) : i * ld + (j - i);
+                lv[q] = CB[ok ? idx : pad_off];
+            }
+            wait_flag(&fl[J]);
+            const T v = ld_sc1(&Yc[J * 64 + lane]);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc = fma_t(lv[q], readlane_t(v, 16 * w + q), acc);
+        }
+        red[w][lane] = acc;
+        __syncthreads();
+        if (w == 0) {
+            const T bi = i < n ? rhs[col * rhs_stride + i] : (T)0;
+            rv[lane] = bi - ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
+        }
+        __syncthreads();
+        T uu = (T)0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) uu = fma_t(minv[q], rv[16 * w + q], uu);
+        red[w][lane] = uu;
+        __syncthreads();
+        if (w == 0) {
+            T u = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+            if (has_adj) {  // the serial step: the neighbour's solution through the coupling matrix
+                const int64_t Ja = FWD ? I - 1 : I + 1;
+                wait_flag(&fl[Ja]);
+                const T v = ld_sc1(&Yc[Ja * 64 + lane]);
+                T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+                for (int q = 0; q < 64; q += 4) {
+                    s0 = fma_t(madj[q], readlane_t(v, q), s0);
+                    s1 = fma_t(madj[q + 1], readlane_t(v, q + 1), s1);
+                    s2 = fma_t(madj[q + 2], readlane_t(v, q + 2), s2);
+                    s3 = fma_t(madj[q + 3], readlane_t(v, q + 3), s3);
+                }
+                u = u - ((s0 + s1) + (s2 + s3));
+            }
+            st_sc1(&Yc[i], u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&fl[I], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    }
+}
+
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 // --------------------------------------------------------------------------
@@ -2084,6 +2295,70 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
                         h[0] / nb, h[3] / nb, h[4] / nb, h[1] / nb, h[2] / nb, h[7], h[5] / hb, h[6] / hb);
             }
             BSM_TRY(launch_backward<T>(n, k, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(), xc.as<T>(), s));
+        }
+        BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        return BSM_OK;
+    };
+    if (a->dtype == BSM_F64) return run.template operator()<double>();
+    if (a->dtype == BSM_F32) return run.template operator()<float>();
+    set_error("solve: f32/f64 only");
+    return BSM_ERR_INVALID;
+}
+
+// solve with reassociated (blocked) triangular solves: the factor is the
+// reference-order band Cholesky; the two solves are blk_trsv (see there).
+int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev,
+                           hipStream_t s) {
+    auto run = [&]<typename T>() -> int {
+        BSM_REQUIRE(a->rows == n, BSM_ERR_PANIC,
+                    "solve: b has %llu rows but A has %llu (index out of bounds in the reference)",
+                    (unsigned long long)n, (unsigned long long)a->rows);
+        Band bd;
+        BSM_TRY(band_factor<T>(a, bd, s));
+        DBuf bc, xc;
+        BSM_TRY(to_colmajor(a->dtype, n, k, b_dev, bc, s));
+        BSM_TRY(xc.alloc(n * k * sizeof(T)));
+        if (n && k) {
+            const uint64_t nb64 = (n + 63) / 64, NP = nb64 * 64;
+            DBuf g, h, mf, mb, yp, xp, fl;
+            BSM_TRY(g.alloc(nb64 * 4096 * sizeof(T)));
+            BSM_TRY(h.alloc(nb64 * 4096 * sizeof(T)));
+            BSM_TRY(mf.alloc(nb64 * 4096 * sizeof(T)));
+            BSM_TRY(mb.alloc(nb64 * 4096 * sizeof(T)));
+            BSM_TRY(yp.alloc(k * NP * sizeof(T)));
+            BSM_TRY(xp.alloc(k * NP * sizeof(T)));
+            const uint64_t nfl = 2 * k * nb64 + 4;  // forward flags, backward flags, 2 tickets, status
+            BSM_TRY(fl.alloc(nfl * sizeof(int)));
+            BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
+            int* ff = fl.as<int>();
+            int* fb = ff + k * nb64;
+            int* tix = fb + k * nb64;
+            int* st = tix + 2;
+            blk_prep<T><<<(unsigned)nb64, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), g.as<T>(), h.as<T>(),
+                                                      mf.as<T>(), mb.as<T>());
+            BSM_HIP_TRY(hipGetLastError());
+            int dev = 0, cus = 0, per_cu = 0;
+            BSM_HIP_TRY(hipGetDevice(&dev));
+            BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, blk_trsv<T, false>, 256, 0));
+            BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_trsv does not fit a CU");
+            uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
+            if (grid > nb64 * k) grid = nb64 * k;
+            blk_trsv<T, true><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), g.as<T>(),
+                                                            mf.as<T>(), bc.as<T>(), (int64_t)n, yp.as<T>(), ff,
+                                                            tix, st, (int64_t)k);
+            BSM_HIP_TRY(hipGetLastError());
+            blk_trsv<T, false><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), h.as<T>(),
+                                                             mb.as<T>(), yp.as<T>(), (int64_t)NP, xp.as<T>(), fb,
+                                                             tix + 1, st, (int64_t)k);
+            BSM_HIP_TRY(hipGetLastError());
+            int hst = 0;
+            BSM_HIP_TRY(read_dev(&hst, st, sizeof(int), s));
+            BSM_HIP_TRY(hipStreamSynchronize(s));
+            BSM_REQUIRE(!(hst & ST_TIMEOUT), BSM_ERR_HIP, "blocked solve: block hand-off timed out");
+            BSM_HIP_TRY(hipMemcpy2DAsync(xc.p, n * sizeof(T), xp.p, NP * sizeof(T), n * sizeof(T), k,
+                                         hipMemcpyDeviceToDevice, s));
         }
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));

@@ -145,6 +145,13 @@ int bsm_backward_substitution(const bsm_csr* u, uint64_t k, uint64_t n,
  * forward/backward substitution, all on the device. */
 int bsm_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
               void* const* x_cols);
+/* solve (lib.rs:11-24) with the triangular solves REASSOCIATED: 64-row
+ * blocks, precomputed inverse diagonal blocks, far sums in any order. The
+ * factor is the reference-order one; x is NOT bit-exact with the reference but
+ * within its f64 tolerance (1e-6 relative, BASELINE.json north_star). Same
+ * arguments, errors and panics as bsm_solve. This build's addition. */
+int bsm_solve_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
+                      void* const* x_cols);
 
 /* ---- device-level entry points (HBM pointers, async on `stream`) --------- */
 /* Synthetic CSR generator (bsm_synth.h recipe): rows [row0, row0+rows) of a

@@ -19,6 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--g", type=int, default=1000)
 ap.add_argument("--dtype", default="f64")
 ap.add_argument("--reps", type=int, default=1)
+ap.add_argument("--order", default="reference", choices=["reference", "blocked"])
 args = ap.parse_args()
 dt = np.float64 if args.dtype == "f64" else np.float32
 g = args.g
@@ -32,7 +33,7 @@ A = Csr.from_csr_arrays((n, n), rp, ci, v.astype(dt))
 B = Dense.from_columns([b.astype(dt)])
 for r in range(args.reps):
     t0 = time.perf_counter()
-    x = solve(A, B).get_col(0)
+    x = solve(A, B, order=args.order).get_col(0)
     t = time.perf_counter() - t0
     rel = np.linalg.norm(x.astype(np.float64) - x_true) / np.linalg.norm(x_true)
-    print(f"C5 g={g} N={n} {args.dtype}: solve wall {t:.3f} s (incl. H2D/D2H), rel err vs x_true {rel:.3e}", flush=True)
+    print(f"C5 g={g} N={n} {args.dtype} order={args.order}: solve wall {t:.3f} s (incl. H2D/D2H), rel err vs x_true {rel:.3e}", flush=True)
