@@ -29,6 +29,11 @@
 #include <utility>
 #include <vector>
 
+#include <unistd.h>
+
+#include <atomic>
+#include <thread>
+
 #include "bsm_internal.hpp"
 
 namespace bsm {
@@ -1692,6 +1697,7 @@ __global__ __launch_bounds__(256) void blk_prep(int64_t n, int64_t b, int64_t ld
 #pragma unroll
             for (int t = 0; t < r; ++t) acc = fma_t(Ls[r][t], x[t], acc);
             x[r] = ((r == lane ? (T)1 : (T)0) - acc) / Ls[r][r];
+            asm volatile("" ::: "memory");
         }
 #pragma unroll
         for (int r = 0; r < 64; ++r) Xs[r][lane] = x[r];
@@ -1853,6 +1859,297 @@ __global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld
     }
 }
 
+// ---------------------------------------------------------------------------
+// Blocked band Cholesky (solve order="blocked"): left-looking over 64 x 64
+// tiles of the band, sums reassociated (FMA, any order). Tile (I, K), I >= K:
+//     S = A_{I,K} - sum_{J < K} L_{I,J} L_{K,J}^T
+//     I == K: L_{K,K} = chol(S), Dinv[K] = L_{K,K}^-1 (G layout of blk_prep)
+//     I >  K: L_{I,K} = S L_{K,K}^-T
+// One 256-thread workgroup per tile, tickets in (K, I - K) order, one flag per
+// tile (write-through stores, drained, then the flag). Out-of-band entries of
+// L are exact zeros (every product there has an out-of-band factor), so tiles
+// read zeros outside the band and write only inside it.
+// ---------------------------------------------------------------------------
+// LDS pointers that keep their address space across a call
+template <typename T> using lds_t = __attribute__((address_space(3))) T;
+
+// 1/sqrt(x): the hardware estimate and two Newton steps (error squares per
+// step): a short dependent chain for the blocked factor's pivots
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double h = __fma_rn(-x * y, y, 1.0);
+        y = __fma_rn(0.5 * y, h, y);
+    }
+    return y;
+}
+__device__ __forceinline__ float rsqrt_nr(float x) {
+    float y = __builtin_amdgcn_rsqf(x);
+    const float h = __fmaf_rn(-x * y, y, 1.0f);
+    return __fmaf_rn(0.5f * y, h, y);
+}
+
+// Factor the 64 x 64 tile S (P[r * 64 + c], lower part) in one wave, lane r =
+// row r: right-looking, column s broadcast through LDS (colb). Out of line: in
+// the ticket loop its 64 unrolled steps would share the register budget with
+// everything the compiler hoists there. P receives L (zero upper part), rd the
+// reciprocal pivots.
+template <typename T>
+__device__ __forceinline__ void blk_diag_factor(lds_t<T>* P, lds_t<T>* colb, lds_t<T>* rd, int* status, int ln) {
+    T a[64];
+#pragma unroll
+    for (int c = 0; c < 64; ++c) a[c] = P[ln * 64 + c];
+    bool pd = true;
+    // one instantiation per column s: a[] is only ever indexed by constants
+    auto step = [&]<int s>(std::integral_constant<int, s>) __attribute__((always_inline)) {
+        const T dd = readlane_t(a[s], s);
+        pd = pd & (dd > (T)0) & (dd < (T)INFINITY);
+        const T rp = rsqrt_nr(dd);
+        // every lane the same formula (no per-lane masks): lane s gets dd / sqrt(dd), the
+        // pivot; lanes above s form upper-triangle values that are never read and zeroed below
+        const T l = a[s] * rp;
+        a[s] = l;
+        rd[s] = rp;  // uniform value, every lane
+        if constexpr (s + 1 < 64) {
+            // the next pivot's column first, by v_readlane: the chain from pivot to
+            // pivot has no LDS round trip; the later columns take the LDS broadcast
+            a[s + 1] = fma_t(-l, readlane_t(l, s + 1), a[s + 1]);
+            colb[ln] = l;
+#pragma unroll
+            for (int c = s + 2; c < 64; ++c) {
+                if ((c & 31) == 0) asm volatile("" ::: "memory");  // at most 32 broadcast values in flight
+                a[c] = fma_t(-l, colb[c], a[c]);
+            }
+            asm volatile("" ::: "memory");
+        }
+    };
+    [&]<int... ss>(std::integer_sequence<int, ss...>) __attribute__((always_inline)) {
+        (step(std::integral_constant<int, ss>{}), ...);
+    }(std::make_integer_sequence<int, 64>{});
+    if (ln == 0 && !pd) atomicOr(status, ST_NOT_PD);
+#pragma unroll
+    for (int c = 0; c < 64; ++c) P[ln * 64 + c] = c <= ln ? a[c] : (T)0;
+}
+
+// Q[c * 64 + r] = Linv[r][c] for L in P (one wave, lane c forms column c of
+// the inverse, rows ascending)
+template <typename T>
+__device__ __forceinline__ void blk_diag_inverse(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* rd, int ln) {
+    T x[64];
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+        T s = (T)0;
+#pragma unroll
+        for (int q = 0; q < r; ++q) s = fma_t(P[r * 64 + q], x[q], s);
+        x[r] = ((r == ln ? (T)1 : (T)0) - s) * rd[r];
+        asm volatile("" ::: "memory");  // keep row r's LDS reads in step r (else all 2016 are hoisted)
+    }
+#pragma unroll
+    for (int r = 0; r < 64; ++r) Q[ln * 64 + r] = x[r];
+}
+
+// The same inverse on all 4 waves: a quad of lanes per column c = 16w + (lane
+// >> 2); lane j of the quad sums the terms q = j (mod 4) of each row's dot
+// product, two DPP butterfly adds give every lane of the quad the sum, and
+// lane j keeps x[4m + j] in xs[m]. The serial chain per row is r/4 FMAs
+// instead of r.
+template <int CTRL> __device__ __forceinline__ double dpp_quad(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL> __device__ __forceinline__ float dpp_quad(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <typename T>
+__device__ __forceinline__ void blk_diag_inverse4(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* rd, int tid) {
+    asm volatile("" : "+v"(tid));  // opaque: keep the per-row masks out of the ticket loop
+    const int c = tid >> 2, j = tid & 3;
+    T xs[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) xs[m] = (T)0;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+        T s = (T)0;
+#pragma unroll
+        for (int m = 0; m < (r + 3) / 4; ++m) {  // q = 4m + j < r
+            const T p = P[r * 64 + 4 * m + j];
+            s = fma_t(4 * m + j < r ? p : (T)0, xs[m], s);
+        }
+        s = s + dpp_quad<0xb1>(s);  // quad_perm [1,0,3,2]
+        s = s + dpp_quad<0x4e>(s);  // quad_perm [2,3,0,1]
+        const T xr = ((r == c ? (T)1 : (T)0) - s) * rd[r];
+        xs[r / 4] = j == (r & 3) ? xr : xs[r / 4];
+        asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) Q[c * 64 + 4 * m + j] = xs[m];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
+                                                T* __restrict__ Dinv, int* __restrict__ flags,
+                                                int* __restrict__ ticket, int* __restrict__ status,
+                                                unsigned long long* __restrict__ dbg) {
+    __shared__ T PT[64][64];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
+    __shared__ T QT[64][64];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
+    __shared__ T rd[64];
+    __shared__ int64_t tk;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tr = tid >> 4, tc = tid & 15;  // this thread's 4 x 4 outputs: rows 4tr.., cols 4tc..
+    const int64_t nb64 = (n + 63) / 64, DM = (63 + b) / 64 + 1;  // tiles per block column (incl. diagonal)
+    auto wait_flag = [&](const int* f) {
+        long long spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (dbg && spins == 100000 && tid == 0) {  // BSM_BLK_DEBUG: which flag a stuck tile waits on
+                __hip_atomic_store(&dbg[1], (unsigned long long)(f - flags), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(&dbg[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (++spins > SPIN_LIMIT) {
+                if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                return;
+            }
+        }
+    };
+    // element (r, c) of tile (I, K) in the band: offset (c-th column, band row 64(I-K) + r - c)
+    auto in_band = [&](int64_t I, int64_t K, int r, int c) -> bool {
+        const int64_t off = 64 * (I - K) + r - c;
+        return (off >= 0) & (off <= b) & (64 * I + r < n);
+    };
+    auto band_idx = [&](int64_t I, int64_t K, int r, int c) -> int64_t {
+        return (64 * K + c) * ld + 64 * (I - K) + r - c;
+    };
+    // stage the transpose of tile (I, J) of L: X[t][r] = L[64I + r][64J + t] (sc1: other workgroups wrote it)
+    auto stage = [&](T (*X)[64], int64_t I, int64_t J) {
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = e & 63, t = e >> 6;
+            X[t][r] = in_band(I, J, r, t) ? ld_sc1(&CB[band_idx(I, J, r, t)]) : (T)0;
+        }
+    };
+    for (;;) {
+        if (tid == 0) tk = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int64_t t = tk;
+        if (dbg && tid == 0) __hip_atomic_fetch_max(&dbg[0], (unsigned long long)t, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t >= nb64 * DM) break;
+        const int64_t K = t / DM, d = t % DM, I = K + d;
+        int* fl = flags + K * DM;
+        if (I >= nb64 || 64 * d - 63 > b) {  // no such tile (past the matrix or the band)
+            __syncthreads();
+            continue;
+        }
+        T acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 4 * tr + i, c = 4 * tc + j;
+                // A itself (band_fill; rows past n: identity on the diagonal)
+                T a = in_band(I, K, r, c) ? CB[band_idx(I, K, r, c)] : (T)0;
+                if (d == 0 && r == c && 64 * I + r >= n) a = (T)1;
+                acc[i][j] = a;
+            }
+        // left-looking updates from block columns J in the band of both I and K
+        const int64_t Jlo = I - (DM - 1) > 0 ? I - (DM - 1) : 0;
+        for (int64_t J = Jlo; J < K; ++J) {
+            wait_flag(&flags[J * DM + (I - J)]);
+            if (d > 0) wait_flag(&flags[J * DM + (K - J)]);
+            stage(PT, I, J);
+            if (d > 0) stage(QT, K, J);
+            __syncthreads();
+            T (*Q)[64] = d > 0 ? QT : PT;
+#pragma unroll 4
+            for (int s = 0; s < 64; ++s) {
+                T pa[4], qb[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    pa[i] = PT[s][4 * tr + i];
+                    qb[i] = Q[s][4 * tc + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j] = fma_t(-pa[i], qb[j], acc[i][j]);
+            }
+            __syncthreads();
+        }
+        if (d == 0) {
+            const long long c0 = dbg ? clock64() : 0;
+            // S to LDS (PT[r][c]), then wave 0 factors it: lane r holds row r
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) PT[4 * tr + i][4 * tc + j] = acc[i][j];
+            __syncthreads();
+            if (w == 0) blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
+            __syncthreads();
+            const long long c1 = dbg ? clock64() : 0;
+            // L_{K,K} to the band (write-through) by all threads; wave 0 then inverts it
+            for (int e = tid; e < 4096; e += 256) {
+                const int r = e & 63, c = e >> 6;
+                if (r >= c && in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], PT[r][c]);
+            }
+            blk_diag_inverse4<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, tid);
+            __syncthreads();
+            if (dbg && tid == 0) {  // cycles: factor, inverse (BSM_BLK_DEBUG)
+                const long long c2 = clock64();
+                __hip_atomic_fetch_add(&dbg[4], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(&dbg[5], (unsigned long long)(c2 - c1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(&dbg[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            // Dinv[K][q * 64 + l] = Linv[l][q] = QT[q][l]
+            for (int e = tid; e < 4096; e += 256) st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+        } else {
+            const long long c0 = dbg ? clock64() : 0;
+            wait_flag(&fl[0]);  // L_{K,K} and its inverse
+            if (dbg && tid == 0 && d == 1)
+                __hip_atomic_fetch_add(&dbg[6], (unsigned long long)(clock64() - c0), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            // PT[s][r] = S[r][s]; QT[s][c] = Linv[c][s] = Dinv[K][s * 64 + c]
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = acc[i][j];
+            for (int e = tid; e < 4096; e += 256) QT[e >> 6][e & 63] = ld_sc1(&Dinv[K * 4096 + e]);
+            __syncthreads();
+            T o[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[i][j] = (T)0;
+#pragma unroll 4
+            for (int s = 0; s < 64; ++s) {
+                T pa[4], qb[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    pa[i] = PT[s][4 * tr + i];
+                    qb[i] = QT[s][4 * tc + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) o[i][j] = fma_t(pa[i], qb[j], o[i][j]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = 4 * tr + i, c = 4 * tc + j;
+                    if (in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], o[i][j]);
+                }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(&fl[d], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 // --------------------------------------------------------------------------
@@ -1940,16 +2237,16 @@ int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     return BSM_OK;
 }
 
+// A into the band layout CB (zeros elsewhere); bw_max: the widest band accepted
 template <typename T>
-int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
+int band_setup(const bsm_csr* a, Band& bd, hipStream_t s, int64_t bw_max) {
     int64_t bw = 0;
     bool sorted = true, empty = false;
     BSM_TRY(band_analyse(a, s, &bw, &sorted, &empty));
     BSM_REQUIRE(sorted, BSM_ERR_UNSUPPORTED,
                 "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
-    const int64_t need = bw + TR;  // accumulators per row pair lane set
-    BSM_REQUIRE(need <= 64 * 17, BSM_ERR_UNSUPPORTED, "cholesky: bandwidth %lld > %d not supported",
-                (long long)bw, 64 * 17 - TR);
+    BSM_REQUIRE(bw <= bw_max, BSM_ERR_UNSUPPORTED, "cholesky: bandwidth %lld > %lld not supported",
+                (long long)bw, (long long)bw_max);
     bd.n = (int64_t)a->rows;
     bd.b = bw;
     // the backward solve walks band_walk_terms(b) terms per row and reads the
@@ -1962,6 +2259,14 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     band_fill<T><<<nblk(bd.n, 256), 256, 0, s>>>(a->row_ptr, a->col, static_cast<const T*>(a->vals), bd.n, bd.ld,
                                                  bd.cb.as<T>());
     BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
+template <typename T>
+int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
+    BSM_TRY(band_setup<T>(a, bd, s, 64 * 17 - TR));  // accumulators per row pair lane set
+    if (bd.n == 0) return BSM_OK;
+    const int64_t bw = bd.b, need = bw + TR;
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
     DBuf prog;
     BSM_TRY(prog.alloc((n_tiles + 1) * sizeof(int) + 16));
@@ -2096,6 +2401,89 @@ int band_to_csr_host(const Band& bd, int dtype, bsm_csr** out, hipStream_t s) {
         return BSM_ERR_HIP;
     }
     *out = m;
+    return BSM_OK;
+}
+
+// BSM_BLK_WATCH: a passive host thread that names the step a blocked solve
+// is in if it takes longer than 15 s, then ends the process (no GPU calls)
+static std::atomic<const char*> g_blk_phase{"idle"};
+static std::atomic<int> g_blk_gen{0};
+static void blk_watch_start() {
+    if (!getenv("BSM_BLK_WATCH")) return;
+    const int gen = ++g_blk_gen;
+    std::thread([gen] {
+        for (int i = 0; i < 150; ++i) {
+            usleep(100000);
+            if (g_blk_gen.load() != gen) return;
+        }
+        fprintf(stderr, "[blk watch] stuck in: %s\n", g_blk_phase.load());
+        fflush(stderr);
+        _exit(3);
+    }).detach();
+}
+static void blk_watch_stop() { ++g_blk_gen; }
+
+// BSM_BLK_DEBUG: wait up to 10 s for the stream, else print the kernel's
+// progress (mapped host counters) and end the process (a hung kernel would
+// otherwise hold the test until its timeout)
+static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hdbg, long long tickets,
+                         long long grid) {
+    if (!getenv("BSM_BLK_DEBUG")) return;
+    for (int i = 0; i < 200; ++i) {
+        if (hipStreamQuery(s) == hipSuccess) {
+            fprintf(stderr, "[blk debug] %s done: tickets %lld grid %lld", what, tickets, grid);
+            if (hdbg && hdbg[7])
+                fprintf(stderr, "; per diagonal tile: factor %.0f cycles, inverse %.0f; tile (K+1, K) waits %.0f "
+                        "for the diagonal", (double)hdbg[4] / hdbg[7], (double)hdbg[5] / hdbg[7],
+                        (double)hdbg[6] / hdbg[7]);
+            fprintf(stderr, "\n");
+            return;
+        }
+        usleep(50000);
+    }
+    fprintf(stderr, "[blk debug] %s HUNG: tickets %lld grid %lld max ticket %llu, waiting on flag %llu "
+            "(stuck waits %llu), tiles done %llu\n", what, tickets, grid, hdbg ? hdbg[0] : 0ull,
+            hdbg ? hdbg[1] : 0ull, hdbg ? hdbg[2] : 0ull, hdbg ? hdbg[3] : 0ull);
+    fflush(stderr);
+    _exit(3);
+}
+
+// blocked (reassociated) band Cholesky into bd; Dinv (nb64 x 4096) receives
+// the inverse diagonal tiles
+template <typename T>
+int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
+    BSM_TRY(band_setup<T>(a, bd, s, (int64_t)1 << 16));
+    const int64_t n = bd.n, nb64 = (n + 63) / 64, DM = (63 + bd.b) / 64 + 1;
+    BSM_TRY(dinv.alloc((size_t)(nb64 > 0 ? nb64 : 1) * 4096 * sizeof(T)));
+    if (n == 0) return BSM_OK;
+    DBuf fl;
+    const size_t nfl = (size_t)(nb64 * DM + 2);
+    BSM_TRY(fl.alloc(nfl * sizeof(int)));
+    BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
+    int* flags = fl.as<int>();
+    int* tix = flags + nb64 * DM;
+    int* st = tix + 1;
+    int dev = 0, cus = 0, per_cu = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, blk_chol<T>, 256, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_chol does not fit a CU");
+    int64_t grid = (int64_t)cus * per_cu;
+    if (grid > nb64 * DM) grid = nb64 * DM;
+    unsigned long long* hdbg = nullptr;
+    if (getenv("BSM_BLK_DEBUG")) BSM_HIP_TRY(hipHostMalloc((void**)&hdbg, 8 * sizeof(unsigned long long), hipHostMallocCoherent));
+    if (hdbg) memset(hdbg, 0, 8 * sizeof(unsigned long long));
+    g_blk_phase = "blk_chol launch";
+    blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg);
+    BSM_HIP_TRY(hipGetLastError());
+    blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid);
+    g_blk_phase = "blk_chol sync";
+    int h = 0;
+    BSM_HIP_TRY(read_dev(&h, st, sizeof(int), s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    BSM_REQUIRE(!(h & ST_TIMEOUT), BSM_ERR_HIP, "blocked cholesky: tile hand-off timed out");
+    BSM_REQUIRE(!(h & ST_NOT_PD), BSM_ERR_UNSUPPORTED,
+                "cholesky: matrix is not positive definite (a pivot is <= 0 or not finite)");
     return BSM_OK;
 }
 
@@ -2314,8 +2702,14 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
         BSM_REQUIRE(a->rows == n, BSM_ERR_PANIC,
                     "solve: b has %llu rows but A has %llu (index out of bounds in the reference)",
                     (unsigned long long)n, (unsigned long long)a->rows);
+        blk_watch_start();
+        g_blk_phase = "band setup";
         Band bd;
-        BSM_TRY(band_factor<T>(a, bd, s));
+        DBuf dinv;
+        // BSM_BLK_CHOL=0: the reference-order factor (band_chol4) under the blocked solves (A/B)
+        const char* bc_env = getenv("BSM_BLK_CHOL");
+        if (bc_env && atoi(bc_env) == 0) BSM_TRY(band_factor<T>(a, bd, s));
+        else BSM_TRY(band_factor_blocked<T>(a, bd, dinv, s));
         DBuf bc, xc;
         BSM_TRY(to_colmajor(a->dtype, n, k, b_dev, bc, s));
         BSM_TRY(xc.alloc(n * k * sizeof(T)));
@@ -2335,6 +2729,7 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
             int* fb = ff + k * nb64;
             int* tix = fb + k * nb64;
             int* st = tix + 2;
+            g_blk_phase = "blk_prep + trsv launches";
             blk_prep<T><<<(unsigned)nb64, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), g.as<T>(), h.as<T>(),
                                                       mf.as<T>(), mb.as<T>());
             BSM_HIP_TRY(hipGetLastError());
@@ -2349,19 +2744,25 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
                                                             mf.as<T>(), bc.as<T>(), (int64_t)n, yp.as<T>(), ff,
                                                             tix, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
+            blk_watchdog(s, "blk_trsv forward", nullptr, (long long)(nb64 * k), (long long)grid);
             blk_trsv<T, false><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), h.as<T>(),
                                                              mb.as<T>(), yp.as<T>(), (int64_t)NP, xp.as<T>(), fb,
                                                              tix + 1, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
+            blk_watchdog(s, "blk_trsv backward", nullptr, (long long)(nb64 * k), (long long)grid);
             int hst = 0;
+            g_blk_phase = "trsv sync";
             BSM_HIP_TRY(read_dev(&hst, st, sizeof(int), s));
             BSM_HIP_TRY(hipStreamSynchronize(s));
             BSM_REQUIRE(!(hst & ST_TIMEOUT), BSM_ERR_HIP, "blocked solve: block hand-off timed out");
             BSM_HIP_TRY(hipMemcpy2DAsync(xc.p, n * sizeof(T), xp.p, NP * sizeof(T), n * sizeof(T), k,
                                          hipMemcpyDeviceToDevice, s));
         }
+        g_blk_phase = "unpack + final sync";
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
+        g_blk_phase = "idle";
+        blk_watch_stop();
         return BSM_OK;
     };
     if (a->dtype == BSM_F64) return run.template operator()<double>();

@@ -14,7 +14,7 @@ from golden.golden_io import matrix, scalars
 
 pytestmark = pytest.mark.gpu
 
-TOL = {np.float64: 1e-10, np.float32: 2e-4}
+TOL = {np.float64: 1e-10, np.float32: 2e-3}
 
 
 def rel_err(x, ref):
@@ -57,8 +57,13 @@ def test_blocked_poisson_vs_oracle(orc, dtype, g, k):
     b = orc.gen_x_cols(1004, n, k, dtype=dtype)
     ex = orc.solve(n, rp, ci, v, b, band=True)
     x = solve(A, Dense.from_columns(b), order="blocked")
-    for j in range(k):
-        assert rel_err(x.get_col(j), ex[j]) < TOL[dtype], j
+    if dtype == np.float64:
+        for j in range(k):
+            assert rel_err(x.get_col(j), ex[j]) < TOL[dtype], j
+    else:  # f32: error ~ cond(A) * 6e-8 (cond <= ~1e4 here) against the f64 solution
+        x64 = orc.solve(n, rp, ci, v.astype(np.float64), [c.astype(np.float64) for c in b], band=True)
+        for j in range(k):
+            assert rel_err(x.get_col(j), x64[j]) < 2e-3, j
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
@@ -103,8 +108,10 @@ def test_blocked_random_spd_vs_oracle(orc):
         assert rel_err(x.get_col(j), ex[j]) < 1e-12
 
 
-def test_blocked_poisson_250_f64_vs_reference_order(orc):
+@pytest.mark.parametrize("blk_chol", ["1", "0"])  # blocked factor / reference-order band_chol4 (A/B)
+def test_blocked_poisson_250_f64_vs_reference_order(orc, monkeypatch, blk_chol):
     """62,500 unknowns, bandwidth 250: blocked vs reference order on the GPU."""
+    monkeypatch.setenv("BSM_BLK_CHOL", blk_chol)
     g = 250
     n = g * g
     rp, ci, v = orc.poisson2d(g)
