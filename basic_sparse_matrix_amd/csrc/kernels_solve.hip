@@ -1981,7 +1981,7 @@ __device__ __forceinline__ void blk_diag_inverse4(const lds_t<T>* P, lds_t<T>* Q
         s = s + dpp_quad<0x4e>(s);  // quad_perm [2,3,0,1]
         const T xr = ((r == c ? (T)1 : (T)0) - s) * rd[r];
         xs[r / 4] = j == (r & 3) ? xr : xs[r / 4];
-        asm volatile("" ::: "memory");
+        if ((r & 3) == 3) asm volatile("" ::: "memory");  // loads of up to 4 rows ahead
     }
 #pragma unroll
     for (int m = 0; m < 16; ++m) Q[c * 64 + 4 * m + j] = xs[m];
@@ -2039,10 +2039,14 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
         if (t >= nb64 * DM) break;
         const int64_t K = t / DM, d = t % DM, I = K + d;
         int* fl = flags + K * DM;
-        if (I >= nb64 || 64 * d - 63 > b) {  // no such tile (past the matrix or the band)
+        // no such tile (past the matrix or the band), or the sub-diagonal tile
+        // (K + 1, K), which diagonal tile K + 1's workgroup forms (one hand-off
+        // on the chain per block column instead of two)
+        if (I >= nb64 || 64 * d - 63 > b || d == 1) {
             __syncthreads();
             continue;
         }
+        const bool sub = d == 0 && K > 0 && DM > 1;  // this workgroup also forms tile (K, K - 1)
         T acc[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -2054,22 +2058,95 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 if (d == 0 && r == c && 64 * I + r >= n) a = (T)1;
                 acc[i][j] = a;
             }
+        T acc2[4][4];  // sub: tile (K, K - 1) = A_{K,K-1} - sum_{J < K-1} L_{K,J} L_{K-1,J}^T
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 4 * tr + i, c = 4 * tc + j;
+                acc2[i][j] = sub && in_band(K, K - 1, r, c) ? CB[band_idx(K, K - 1, r, c)] : (T)0;
+            }
         // left-looking updates from block columns J in the band of both I and K
+        // (with sub, J = K - 1 comes after tile (K, K - 1) is formed, below)
         const int64_t Jlo = I - (DM - 1) > 0 ? I - (DM - 1) : 0;
-        for (int64_t J = Jlo; J < K; ++J) {
+        for (int64_t J = Jlo; J < (sub ? K - 1 : K); ++J) {
             wait_flag(&flags[J * DM + (I - J)]);
             if (d > 0) wait_flag(&flags[J * DM + (K - J)]);
+            if (sub) wait_flag(&flags[J * DM + (K - 1 - J)]);
             stage(PT, I, J);
             if (d > 0) stage(QT, K, J);
+            if (sub) stage(QT, K - 1, J);
             __syncthreads();
             T (*Q)[64] = d > 0 ? QT : PT;
+#pragma unroll 4
+            for (int s = 0; s < 64; ++s) {
+                T pa[4], qb[4], q2[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    pa[i] = PT[s][4 * tr + i];
+                    qb[i] = Q[s][4 * tc + i];
+                    q2[i] = QT[s][4 * tc + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        acc[i][j] = fma_t(-pa[i], qb[j], acc[i][j]);
+                        if (sub) acc2[i][j] = fma_t(-pa[i], q2[j], acc2[i][j]);
+                    }
+            }
+            __syncthreads();
+        }
+        if (sub) {
+            // L_{K,K-1} = S_{K,K-1} L_{K-1,K-1}^-T once diagonal tile K - 1 is done
+            wait_flag(&flags[(K - 1) * DM]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = acc2[i][j];
+            for (int e = tid; e < 4096; e += 256) QT[e >> 6][e & 63] = ld_sc1(&Dinv[(K - 1) * 4096 + e]);
+            __syncthreads();
+            T o[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[i][j] = (T)0;
 #pragma unroll 4
             for (int s = 0; s < 64; ++s) {
                 T pa[4], qb[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     pa[i] = PT[s][4 * tr + i];
-                    qb[i] = Q[s][4 * tc + i];
+                    qb[i] = QT[s][4 * tc + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) o[i][j] = fma_t(pa[i], qb[j], o[i][j]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = 4 * tr + i, c = 4 * tc + j;
+                    if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[i][j]);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t]
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = o[i][j];
+            __syncthreads();
+#pragma unroll 4
+            for (int s = 0; s < 64; ++s) {
+                T pa[4], qb[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    pa[i] = PT[s][4 * tr + i];
+                    qb[i] = PT[s][4 * tc + i];
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
