@@ -639,6 +639,16 @@ Dense<T> solve(Csr<T> a, Dense<T> b) {
     return detail::run_solver<T>(bsm_solve, a, b);
 }
 
+/// solve with the sums reassociated (bsm_solve_blocked; this build's
+/// addition): within the f64 tolerance, not bit-exact; same errors/panics.
+template <class T>
+    requires std::is_floating_point_v<T>
+Dense<T> solve_blocked(Csr<T> a, Dense<T> b) {
+    if (a.get_dims().rows != a.get_dims().cols)
+        throw Panic("called `Result::unwrap()` on an `Err` value: NonSquareMatrix");
+    return detail::run_solver<T>(bsm_solve_blocked, a, b);
+}
+
 }  // namespace bsm
 
 #endif  // BSM_HPP

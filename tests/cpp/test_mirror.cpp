@@ -314,6 +314,15 @@ GPU_TEST(solve_poisson_f64_vs_band_oracle) {
     CHECK(orc_solve_f64(n, rp.data(), ci.data(), v.data(), 1, b.data(), n, ex.data(), n, 1) == ORC_OK);
     std::vector<double> got(x.get_col(0).begin(), x.get_col(0).end());
     CHECK(same_bits(got, ex));
+    // the reassociated solve: within the f64 tolerance of the reference order
+    auto xb = bsm::solve_blocked(a, Dense<double>::from_data({b}));
+    double num = 0, den = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const double e = xb.get_col(0)[i] - ex[i];
+        num += e * e;
+        den += ex[i] * ex[i];
+    }
+    CHECK(std::sqrt(num / den) < 1e-10);
 }
 
 int main(int argc, char** argv) {
