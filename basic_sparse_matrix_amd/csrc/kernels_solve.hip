@@ -1990,6 +1990,78 @@ __device__ __forceinline__ void blk_diag_inverse4(const lds_t<T>* P, lds_t<T>* Q
     for (int m = 0; m < 16; ++m) Q[c * TLD + 4 * m + j] = xs[m];
 }
 
+// Linv of the tile's L (P, lower part) from the inverses Di[p] of its four
+// 16 x 16 diagonal blocks: diagonal blocks Di, zeros above, then the blocks
+// below by distance: Linv[p2][p1] = -Di[p2] sum_q L[p2][q] Linv[q][p1].
+// Q[c * TLD + r] = Linv[r][c]. All threads; barriers inside.
+template <typename T>
+__device__ __forceinline__ void blk_linv_from_blocks(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di,
+                                                     lds_t<T>* Tb, int tid) {
+    for (int e = tid; e < 4096; e += 256) {
+        const int c = e >> 6, r = e & 63, pr = r >> 4, pc = c >> 4;
+        Q[c * TLD + r] = pr == pc ? Di[pr * 256 + (r & 15) * 16 + (c & 15)] : (T)0;
+    }
+    __syncthreads();
+    for (int dd = 1; dd < 4; ++dd) {
+        // Tb[blk][rr][cc] = sum_q L[16 p2 + rr][q] Linv[q][16 p1 + cc], q in [16 p1, 16 p2)
+        for (int e = tid; e < (4 - dd) * 256; e += 256) {
+            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
+            T s = (T)0;
+            for (int qb = p1; qb < p2; ++qb) {  // 16 terms at a time: their loads in flight together
+                T s2 = (T)0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    s2 = fma_t(P[(16 * p2 + rr) * TLD + 16 * qb + t], Q[(16 * p1 + cc) * TLD + 16 * qb + t], s2);
+                s += s2;
+            }
+            Tb[e] = s;
+        }
+        __syncthreads();
+        for (int e = tid; e < (4 - dd) * 256; e += 256) {
+            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
+            T s = (T)0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) s = fma_t(Di[p2 * 256 + rr * 16 + t], Tb[p1 * 256 + t * 16 + cc], s);
+            Q[(16 * p1 + cc) * TLD + 16 * p2 + rr] = -s;
+        }
+        __syncthreads();
+    }
+}
+
+// Linv of the tile's L (P, lower part) on all four waves: wave 0's four DPP
+// rows invert the four 16 x 16 diagonal blocks at once (lane 16k + r: row r
+// of block k, L[q2][q] by row broadcast), then blk_linv_from_blocks.
+template <typename T>
+__device__ __forceinline__ void blk_diag_inverse_blocked(const lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di,
+                                                         lds_t<T>* Tb, int tid) {
+    asm volatile("" : "+v"(tid));  // opaque: keep the per-row masks out of the ticket loop
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+        const int k = (tid >> 4) & 3, r = tid & 15;
+        T dv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dv[q] = P[(16 * k + r) * TLD + 16 * k + q];
+        T rown = (T)0;  // this row's diagonal element L[r][r]
+#pragma unroll
+        for (int q = 0; q < 16; ++q) rown = q == r ? dv[q] : rown;
+        const T rinv = (T)1 / rown;
+        T x[16];
+        auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
+            T sacc = (T)0;
+            [&]<int... qs>(std::integer_sequence<int, qs...>) __attribute__((always_inline)) {
+                ((sacc = fma_t(rowbcast<q2>(dv[qs]), x[qs], sacc)), ...);
+            }(std::make_integer_sequence<int, q2>{});
+            x[q2] = ((q2 == r ? (T)1 : (T)0) - sacc) * rowbcast<q2>(rinv);
+        };
+        [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+            (irow(std::integral_constant<int, ts>{}), ...);
+        }(std::make_integer_sequence<int, 16>{});
+#pragma unroll
+        for (int q2 = 0; q2 < 16; ++q2) Di[k * 256 + q2 * 16 + r] = x[q2];  // Di[k][row][col]
+    }
+    __syncthreads();
+    blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
+}
+
 // Factor AND invert the 64 x 64 tile S (P[r * TLD + c], lower part) on all
 // four waves, by 16-column panels p (columns c0 = 16p ...):
 //   1. wave 0 factors the 16 x 16 diagonal block (lane r & 15 = row, pivots
@@ -2097,30 +2169,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
         __syncthreads();
     }
     if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
-    // Linv: diagonal blocks Di, zeros above, then the blocks below by distance
-    for (int e = tid; e < 4096; e += 256) {
-        const int c = e >> 6, r = e & 63, pr = r >> 4, pc = c >> 4;
-        Q[c * TLD + r] = pr == pc ? Di[pr * 256 + (r & 15) * 16 + (c & 15)] : (T)0;
-    }
-    __syncthreads();
-    for (int dd = 1; dd < 4; ++dd) {
-        // Tb[blk][rr][cc] = sum_q L[16 p2 + rr][q] Linv[q][16 p1 + cc], q in [16 p1, 16 p2)
-        for (int e = tid; e < (4 - dd) * 256; e += 256) {
-            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
-            T s = (T)0;
-            for (int q = 16 * p1; q < 16 * p2; ++q) s = fma_t(P[(16 * p2 + rr) * TLD + q], Q[(16 * p1 + cc) * TLD + q], s);
-            Tb[e] = s;
-        }
-        __syncthreads();
-        for (int e = tid; e < (4 - dd) * 256; e += 256) {
-            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
-            T s = (T)0;
-#pragma unroll
-            for (int t = 0; t < 16; ++t) s = fma_t(Di[p2 * 256 + rr * 16 + t], Tb[p1 * 256 + t * 16 + cc], s);
-            Q[(16 * p1 + cc) * TLD + 16 * p2 + rr] = -s;
-        }
-        __syncthreads();
-    }
+    blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
 }
 
 template <typename T>
@@ -2315,7 +2364,9 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 const int r = e & 63, c = e >> 6;
                 if (r >= c && in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], PT[r][c]);
             }
-            if (!panels) blk_diag_inverse4<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, tid);
+            if (!panels)
+                blk_diag_inverse_blocked<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
+                                            tid);
             __syncthreads();
             if (dbg && tid == 0) {  // cycles: factor, inverse (BSM_BLK_DEBUG)
                 const long long c2 = clock64();
