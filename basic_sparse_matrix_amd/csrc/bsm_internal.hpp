@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/bsm.h"
@@ -159,7 +160,9 @@ struct bsm_csr {
     bool analysed = false;
     bool rows_sorted = true;  // col non-decreasing inside every row
     uint64_t max_row_len = 0;
-    // cached column-panel plan of mul_dense (spmm_plan), keyed by panel width
+    // cached column-panel plan of mul_dense (spmm_plan), keyed by panel width;
+    // plan_mu serialises its (re)build and use across threads sharing the handle
+    mutable std::mutex plan_mu;
     mutable int32_t* plan_seg = nullptr;
     mutable uint64_t plan_cols = 0;
     mutable bool plan_usable = false;

@@ -101,7 +101,17 @@ BSM_HD double bsm_a_value(uint64_t seed, uint64_t row, uint64_t j, int kind) {
     return bsm_val_from_hash(bsm_hash(seed, row, j, BSM_SALT_VAL), kind);
 }
 
-/* Row length for the CONST / UNIFORM families (BINOMIAL is host-only). */
+/* Row length of the BINOMIAL family: the number of columns j < n_cols whose
+ * hash falls below p * 2^32 (p = a / 2^32), i.e. Binomial(n_cols, p); O(n_cols)
+ * per row, meant for small matrices (C1: 1024 x 1024, p = 0.01). */
+BSM_HD uint32_t bsm_rowlen_binomial(uint64_t seed, uint64_t row, uint32_t n_cols, uint32_t a) {
+    uint32_t len = 0;
+    for (uint32_t j = 0; j < n_cols; ++j)
+        if ((bsm_hash(seed, row, j, BSM_SALT_ROWLEN) >> 32) < (uint64_t)a) ++len;
+    return len;
+}
+
+/* Row length for the CONST / UNIFORM families (BINOMIAL: bsm_rowlen_binomial). */
 BSM_HD uint32_t bsm_rowlen(uint64_t seed, uint64_t row, int kind, uint32_t a, uint32_t b) {
     if (kind == BSM_ROWLEN_UNIFORM) {
         uint64_t h = bsm_hash(seed, row, 0, BSM_SALT_ROWLEN);

@@ -201,6 +201,9 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
         BSM_HIP_TRY(hipMemsetAsync(row_nnz.p, 0, rows * sizeof(int32_t), s));
     } else {
         const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
+        // one thread at a time builds and launches with the cached plan (a
+        // rebuild frees the old plan; hipFree waits for launches using it)
+        std::lock_guard<std::mutex> plan_lock(a->plan_mu);
         if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
             if (a->plan_seg) (void)hipFree(a->plan_seg);
             a->plan_seg = nullptr;

@@ -43,7 +43,18 @@ constexpr int TR = 16;              // rows per tile-row
 constexpr int CH_THREADS = 1024;    // 16 rows x 64 column lanes
 constexpr long long SPIN_LIMIT = 1ll << 25;
 
-enum { ST_NOT_PD = 1, ST_TIMEOUT = 2, ST_EMPTY_ROW = 4 };
+enum { ST_NOT_PD = 1, ST_TIMEOUT = 2, ST_EMPTY_ROW = 4, ST_COL_OOB = 8 };
+
+// Row-block tickets for the persistent Cholesky grids, handed out in
+// ascending order: a workgroup only ever waits on LOWER row-blocks, which
+// workgroups already running hold, so progress needs no co-residency of the
+// grid (a CU held by another kernel or stream only slows the factor down).
+__device__ __forceinline__ int64_t next_ticket(int* ticket, int* s_tk) {
+    __syncthreads();  // every thread has read the previous ticket
+    if (threadIdx.x == 0) *s_tk = atomicAdd(ticket, 1);
+    __syncthreads();
+    return *s_tk;
+}
 
 // ---- write-through (sc1) loads/stores of T via same-width integers --------
 template <typename T> struct Bits;
@@ -233,7 +244,8 @@ constexpr int TRACE_TILES = 4096;  // diagnostic trace (BSM_CHOL_TRACE=1): first
 template <typename T, int M>
 __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                          int* __restrict__ progress, int* __restrict__ status,
-                                                         int64_t n_tiles, unsigned long long* __restrict__ trace) {
+                                                         int* __restrict__ ticket, int64_t n_tiles,
+                                                         unsigned long long* __restrict__ trace) {
     using A = Arith<T>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* colL = reinterpret_cast<T*>(smem_raw);  // [b + 1]: L[k + d][k] of column k
@@ -245,7 +257,8 @@ __global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, in
     const int r = tid >> 6, c = tid & 63;
     const int pf = tid;  // prefetch lane
     constexpr int PFN = CH_THREADS;
-    for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
+    __shared__ int s_tk;
+    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
         const int64_t i0 = I * TR;
         const int64_t i = i0 + r;  // this thread's row
         const int64_t jb = i0 - b > 0 ? i0 - b : 0;
@@ -446,8 +459,8 @@ constexpr int C3S = 4;  // columns per staging batch (one barrier per batch)
 template <typename T, int M, int RW>
 __global__ __launch_bounds__(1024 / RW) void band_chol3(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                          T* __restrict__ R, int* __restrict__ progress,
-                                                         int* __restrict__ status, int64_t n_tiles,
-                                                         unsigned long long* __restrict__ trace) {
+                                                         int* __restrict__ status, int* __restrict__ ticket,
+                                                         int64_t n_tiles, unsigned long long* __restrict__ trace) {
     using A = Arith<T>;
     constexpr int NT = 1024 / RW;           // threads
     constexpr int SPAN = 64 * M;            // staged d = 1 .. SPAN of each column
@@ -467,7 +480,8 @@ __global__ __launch_bounds__(1024 / RW) void band_chol3(int64_t n, int64_t b, in
         const int e = tid + NT * q;
         off[q] = e < C3S * SPAN ? (e / SPAN) * (int)ld + e % SPAN + 1 : 0;
     }
-    for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
+    __shared__ int s_tk;
+    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
         const int i0 = (int)(I * TR);
         const int jb = i0 - (int)b > 0 ? i0 - (int)b : 0;
         const int nb = (i0 - jb + C3S - 1) / C3S;  // batches of the sweep
@@ -721,8 +735,8 @@ __global__ __launch_bounds__(256) void band_chol4_init(int64_t n_tiles, int64_t 
 template <typename T, int M>
 __global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                     T* __restrict__ R, int* __restrict__ fprog,
-                                                    int* __restrict__ status, int64_t n_tiles,
-                                                    unsigned long long* __restrict__ trace) {
+                                                    int* __restrict__ status, int* __restrict__ ticket,
+                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
     using A = Arith<T>;
     constexpr int CS = 64 + 64 * M;  // [64 zero pad][column tile K of rows k0+16 ...]
     __shared__ T colK[C4_TB][CS];
@@ -752,7 +766,8 @@ __global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_
             }
         }
     };
-    for (int64_t I = blockIdx.x; I < n_tiles; I += gridDim.x) {
+    __shared__ int s_tk;
+    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
         const int i0 = (int)(I * C4_TB);
         const int K0 = (i0 - ib > 0 ? i0 - ib : 0) / C4_TB, jb = C4_TB * K0;
         const bool live = i0 + w < n;
@@ -1647,6 +1662,24 @@ __global__ __launch_bounds__(64) void csr_backward(int64_t n, const int64_t* __r
     }
 }
 
+// The tri-solves index the n-row y / x with the column of every entry of
+// rows [0, n) they read: forward all of them (col != row, lib.rs:37-38),
+// backward all but the first (row.iter().skip(1), lib.rs:57-58). A column
+// >= n there is an index-out-of-bounds panic in the reference. One thread
+// per row (only launched when the matrix is wider than the RHS).
+__global__ __launch_bounds__(256) void csr_cols_past_rhs(int64_t n, const int64_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ col, bool skip_first,
+                                                         int* __restrict__ status) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t a = rp[i] + (skip_first ? 1 : 0), e1 = rp[i + 1];
+    for (int64_t e = a; e < e1; ++e)
+        if (col[e] >= n) {
+            atomicOr(status, ST_COL_OOB);
+            return;
+        }
+}
+
 // ---------------------------------------------------------------------------
 // Blocked band solves (bsm_solve_blocked): the same L L^T x = b as solve
 // (lib.rs:11-24), with the sums REASSOCIATED. Not bit-exact with the
@@ -2461,12 +2494,11 @@ int launch_chol(Band& bd, int* progress, int* status, hipStream_t s, unsigned lo
     int per_cu = 0;
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol<T, M>, CH_THREADS, shm));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol does not fit a CU");
-    // every workgroup must be resident (tile-row I waits on tile-row I-1)
-    int64_t grid = cus;
+    int64_t grid = cus;  // one per CU; tickets keep it correct when fewer are resident
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol<T, M><<<(unsigned)grid, CH_THREADS, shm, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), progress, status,
-                                                             n_tiles, trace);
+                                                             status + 1, n_tiles, trace);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -2480,11 +2512,11 @@ int launch_chol3(Band& bd, int* progress, int* status, hipStream_t s, unsigned l
     int per_cu = 0;
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol3<T, M, RW>, 1024 / RW, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol3 does not fit a CU");
-    int64_t grid = cus;  // every workgroup resident: tile-row I waits on tile-row I-1
+    int64_t grid = cus;  // one per CU; tickets keep it correct when fewer are resident
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol3<T, M, RW><<<(unsigned)grid, 1024 / RW, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), progress,
-                                                            status, n_tiles, trace);
+                                                            status, status + 1, n_tiles, trace);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -2500,11 +2532,11 @@ int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol4 does not fit a CU");
     band_chol4_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
     BSM_HIP_TRY(hipGetLastError());
-    int64_t grid = (int64_t)cus * per_cu;  // every workgroup resident: row-blocks wait on lower ones only
+    int64_t grid = (int64_t)cus * per_cu;  // all resident when the chip is free; tickets keep order otherwise
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol4<T, M><<<(unsigned)grid, C4_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
-                                                     n_tiles, trace);
+                                                     status + 1, n_tiles, trace);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -2810,6 +2842,15 @@ int solve_dispatch_trsv(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, co
         BSM_HIP_TRY(hipMemsetAsync(xc.p, 0, n * k * sizeof(T), s));  // Dense::new_default_with_dims
         BSM_TRY(st.alloc(16));
         BSM_HIP_TRY(hipMemsetAsync(st.p, 0, 16, s));
+        if (n && k && m->cols > n) {  // columns past the RHS rows: the reference panics on them
+            csr_cols_past_rhs<<<nblk(n, 256), 256, 0, s>>>((int64_t)n, m->row_ptr, m->col, !lower, st.as<int>());
+            BSM_HIP_TRY(hipGetLastError());
+            int h = 0;
+            BSM_HIP_TRY(read_dev(&h, st.p, sizeof(int), s));
+            BSM_REQUIRE(!(h & ST_COL_OOB), BSM_ERR_PANIC,
+                        "index out of bounds: a column index >= the %llu rows of the right-hand side "
+                        "(lib.rs:38 / :58)", (unsigned long long)n);
+        }
         if (n && k) {
             if (lower)
                 csr_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, m->row_ptr, m->col,

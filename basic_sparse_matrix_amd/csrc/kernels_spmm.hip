@@ -507,6 +507,66 @@ __global__ __launch_bounds__(256) void spmv_stream(int64_t rows, int64_t nnz,
 }
 
 // ---------------------------------------------------------------------------
+// SpMV (k = 1), rows-blocked: workgroup b owns rows [256b, 256b + 256), one
+// per thread. Its entry range [rp[r0], rp[r1]) is swept in chunks of
+// 256 * ITEMS entries: coalesced col/val loads and the x gathers of a chunk
+// are all in flight together, the products land in LDS, and each thread then
+// adds the part of its row that lies in the chunk, in storage order, onto its
+// running sum (chunks ascend, so the per-row order is the reference's,
+// sparse.rs:434-440). No search: the row bounds are direct loads, so a
+// workgroup is three dependent memory round trips (row bounds -> entries ->
+// x) instead of spmv_stream's binary search in front of them. A long row is
+// summed by its one thread across chunks (order kept, slower); rows this
+// long on average go to spmv_stream instead.
+// ---------------------------------------------------------------------------
+template <typename T, int ITEMS>
+__global__ __launch_bounds__(256) void spmv_rows(int64_t rows, const int64_t* __restrict__ rp,
+                                                 const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                 const T* __restrict__ x, T* __restrict__ y,
+                                                 int32_t* __restrict__ row_nnz, bool neg_init) {
+    using A = Arith<T>;
+    constexpr int CAP = 256 * ITEMS;
+    __shared__ T prod[CAP];
+    const int tid = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * 256;
+    const int64_t r1 = r0 + 256 < rows ? r0 + 256 : rows;
+    const int64_t rr = r0 + tid;
+    const bool live = rr < r1;
+    // the workgroup's entry range and this thread's row, loaded together
+    const int64_t e0 = rp[r0], e1 = rp[r1];
+    const int64_t ra = live ? rp[rr] : e1, rb = live ? rp[rr + 1] : e1;
+    T acc = neg_init ? A::neg_zero() : A::zero();
+    for (int64_t base = e0; base < e1; base += CAP) {
+        const int64_t n = e1 - base < CAP ? e1 - base : CAP;
+        const int nit = (int)((n + 255) / 256);  // uniform over the workgroup
+        int32_t c[ITEMS];
+        T v[ITEMS];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit) {
+                const int64_t e = base + min<int64_t>(it * 256 + tid, n - 1);
+                c[it] = col[e];
+                v[it] = val[e];
+            }
+        T xv[ITEMS];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit) xv[it] = x[c[it]];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit && it * 256 + tid < n) prod[it * 256 + tid] = A::mul(v[it], xv[it]);
+        __syncthreads();
+        const int64_t a = ra > base ? ra : base, b = rb < base + n ? rb : base + n;
+        for (int64_t i = a; i < b; ++i) acc = A::add(acc, prod[i - base]);
+        __syncthreads();
+    }
+    if (live) {
+        y[rr] = acc;
+        if (row_nnz) row_nnz[rr] = A::nz(acc) ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Compaction of dense Y (rows x k, row-major) into the output Csr: entry
 // (r, j) is kept iff Y[r][j] != 0 (insert's zero skip, sparse.rs:229), in
 // ascending j, at out_rp[r] + (kept entries of row r before j).
@@ -636,7 +696,8 @@ __global__ __launch_bounds__(256) void gen_rowlen(uint64_t seed, uint64_t row0, 
                                                   int32_t* len) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
-    uint32_t l = bsm_rowlen(seed, row0 + r, kind, a, b);
+    uint32_t l = kind == BSM_ROWLEN_BINOMIAL ? bsm_rowlen_binomial(seed, row0 + r, n_cols, a)
+                                             : bsm_rowlen(seed, row0 + r, kind, a, b);
     if (l > n_cols) l = n_cols;
     len[r] = (int32_t)l;
 }
@@ -738,6 +799,7 @@ int spmv_items() {
     return (v == 2 || v == 8) ? v : 4;
 }
 constexpr uint64_t SHORT_ROW_AVG = 24;  // nnz/rows at or below: four rows per wave
+constexpr uint64_t SPMV_ROWS_AVG = 12;  // k = 1, nnz/rows at or below: spmv_rows (one chunk per workgroup)
 int spmm_variant() {
     const char* e = getenv("BSM_SPMM_VARIANT");
     return e ? atoi(e) : 0;
@@ -748,6 +810,16 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
                 const T* vals, uint64_t k, const T* x, T* y, int32_t* row_nnz, bool neg_init,
                 hipStream_t s) {
     if (rows == 0) return BSM_OK;
+    // short rows on average (C2: 10): the rows-blocked SpMV; BSM_SPMV_VARIANT=1
+    // forces the nnz-balanced spmv_stream (A/B)
+    const char* sv = getenv("BSM_SPMV_VARIANT");
+    if (k == 1 && nnz <= SPMV_ROWS_AVG * rows && !(sv && atoi(sv) == 1)) {
+        const uint64_t blocks = (rows + 255) / 256;
+        BSM_REQUIRE(blocks < (1ull << 31), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
+        spmv_rows<T, 16><<<(unsigned)blocks, 256, 0, s>>>((int64_t)rows, rp, col, vals, x, y, row_nnz, neg_init);
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    }
     if (k == 1) {
         const int items = spmv_items();
         const uint64_t blocks = nnz / (256ull * items) + 1;
@@ -1067,9 +1139,12 @@ int analyse_dispatch(const int64_t* rp, const int32_t* col, uint64_t rows, uint6
 
 int gen_row_ptr(uint64_t seed, uint64_t row0, uint64_t rows, uint32_t n_cols, int kind, uint32_t a,
                 uint32_t b, int64_t* rp, void* ws, uint64_t ws_bytes, hipStream_t s) {
-    BSM_REQUIRE(kind == BSM_ROWLEN_CONST || kind == BSM_ROWLEN_UNIFORM, BSM_ERR_UNSUPPORTED,
-                "device generator supports CONST/UNIFORM row lengths only");
-    BSM_REQUIRE(b <= GEN_MAX && a <= GEN_MAX, BSM_ERR_UNSUPPORTED, "row length > %d", GEN_MAX);
+    BSM_REQUIRE(kind == BSM_ROWLEN_CONST || kind == BSM_ROWLEN_UNIFORM ||
+                    (kind == BSM_ROWLEN_BINOMIAL && n_cols <= GEN_MAX),
+                BSM_ERR_UNSUPPORTED, "device generator: CONST/UNIFORM row lengths, or BINOMIAL up to %d columns",
+                GEN_MAX);
+    BSM_REQUIRE(kind == BSM_ROWLEN_BINOMIAL || (b <= GEN_MAX && a <= GEN_MAX), BSM_ERR_UNSUPPORTED,
+                "row length > %d", GEN_MAX);
     // workspace: [len int32 rows][scan ws]
     const uint64_t len_bytes = ((rows * sizeof(int32_t)) + 255) / 256 * 256;
     BSM_REQUIRE(ws && ws_bytes >= len_bytes + scan_workspace_bytes(rows), BSM_ERR_INVALID,

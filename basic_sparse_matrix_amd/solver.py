@@ -28,9 +28,14 @@ def _run(fn_name: str, m: Csr, rhs: Dense) -> Dense:
     n, k = dims.rows, dims.cols
     if m.dims.rows < n:
         raise Panic("index out of bounds: matrix has fewer rows than the right-hand side")
+    b_cols = []
+    for j in range(k):
+        c = np.ascontiguousarray(rhs.get_col(j))
+        if c.shape[0] < n:  # b.get_col(c)[row] / y.get_col(c)[row] for every row < n (lib.rs:33, :54)
+            raise Panic(f"index out of bounds: the len is {c.shape[0]} but the index is {c.shape[0]}")
+        b_cols.append(np.ascontiguousarray(c[:n]))
     dev = m._device()
     lib = _lib.require_device()
-    b_cols = [np.ascontiguousarray(rhs.get_col(j)) for j in range(k)]
     out = Dense.new_default_with_dims(k, n, dtype=m.dtype)
     _raise_for(getattr(lib, fn_name)(dev.handle, k, n, _lib.ptr_array(b_cols), _lib.ptr_array(out.data)))
     return out

@@ -412,7 +412,17 @@ class Csr(GetDims):
                 raise TypeError(f"mul_dense: Csr<{self.dtype}> x Dense<{c.dtype}>")
         dev = self._device()
         lib = _lib.require_device()
-        arrs = [np.ascontiguousarray(c) for c in cols]
+        arrs = []
+        for c in cols:
+            a = np.ascontiguousarray(c)
+            if a.shape[0] < x_rows:
+                # rhs.get_col(col)[e.col_index] (sparse.rs:437): a short column panics
+                # only when an entry reaches past its end; the rest is never read
+                ci = self._csr_arrays()[1]
+                if ci.size and int(ci.max()) >= a.shape[0]:
+                    raise Panic(f"index out of bounds: the len is {a.shape[0]} but the index is {int(ci.max())}")
+                a = np.concatenate([a, np.zeros(x_rows - a.shape[0], dtype=a.dtype)])
+            arrs.append(np.ascontiguousarray(a[:x_rows]))
         out = ctypes.c_void_p()
         _raise_for(lib.bsm_csr_mul_dense(dev.handle, len(arrs), x_rows, _lib.ptr_array(arrs), ctypes.byref(out)))
         return Csr._from_device(_lib.DeviceCsr(out.value))

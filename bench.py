@@ -39,12 +39,15 @@ import torch  # noqa: E402  (imported before the HIP library: one runtime)
 import torch.distributed as dist  # noqa: E402
 
 CONFIGS = {
-    # name: (rows, n_cols, nnz_per_row, k)
+    # name: (rows, n_cols, nnz_per_row, k); BASELINE.json configs[0..3]
     "c4": (10_000_000, 10_000_000, 1000, 32),
     "c3": (1_000_000, 1_000_000, 10, 32),
     "c2": (1_000_000, 1_000_000, 10, 1),
+    "c1": (1024, 1024, None, 1),  # row lengths ~ Binomial(1024, 0.01): ~10.5k nnz (host generator)
 }
+C1_P = 0.01
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ROWLEN_CONST, ROWLEN_BINOMIAL = 0, 2  # bsm_synth.h row-length families
 SEED_A, SEED_X = 1000, 1001
 
 
@@ -52,37 +55,131 @@ def b_alg(rows, n_cols, nnz, k):
     return 8 * (rows + 1) + 12 * nnz + 8 * n_cols * k + 8 * rows * k
 
 
+def b_gather(rows, nnz, k):
+    """SURVEY.md §8d traffic model: every nnz gathers its whole X row (no reuse
+    beyond the caches): 8(N+1) + 12 nnz + 8 nnz k + 8 N k."""
+    return 8 * (rows + 1) + 12 * nnz + 8 * nnz * k + 8 * rows * k
+
+
+def kernel_label(rows, nnz, k, panel_cols):
+    """The kernel launch_spmm (kernels_spmm.hip) picks for this shape."""
+    if k == 1:
+        return "spmv_rows<double,16>" if nnz <= 12 * rows else "spmv_stream<double,4>"
+    if k == 32:
+        if nnz <= 24 * rows and not panel_cols:
+            return "spmm_k32_f64_rows4<4>"
+        return f"spmm_k32_f64<4,true,{'true' if panel_cols else 'false'}>"
+    return "spmm_rowwave<double>"
+
+
+def end_to_end(cfg_name, blks, x, comp, step, rows, k, iters=3):
+    """End-to-end figures next to the device-resident step:
+    device_ms = H2D of X from pinned host memory + the step + D2H of the
+    output Csr (row_ptr, col, vals) into pinned host memory, A resident (as the
+    host mirror caches it); public_api_ms (host-sized configs only) =
+    Csr.mul_dense(Dense) through the public API, host Dense in, host Csr out
+    (the library's own X upload/packing and int32 -> usize column widening)."""
+    out = {}
+    n_out = comp.nnz()
+    xh = x.cpu().pin_memory()
+    rp_h = torch.empty(rows + 1, dtype=torch.int64).pin_memory()
+    col_h = torch.empty(max(1, n_out), dtype=torch.int32).pin_memory()
+    val_h = torch.empty(max(1, n_out), dtype=torch.float64).pin_memory()
+    ts = []
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        x.copy_(xh, non_blocking=True)
+        step(False)
+        rp_h.copy_(comp.row_ptr, non_blocking=True)
+        col_h[:n_out].copy_(comp.col[:n_out], non_blocking=True)
+        val_h[:n_out].copy_(comp.vals[:n_out], non_blocking=True)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    out["device_ms"] = round(float(np.median(ts)) * 1e3, 3)
+    out["h2d_bytes"] = int(xh.numel() * 8)
+    out["d2h_bytes"] = int((rows + 1) * 8 + n_out * 12)
+    if len(blks) == 1 and blks[0].nnz <= 200_000_000:
+        from basic_sparse_matrix_amd import Csr, Dense
+
+        b = blks[0]
+        a = Csr.from_csr_arrays((b.rows, b.n_cols), b.row_ptr.cpu().numpy().astype(np.uint64),
+                                b.col.cpu().numpy().astype(np.uint64), b.vals.cpu().numpy())
+        xd = Dense.from_columns([np.ascontiguousarray(xh[:, j].numpy()) for j in range(k)])
+        a.mul_dense(xd)  # first call uploads and caches A on the device (untimed, like the bench's setup)
+        ts = []
+        for _ in range(max(iters, 20 if cfg_name == "c1" else iters)):
+            t0 = time.perf_counter()
+            a.mul_dense(xd)
+            ts.append(time.perf_counter() - t0)
+        out["public_api_ms"] = round(float(np.median(ts)) * 1e3, 4)
+        out["public_api_calls"] = len(ts)
+    return out
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg_name, sample_rows):
-    """The oracle's restatement of Csr::mul_dense (oracle/, single thread)
-    timed on the first `sample_rows` rows of the same workload, extrapolated
-    linearly to the full row count (rows are statistically identical)."""
+def c1_rowlen_a():
+    """Binomial(1024, p) row lengths: p = a / 2^32 (bsm_synth.h bsm_rowlen_binomial)."""
+    return int(round(C1_P * 2 ** 32))
+
+
+def rowlen_spec(cfg_name):
+    """(kind, a, b) of the synthetic row-length family of a config."""
+    rows, n_cols, nnz_r, k = CONFIGS[cfg_name]
+    if nnz_r is None:
+        return ROWLEN_BINOMIAL, c1_rowlen_a(), 0
+    return ROWLEN_CONST, nnz_r, nnz_r
+
+
+def cpu_baseline(cfg_name, sample_rows, reps=20):
+    """The oracle's restatement of Csr::mul_dense (oracle/, single thread),
+    with get_row_compact's per-row Vec allocation emulated
+    (orc_set_emulate_row_alloc). A config that fits (C1-C3 row counts up to
+    `sample_rows`) is timed whole, median of `reps` calls; a bigger one (C4)
+    on its first `sample_rows` rows, extrapolated linearly to the full row
+    count (its rows are statistically identical)."""
     from oracle import pyoracle as orc
 
-    rows, n_cols, nnz_r, k = CONFIGS[cfg_name]
-    rp = np.arange(sample_rows + 1, dtype=np.uint64) * nnz_r
+    rows, n_cols, _, k = CONFIGS[cfg_name]
+    kind, a, b = rowlen_spec(cfg_name)
+    n = min(rows, sample_rows)
+    rp = orc.gen_row_ptr(SEED_A, n, n_cols, kind, a, b)
     ci, v = orc.gen_entries(SEED_A, rp, n_cols)
     t0 = time.perf_counter()
     x_cols = orc.gen_x_cols(SEED_X, n_cols, k)
     t_gen = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    orc.mul_dense(sample_rows, n_cols, rp, ci, v, x_cols)
-    t = time.perf_counter() - t0
-    t_full = t * rows / sample_rows
-    nnz = rows * nnz_r
+    orc.lib().orc_set_emulate_row_alloc(1)
+    try:
+        ts = []
+        while True:  # whole matrix: `reps` calls, fewer if they would take over ~30 s
+            t0 = time.perf_counter()
+            orc.mul_dense(n, n_cols, rp, ci, v, x_cols)
+            ts.append(time.perf_counter() - t0)
+            if n < rows or len(ts) >= reps or (len(ts) >= 3 and sum(ts) > 30.0):
+                break
+    finally:
+        orc.lib().orc_set_emulate_row_alloc(0)
+    t = float(np.median(ts))
+    t_full = t * rows / n
+    nnz_s = int(rp[n])
+    nnz = nnz_s if n == rows else nnz_s * rows // n
+    how = (f"whole matrix, median of {len(ts)} calls ({t * 1e3:.3f} ms)" if n == rows else
+           f"first {n} of {rows} rows ({nnz_s} nnz x {k} RHS) in {t:.2f} s, extrapolated x{rows // n} "
+           f"to {t_full:.1f} s per full SpMM")
     return {
         "value": round(b_alg(rows, n_cols, nnz, k) / t_full / 1e9, 4),
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"oracle mul_dense (C restatement of sparse.rs:426-446, -O2, 1 thread) on the first "
-                  f"{sample_rows} of {rows} rows ({sample_rows * nnz_r} nnz x {k} RHS) in {t:.2f} s, "
-                  f"extrapolated x{rows // sample_rows} to {t_full:.1f} s per full SpMM (X generation "
+        "sample": f"oracle mul_dense (C restatement of sparse.rs:426-446, -O2 -ffp-contract=off, 1 thread, "
+                  f"get_row_compact's per-row dims.cols x 24 B Vec allocated as in sparse.rs:254; output "
+                  f"arrays preallocated, where the reference grows Vecs) on the {how} (X generation "
                   f"{t_gen:.1f} s untimed)",
-        "nnz_per_s": round(sample_rows * nnz_r / t, 1),
+        "ms_per_spmm": round(t_full * 1e3, 4),
+        "nnz_per_s": round(nnz_s / t, 1),
         "host_cpus": os.cpu_count(),
     }
 
@@ -189,7 +286,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=5000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=100_000,
+                    help="rows of the CPU baseline sample (configs with more rows are extrapolated)")
     ap.add_argument("--panel-cols", type=int, default=None,
                     help="column-panel width of the SpMM schedule (default: the library's choice; 0 = one pass)")
     ap.add_argument("--chunks", type=int, default=0,
@@ -199,6 +297,7 @@ def main():
                     help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (H2D/D2H included) figures")
     ap.add_argument("--ref-benches", default=None,
                     help="comma list of the reference's own criterion benches to run instead "
                          "(sd_mul,ss_add,ss_mul; one JSON line per size)")
@@ -228,6 +327,7 @@ def main():
     from basic_sparse_matrix_amd.distributed import partition_rows_cyclic
 
     rows, n_cols, nnz_r, k = CONFIGS[args.config]
+    kind, ra, rb = rowlen_spec(args.config)
     # block-cyclic row partition (equal rows = equal nnz: constant row length):
     # `chunks` rounds, each finished by its own SpMM launch and all-gathered
     # asynchronously while the next round computes (N > 1)
@@ -237,9 +337,14 @@ def main():
     my_rows = sum(n for _, n in mine)
 
     t0 = time.perf_counter()
-    blks = [DeviceCsrBlock.generate(SEED_A, r0, n, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r, _lib.VAL_UNIFORM,
-                                    np.float64, device=dev) for r0, n in mine]
+    blks = [DeviceCsrBlock.generate(SEED_A, r0, n, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64, device=dev)
+            for r0, n in mine]
     my_nnz = sum(b.nnz for b in blks)
+    nnz_total = my_nnz
+    if world > 1:
+        t = torch.tensor([my_nnz], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        nnz_total = int(t.item())
     x = gen_dense(SEED_X, 0, n_cols, k, device=dev)
     y_local = torch.empty((chunks, cr, k), dtype=torch.float64, device=dev)
     nnz_local = torch.zeros((chunks, cr), dtype=torch.int32, device=dev)
@@ -319,8 +424,8 @@ def main():
     verified = None
     if args.verify:
         if rank == 0:  # the whole product on one GPU, compared with the assembled one
-            full = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r,
-                                           _lib.VAL_UNIFORM, np.float64, device=dev)
+            full = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64,
+                                           device=dev)
             full.plan(k, args.panel_cols)
             y_ref = torch.empty((rows, k), dtype=torch.float64, device=dev)
             nnz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
@@ -332,7 +437,10 @@ def main():
         if world > 1:
             dist.barrier()
     out_nnz = comp.nnz()
-    nnz_total = rows * nnz_r
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = end_to_end(args.config, blks, x, comp, step, rows, k)
+        log(f"end to end: {e2e}")
     ms_per_step = elapsed / args.steps * 1e3
     value = b_alg(rows, n_cols, nnz_total, k) / (elapsed / args.steps) / 1e9
     # roofline of the dominant kernel (the SpMM: n_passes launches of the
@@ -340,6 +448,7 @@ def main():
     # bytes of THIS rank's SpMM over its measured average duration
     b_launch = b_alg(my_rows, n_cols, my_nnz, k)
     achieved = b_launch / (float(np.mean(kern_ms)) / 1e3) / 1e9
+    achieved_gather = b_gather(my_rows, my_nnz, k) / (float(np.mean(kern_ms)) / 1e3) / 1e9
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -370,8 +479,9 @@ def main():
             "data": "synthetic (SplitMix64 random CSR, sorted distinct uniform columns, values U[0.5,1.5); "
                     "generated on device from seeds 1000/1001)",
             "config": {
-                "workload": f"{args.config}: {rows:,} x {n_cols:,} CSR, {nnz_r} nnz/row "
-                            f"({100.0 * nnz_r / n_cols:g} % density, nnz {nnz_total:,}) x {k}-column dense RHS, "
+                "workload": f"{args.config}: {rows:,} x {n_cols:,} CSR, "
+                            + (f"{nnz_r} nnz/row" if nnz_r else f"Binomial({n_cols}, {C1_P:g}) nnz/row")
+                            + f" ({100.0 * nnz_total / rows / n_cols:.3g} % density, nnz {nnz_total:,}) x {k}-column dense RHS, "
                             f"f64; step = SpMM + {'RCCL all-gather of Y + ' if world > 1 else ''}compaction "
                             f"to Csr",
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
@@ -391,8 +501,8 @@ def main():
             "verified_vs_single_gpu": verified,
             "roofline": {
                 "bound": "hbm",
-                "kernel": (f"spmm_k32_f64<4,true,{'true' if panel_cols else 'false'}>" if k == 32
-                           else ("spmv_stream<double>" if k == 1 else "spmm_rowwave<double>")),
+                "kernel": kernel_label(my_rows, my_nnz, k, panel_cols),
+                "model": "B_alg (SURVEY.md §8d canonical: X and Y counted once)",
                 "launches_per_spmm": n_passes,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
@@ -403,6 +513,16 @@ def main():
                 "traffic_GBps": round(traffic / (float(np.mean(kern_ms)) / 1e3) / 1e9, 1) if traffic else None,
                 "bytes_per_launch_alg": b_launch,
             },
+            "roofline_gather": {
+                "bound": "hbm",
+                "model": "B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row)",
+                "achieved": round(achieved_gather, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gather / HBM_PEAK_GBS, 5),
+                "bytes_per_launch_gather": b_gather(my_rows, my_nnz, k),
+            },
+            "end_to_end_ms": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -10,6 +10,14 @@
 
 #include "../basic_sparse_matrix_amd/csrc/bsm_synth.h"
 
+/* Timing fidelity for the CPU baseline (bench.py cpu_baseline): when set,
+ * mul_dense allocates and fills get_row_compact's per-row Vec exactly as the
+ * reference does (capacity dims.cols x 24 B, sparse.rs:254) before the
+ * column loop. Results are identical either way. */
+static int orc_emulate_row_alloc = 0;
+void orc_set_emulate_row_alloc(int on) { orc_emulate_row_alloc = on; }
+typedef struct { const void* v; uint64_t col; uint64_t row; } orc_entry_; /* CsrEntry<&T> */
+
 #define T double
 #define SUF f64
 #define UT uint64_t

@@ -147,6 +147,10 @@ ORC_DECL_CHOL(f64, double)
 ORC_DECL_CHOL(f32, float)
 
 /* ---- Synthetic inputs (bsm_synth.h recipe, host side) -------------------- */
+/* Timing fidelity switch for the CPU baseline: emulate get_row_compact's
+ * per-row Vec allocation (capacity dims.cols x 24 B, sparse.rs:254). */
+void orc_set_emulate_row_alloc(int on);
+
 /* Row lengths for CONST/UNIFORM/BINOMIAL families -> row_ptr (rows+1). */
 int orc_gen_row_ptr(uint64_t seed, uint64_t rows, uint32_t n_cols, int rowlen_kind,
                     uint32_t a, uint32_t b, uint64_t* row_ptr);

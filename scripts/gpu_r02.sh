@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-2 GPU session: scripts/gpu_r02.sh TAG STEP...
+# STEP: tests | smoke | bench:<config>[:extra bench args] | prof:<config> | c5
+# Every step runs under its own time limit; the session stops at the first
+# failing step (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+OUT=gpurun_out
+TAG=$1
+shift
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session_$TAG.log
+  timeout -k 10 "$t" "$@" > "$OUT/${name}_$TAG.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/session_$TAG.log
+  tail -3 "$OUT/${name}_$TAG.log" | cut -c1-600 | tee -a $OUT/session_$TAG.log
+  return $rc
+}
+for step in "$@"; do
+  case $step in
+    tests) run gpu_tests 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
+             --timeout-method thread --durations=8 || exit $? ;;
+    tests:*) run gpu_tests_sel 600 python -u -m pytest ${step#tests:} -m gpu -x -q -p no:cacheprovider \
+             --timeout 150 --timeout-method thread --durations=8 || exit $? ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench:*) IFS=: read -r _ cfg extra <<< "$step"
+             run bench_$cfg 600 python bench.py --config $cfg $extra || exit $? ;;
+    prof:*) cfg=${step#prof:}
+            run prof_$cfg 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${cfg}_$TAG -o run \
+                --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e || exit $? ;;
+    c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session $TAG done" | tee -a $OUT/session_$TAG.log

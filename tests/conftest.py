@@ -24,6 +24,15 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_c5():
+    """The band oracle's C5 solve (scripts/make_c5_fixture.py)."""
+    import json
+
+    with open(os.path.join(HERE, "golden", "c5_poisson_1000.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
 def orc():
     from oracle import pyoracle
 

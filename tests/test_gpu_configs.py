@@ -29,6 +29,7 @@ def test_device_generator_matches_host(orc):
         (5000, 100_000, orc.ROWLEN_CONST, 10, 10, orc.VAL_UNIFORM, np.float64),
         (3000, 5000, orc.ROWLEN_UNIFORM, 0, 1200, orc.VAL_SMALLINT, np.int32),
         (400, 1500, orc.ROWLEN_UNIFORM, 1000, 1500, orc.VAL_UNIFORM, np.float32),  # bump passes
+        (1024, 1024, orc.ROWLEN_BINOMIAL, round(0.01 * 2 ** 32), 0, orc.VAL_UNIFORM, np.float64),  # C1
     ]:
         blk = device.DeviceCsrBlock.generate(1000, 777, rows, n_cols, kind, a, b, vk, dt)
         rp = orc.gen_row_ptr(1000, rows + 777, n_cols, kind, a, b)
@@ -59,6 +60,51 @@ def _run_spmm(blk, x, k):
     comp(y, row_nnz)
     torch.cuda.synchronize()
     return y, comp
+
+
+def test_c1_public_api_bit_exact(orc):
+    """C1 (BASELINE.json configs[0]): 1024 x 1024, Binomial(1024, 0.01) row
+    lengths (~10.5k nnz, some rows empty or long), k = 1, f64, through the
+    public Csr.mul_dense (sparse.rs:426-446) with host operands, bit-exact
+    against the oracle; then the same matrix through the device-level SpMV
+    (the bench's timed path) and compaction."""
+    from basic_sparse_matrix_amd import Csr, Dense
+
+    rows = n_cols = 1024
+    rp = orc.gen_row_ptr(1000, rows, n_cols, orc.ROWLEN_BINOMIAL, round(0.01 * 2 ** 32), 0)
+    ci, v = orc.gen_entries(1000, rp, n_cols)
+    lens = np.diff(rp.astype(np.int64))
+    assert 9_000 < rp[-1] < 12_000 and lens.min() <= 3 and lens.max() >= 18
+    x_cols = orc.gen_x_cols(1001, n_cols, 1)
+    got = Csr.from_csr_arrays((rows, n_cols), rp, ci, v).mul_dense(Dense.from_columns(x_cols))
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    assert np.array_equal(np.asarray(got.row_index, np.uint64), erp)
+    assert np.array_equal(np.asarray(got.col_index, np.uint64), eci)
+    assert np.array_equal(np.asarray(got.v).view(np.uint64), ev.view(np.uint64))
+    device = _dev()
+    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_BINOMIAL, round(0.01 * 2 ** 32), 0)
+    y, comp = _run_spmm(blk, device.gen_dense(1001, 0, n_cols, 1), 1)
+    assert np.array_equal(comp.row_ptr.cpu().numpy(), erp.astype(np.int64))
+    assert np.array_equal(comp.vals[:comp.nnz()].cpu().numpy().view(np.uint64), ev.view(np.uint64))
+
+
+@pytest.mark.parametrize("variant", ["0", "1"])  # spmv_rows (default for short rows) / spmv_stream
+def test_spmv_variants_ragged_rows_bit_exact(orc, monkeypatch, variant):
+    """k = 1 on ragged rows (empty rows, rows longer than a workgroup's LDS
+    chunk) through both SpMV kernels, bit-exact."""
+    from basic_sparse_matrix_amd import Csr, Dense
+
+    monkeypatch.setenv("BSM_SPMV_VARIANT", variant)
+    rows, n_cols = 3000, 50_000
+    lens = np.random.default_rng(7).integers(0, 12, rows)
+    lens[[5, 700, 2999]] = [0, 9000, 5000]  # rows longer than 256 * 16 entries
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ci, v = orc.gen_entries(1000, rp, n_cols)
+    x_cols = orc.gen_x_cols(1001, n_cols, 1)
+    got = Csr.from_csr_arrays((rows, n_cols), rp, ci, v).mul_dense(Dense.from_columns(x_cols))
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    assert np.array_equal(np.asarray(got.row_index, np.uint64), erp)
+    assert np.array_equal(np.asarray(got.v).view(np.uint64), ev.view(np.uint64))
 
 
 @pytest.mark.parametrize("k", [1, 32])

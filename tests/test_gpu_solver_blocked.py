@@ -126,9 +126,10 @@ def test_blocked_poisson_250_f64_vs_reference_order(orc, monkeypatch, blk_chol, 
 
 
 @pytest.mark.slow
-def test_c5_blocked_poisson_1m_f64_properties(orc):
-    """C5 (N = 1M, bandwidth 1000) through the blocked solves: x_true to
-    1e-6 relative (BASELINE.json), residual tiny."""
+def test_c5_blocked_poisson_1m_f64_properties(orc, golden_c5):
+    """C5 (N = 1M, bandwidth 1000) through the blocked solves: within 1e-6
+    relative (BASELINE.json) of the band oracle's exact x (sampled from
+    tests/golden/c5_poisson_1000.json) and of x_true, residual tiny."""
     g = 1000
     n = g * g
     rp, ci, v = orc.poisson2d(g)
@@ -138,6 +139,8 @@ def test_c5_blocked_poisson_1m_f64_properties(orc):
     b = np.zeros(n)
     np.add.at(b, rows, v * x_true[ci.astype(np.int64)])
     x = solve(A, Dense.from_columns([b]), order="blocked").get_col(0)
+    exact = np.asarray([int(h, 16) for h in golden_c5["x_sample_bits"]], dtype=np.uint64).view(np.float64)
+    assert rel_err(x[::golden_c5["x_stride"]], exact) < 1e-6
     assert rel_err(x, x_true) < 1e-6
     r = np.zeros(n)
     np.add.at(r, rows, v * x[ci.astype(np.int64)])
