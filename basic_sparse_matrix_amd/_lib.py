@@ -47,6 +47,7 @@ BSM_ERR_PANIC = 4
 BSM_ERR_HIP = 5
 BSM_ERR_OOM = 6
 BSM_ERR_UNSUPPORTED = 7
+BSM_TILED_ANY_PADDING = 1
 BSM_ERR_NO_DEVICE = 8
 BSM_ERR_OUT_OF_BOUNDS = 9
 
@@ -108,6 +109,11 @@ SIGNATURES = [
     ("bsm_dev_spmm_plan_bytes", _u64, [_u64, _u64, _u64]),
     ("bsm_dev_spmm_plan", _int, [_u64, _u64, _vp, _vp, _u64, _vp, ctypes.POINTER(_int), _vp]),
     ("bsm_dev_spmm_panelled", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
+    ("bsm_dev_tiled_wanted", _int, [_int, _u64, _u64, _u64, _u64, _u64]),
+    ("bsm_dev_tiled_create", _int, [_u64, _u64, _u64, _vp, _vp, _vp, _int, ctypes.POINTER(_vp), _vp]),
+    ("bsm_dev_spmm_tiled", _int, [_vp, _vp, _vp, _vp, _vp]),
+    ("bsm_tiled_info", _int, [_vp, _u64p, _u64p, _u64p]),
+    ("bsm_tiled_destroy", None, [_vp]),
     ("bsm_dev_compact", _int, [_int, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
 ]
 

@@ -168,6 +168,18 @@ struct bsm_csr {
     mutable bool plan_usable = false;
 };
 
+// Row-block x column-panel copy of a matrix (kernels_tiled.hip).
+struct bsm_tiled {
+    int device = 0;
+    uint64_t rows = 0, n_cols = 0, nnz = 0;
+    uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
+    uint64_t chunks = 0;         // total, without the over-read padding (4 chunks)
+    int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
+    uint32_t* meta = nullptr;    // (chunks + OVERREAD) * 64
+    double* val = nullptr;       // (chunks + OVERREAD) * 64
+    unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
+};
+
 namespace bsm {
 int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz);
 int csr_analyse(bsm_csr* m, hipStream_t s);
@@ -200,6 +212,12 @@ int spmm_plan(uint64_t rows, uint64_t n_cols, const int64_t* rp, const int32_t* 
 int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
                   int32_t* row_nnz, uint64_t panel_cols, const int32_t* seg, hipStream_t s);
+// row-block x column-panel schedule (kernels_tiled.hip)
+bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len);
+int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                 const double* vals, int flags, bsm_tiled** out, hipStream_t s);  // synchronous
+int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, hipStream_t s);
+void tiled_destroy(bsm_tiled* t);
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
                      int32_t* out_col, void* out_vals, hipStream_t s);
 int pack_cols_to_rowmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor, void* rowmajor,

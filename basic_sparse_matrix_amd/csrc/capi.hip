@@ -651,6 +651,31 @@ int bsm_dev_spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nn
                          seg, static_cast<hipStream_t>(stream));
 }
 
+int bsm_dev_tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k,
+                         uint64_t max_row_len) {
+    return tiled_wanted(dtype, rows, n_cols, nnz, k, max_row_len) ? 1 : 0;
+}
+
+int bsm_dev_tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* row_ptr,
+                         const int32_t* col, const double* vals, int flags, bsm_tiled** out, void* stream) {
+    return tiled_create(rows, n_cols, nnz, row_ptr, col, vals, flags, out, static_cast<hipStream_t>(stream));
+}
+
+int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* row_nnz, void* stream) {
+    return tiled_spmm(t, x, y, row_nnz, static_cast<hipStream_t>(stream));
+}
+
+int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols) {
+    BSM_REQUIRE(t, BSM_ERR_INVALID, "null argument");
+    const uint64_t n = (t->chunks + 4) * 64;
+    if (bytes) *bytes = n * 12 + ((uint64_t)t->nw * t->nb + 1) * 8;
+    if (slots) *slots = t->chunks * 64;
+    if (panel_cols) *panel_cols = 1ull << t->pshift;
+    return BSM_OK;
+}
+
+void bsm_tiled_destroy(bsm_tiled* t) { tiled_destroy(t); }
+
 int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y, const int32_t* row_nnz,
                     int64_t* out_row_ptr, int32_t* out_col, void* out_vals, void* workspace,
                     uint64_t workspace_bytes, void* stream) {

@@ -1,0 +1,420 @@
+// kernels_tiled.hip -- row-block x column-panel schedule of Csr::mul_dense
+// for k = 32, f64 (reference: src/sparse.rs:426-446; the C4 shape).
+//
+// Why. At C4 every entry gathers a whole 256-B row of X (2.56 TB per SpMM)
+// from a 2.56 GB table: the one-row-per-wave kernels read it at the
+// Infinity-Cache/HBM rate (7.2 TB/s). Here each wave keeps the Y rows of a
+// block of RW rows in LDS for a whole sweep of X in panels of PC columns
+// (1 MiB of X at PC = 4096, well inside one XCD's 4 MiB L2). All waves sweep
+// the panels in step, so an XCD's 32 CUs (18k rows) gather each panel from
+// their shared L2; an X row is re-used about 1.8 times per L2 fill and the
+// misses go to the Infinity Cache, which holds the panels the 8 XCDs are on.
+// Measured at C4: 14.2 TB/s of gathers (180 ms) against 7.2 (353 ms).
+//
+// Layout (tiled_layout, once per matrix). Wave gw of NW owns the rows
+// [gw*RPW, (gw+1)*RPW), taken in NB batches of RW rows. A (wave, batch) task
+// is a stream of chunks of 64 entries; a chunk holds at most one entry of a
+// row, so the kernel reads, adds and writes back the 64 LDS rows of a chunk
+// as one batch. Chunks are filled greedily: the 64 rows whose next entry
+// (in storage order) has the lowest column panel, ties by row. Every row's
+// entries therefore stay in storage order and the per-element sum is the
+// reference's sequential sum: bit-exact. Chunk n may only take entries of
+// panels <= n / R, R = the task's mean chunks per panel + 3 %: waves with
+// equal work then sweep the panels in step without talking to each other.
+// Free slots hold dummy entries (row RW, a scratch LDS row; X row 0; value
+// 0). Entry = meta (col << 8 | row-in-batch, so cols < 2^24) + the f64
+// value: 12 B, like CSR's col + val.
+//
+// Kernel (spmm_tiled_k32). One 256-thread workgroup per CU (LDS-bound), four
+// waves. Per task: zero the LDS rows, stream the chunks through a six-phase
+// pipeline (indices four chunks ahead, gathers two ahead, so 32 gathers of
+// 1 KiB are in flight per wave), write the Y rows and their nonzero counts,
+// then meet the other waves at a bounded batch barrier (time noise would
+// otherwise spread the waves over the batch cycle: 369 ms without it).
+// Lane 16g+q of a chunk handles entry (quad q, group g) at load time; a DPP
+// row broadcast hands entry (u, g) to the 16 lanes of group g, which gather
+// X[col][2q..2q+1] (16 B each, one 256-B row per group).
+#include "bsm_internal.hpp"
+
+#include <cstdlib>
+#include <utility>
+
+
+namespace bsm {
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int CHUNK = 64;        // entries per chunk = 16 quads x 4 lane groups
+constexpr int PHASES = 6;        // pipeline unroll; task chunk counts are multiples of it
+constexpr int OVERREAD = 4;      // chunks the pipeline reads past a task's end
+constexpr uint32_t DONE = 0xffffffffu;
+constexpr uint32_t RW_MAX = 144;  // 4 waves x (RW+1) rows x 256 B <= 160 KiB of LDS
+constexpr uint32_t PSHIFT = 12;   // panel = 4096 columns = 1 MiB of X (C4 sweep: 2^10..2^12 flat, 2^13 +12 %, 2^14 +42 %)
+constexpr uint32_t PACE_PCT = 3;  // chunk budget per panel over the task's mean (padding ~ this; C4: 2 % +19 %, 6 % +2 %)
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) {
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, WAVE));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// layout builder: one wave per task (gw, b). COUNT pass writes the task's
+// chunk count (a multiple of PHASES); WRITE pass fills its chunks from offs.
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+__global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_cols, double pace,
+                                                    const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col,
+                                                    const double* __restrict__ vals, uint32_t nw,
+                                                    uint32_t rpw, uint32_t nb, uint32_t rw, uint32_t pshift,
+                                                    int32_t* __restrict__ counts,
+                                                    const int64_t* __restrict__ offs,
+                                                    uint32_t* __restrict__ meta, double* __restrict__ val) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const uint64_t task = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    if (task >= (uint64_t)nw * nb) return;
+    const uint64_t gw = task / nb, b = task % nb;
+    const uint64_t w0 = gw * rpw;
+    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
+    const uint64_t r0 = w0 + b * rw;
+    int64_t cur[3], end[3];
+    uint32_t h[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t s = lane + WAVE * j;
+        const bool live = s < rw && r0 + s < wend;
+        cur[j] = live ? rp[r0 + s] : 0;
+        end[j] = live ? rp[r0 + s + 1] : 0;
+        h[j] = cur[j] < end[j] ? (uint32_t)col[cur[j]] >> pshift : DONE;
+    }
+    // pace: chunk n may take entries from panels <= n * inv_r, inv_r = panels
+    // per chunk at the task's own density plus a margin, so that the waves of a
+    // batch (equal work at C4) stay on the same panels in step without talking
+    // to each other; a wave that falls behind catches up by the margin
+    const int64_t t0 = rp[r0], t1 = rp[min<uint64_t>(r0 + rw, wend)];
+    const double np = (double)(((n_cols - 1) >> pshift) + 1);
+    const double inv_r = t1 > t0 ? (double)CHUNK * np / ((double)(t1 - t0) * pace) : 1e30;
+    int64_t c = WRITE ? offs[task] : 0;
+    int64_t n = 0;
+    for (;;) {
+        bool sel[3] = {false, false, false};
+        int pos[3] = {0, 0, 0};
+        int taken = 0;
+        const double pm = (double)n * inv_r;
+        const uint32_t pmax = pm >= 4.0e9 ? DONE - 1 : (uint32_t)pm;
+        bool done = false;
+        while (taken < CHUNK) {  // the lowest panels first, ties by row
+            uint32_t m = min(min(sel[0] ? DONE : h[0], sel[1] ? DONE : h[1]), sel[2] ? DONE : h[2]);
+            m = wave_min_u32(m);
+            if (m == DONE) {
+                done = taken == 0;
+                break;
+            }
+            if (m > pmax) break;  // ahead of the pace: the rest of the chunk is padding
+            uint64_t bal[3];
+            int cnt[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                bal[j] = __ballot(!sel[j] && h[j] == m);
+                cnt[j] = __popcll(bal[j]);
+            }
+            const int take = min(cnt[0] + cnt[1] + cnt[2], CHUNK - taken);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                if (!sel[j] && h[j] == m) {
+                    const int rank = (j > 0 ? cnt[0] : 0) + (j > 1 ? cnt[1] : 0) +
+                                     __popcll(bal[j] & lanemask_lt(lane));
+                    if (rank < take) {
+                        sel[j] = true;
+                        pos[j] = taken + rank;
+                    }
+                }
+            }
+            taken += take;
+        }
+        if (done) break;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (sel[j]) {
+                const int64_t e = cur[j];
+                if (WRITE) {
+                    meta[c * CHUNK + pos[j]] = ((uint32_t)col[e] << 8) | (uint32_t)(lane + WAVE * j);
+                    val[c * CHUNK + pos[j]] = vals[e];
+                }
+                cur[j] = e + 1;
+                h[j] = cur[j] < end[j] ? (uint32_t)col[cur[j]] >> pshift : DONE;
+            }
+        }
+        if (WRITE && lane >= taken) {  // dummy entries: scratch row rw, X row 0, value 0
+            meta[c * CHUNK + lane] = rw;
+            val[c * CHUNK + lane] = 0.0;
+        }
+        ++c;
+        ++n;
+    }
+    const int64_t padded = (n + PHASES - 1) / PHASES * PHASES;
+    if (WRITE) {
+        for (int64_t p = n; p < padded; ++p, ++c) {
+            meta[c * CHUNK + lane] = rw;
+            val[c * CHUNK + lane] = 0.0;
+        }
+    } else if (lane == 0) {
+        counts[task] = (int32_t)padded;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the SpMM
+// ---------------------------------------------------------------------------
+struct Idx {
+    uint32_t mi;  // lane 16g+q: entry (quad q, group g) of the chunk
+    double vi;
+};
+__device__ __forceinline__ void load_idx(Idx& c, const uint32_t* __restrict__ meta, const double* __restrict__ val,
+                                         int64_t chunk, int lane) {
+    c.mi = meta[chunk * CHUNK + lane];
+    c.vi = val[chunk * CHUNK + lane];
+}
+template <int I>
+__device__ __forceinline__ uint32_t bm(const Idx& c) {  // entry (I, g) to every lane of group g
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.mi, 0x150 + I, 0xf, 0xf, false);
+}
+template <int I>
+__device__ __forceinline__ double bv(const Idx& c) {
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(c.vi), 0x150 + I, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, __double2loint(c.vi), 0x150 + I, 0xf, 0xf, false));
+}
+template <int... I>
+__device__ __forceinline__ void gather(double2 (&x)[16], const Idx& c, const double2* __restrict__ X, int q,
+                                       std::integer_sequence<int, I...>) {
+    ((x[I] = X[(int64_t)(bm<I>(c) >> 8) * 16 + q]), ...);
+}
+template <int I>
+__device__ __forceinline__ double2* yaddr(const Idx& c, double2* yw, int q) {
+    return yw + (bm<I>(c) & 255u) * 16 + q;
+}
+template <int I>
+__device__ __forceinline__ void madd(double2& y, const double2& x, const Idx& c) {
+    const double v = bv<I>(c);
+    y.x = __dadd_rn(y.x, __dmul_rn(v, x.x));
+    y.y = __dadd_rn(y.y, __dmul_rn(v, x.y));
+}
+// the chunk's rows are distinct (dummies all hit the scratch row): all 16
+// LDS reads, the 32 multiply-adds, all 16 writes
+template <int... I>
+__device__ __forceinline__ void sum_chunk(const double2 (&x)[16], const Idx& c, double2* yw, int q,
+                                          std::integer_sequence<int, I...>) {
+    double2 y[16];
+    ((y[I] = *yaddr<I>(c, yw, q)), ...);
+    (madd<I>(y[I], x[I], c), ...);
+    ((*yaddr<I>(c, yw, q) = y[I]), ...);
+}
+
+// Batch pacing. Within a batch the layout keeps the waves on the same
+// panels (equal chunks per panel), but time noise accumulates from batch to
+// batch; once the waves are spread over the batch cycle, every XCD gathers
+// from all of X again. So the waves meet at every batch start: arrivals are
+// counted in 8 words (one per blockIdx % 8, 128-B apart) by relaxed agent
+// atomics and a wave polls their sum. A pacing aid only: nothing is handed
+// off (X, the stream and the wave's own LDS rows are all it reads), and the
+// wait is bounded, so a grid that is not all resident (other kernels on the
+// CUs) costs one timeout per wave and then runs unpaced.
+constexpr int BAR_STRIDE = 32;  // words between the arrival counters
+__device__ __forceinline__ void batch_arrive(unsigned* bar, uint32_t n, int lane) {
+    if (lane == 0) __hip_atomic_fetch_add(bar + (blockIdx.x & 7) * BAR_STRIDE, n, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int lane) {
+    for (int spin = 0; spin < 4000; ++spin) {
+        uint32_t v = lane < 8 ? __hip_atomic_load(bar + lane * BAR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : 0u;
+        v += (uint32_t)__shfl_xor((int)v, 1);
+        v += (uint32_t)__shfl_xor((int)v, 2);
+        v += (uint32_t)__shfl_xor((int)v, 4);
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)v) >= target) return true;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    return false;  // not all resident: stop pacing
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
+    uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
+    const uint32_t* __restrict__ meta, const double* __restrict__ val, const double2* __restrict__ X,
+    double2* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar) {
+    extern __shared__ double2 ylds[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = threadIdx.x / WAVE;
+    const int g = lane >> 4, q = lane & 15;
+    double2* yw = ylds + (size_t)wave * (rw + 1) * 16;
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+    const uint64_t w0 = gw * rpw;
+    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
+    constexpr auto SEQ = std::make_integer_sequence<int, 16>{};
+    bool sync = bar != nullptr;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t r0 = w0 + (uint64_t)b * rw;
+        if (r0 >= wend) {  // out of rows: arrive for the batches left and stop
+            if (sync) batch_arrive(bar, nb - b, lane);
+            break;
+        }
+        if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane);
+        const int nr = (int)min<uint64_t>(rw, wend - r0);
+        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = make_double2(0.0, 0.0);
+        const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
+        if (c1 > c0) {  // (c1 - c0) % PHASES == 0
+            Idx M[6];
+            double2 XS[3][16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
+            gather(XS[0], M[0], X, q, SEQ);
+            gather(XS[1], M[1], X, q, SEQ);
+            for (int64_t i = c0; i < c1; i += PHASES) {
+#pragma unroll
+                for (int k = 0; k < PHASES; ++k) {
+                    load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
+                    gather(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, SEQ);
+                    __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
+                    sum_chunk(XS[k % 3], M[k], yw, q, SEQ);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        for (int rb = 0; rb < nr; rb += 4) {  // Y rows and their nonzero counts
+            const int r = rb + g;
+            const bool live = r < nr;
+            const double2 y = live ? yw[r * 16 + q] : make_double2(0.0, 0.0);
+            if (live) Y[(r0 + r) * 16 + q] = y;
+            const uint64_t m0 = __ballot(y.x != 0.0), m1 = __ballot(y.y != 0.0);
+            if (live && q == 0 && row_nnz)
+                row_nnz[r0 + r] = __popcll((m0 >> (16 * g)) & 0xffffull) + __popcll((m1 >> (16 * g)) & 0xffffull);
+        }
+        if (sync) batch_arrive(bar, 1, lane);
+    }
+}
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* e = getenv(name);
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
+}
+
+}  // namespace
+
+// Shape test: f64, k = 32, X beyond the Infinity Cache, columns < 2^24, rows
+// at most a few times the mean length (a long row serialises its chunks).
+bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len) {
+    if (const char* e = getenv("BSM_SPMM_TILED")) {
+        if (atoi(e) == 0) return false;
+        if (atoi(e) == 2) return dtype == BSM_F64 && k == 32 && n_cols < (1u << 24) && rows > 0 && nnz > 0;
+    }
+    if (dtype != BSM_F64 || k != 32 || n_cols >= (1u << 24) || rows == 0 || nnz == 0) return false;
+    const uint64_t x_bytes = n_cols * k * sizeof(double);
+    if (x_bytes <= (1ull << 30)) return false;
+    const uint64_t mean = (nnz + rows - 1) / rows;
+    return max_row_len <= 2 * mean + 256;
+}
+
+int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                 const double* vals, int flags, bsm_tiled** out, hipStream_t s) {
+    BSM_REQUIRE(out && rp && (nnz == 0 || (col && vals)), BSM_ERR_INVALID, "tiled: null argument");
+    BSM_REQUIRE(n_cols < (1u << 24), BSM_ERR_UNSUPPORTED, "tiled: columns must be < 2^24");
+    *out = nullptr;
+    int dev = 0;
+    BSM_TRY(current_device(&dev));
+    int cus = 0;
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const uint32_t nw = env_u32("BSM_TILED_WAVES", 4u * (uint32_t)cus);
+    uint32_t rw_max = env_u32("BSM_TILED_RW", RW_MAX);
+    rw_max = rw_max < 8u ? 8u : (rw_max > RW_MAX ? RW_MAX : rw_max);
+    const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", PSHIFT);
+    const double pace = 1.0 + env_u32("BSM_TILED_PACE_PCT", PACE_PCT) / 100.0;
+    BSM_REQUIRE(nw >= 4 && nw % 4 == 0 && pshift < 24, BSM_ERR_INVALID, "tiled: bad geometry");
+    const uint64_t rpw64 = (rows + nw - 1) / nw;
+    BSM_REQUIRE(rpw64 < (1ull << 31), BSM_ERR_UNSUPPORTED, "tiled: too many rows per wave");
+    const uint32_t rpw = rpw64 ? (uint32_t)rpw64 : 1u;
+    const uint32_t nb = (rpw + rw_max - 1) / rw_max;
+    const uint32_t rw = (rpw + nb - 1) / nb;  // equal batches
+    const uint64_t tasks = (uint64_t)nw * nb;
+
+    DBuf counts, offs, ws;
+    BSM_TRY(counts.alloc(tasks * sizeof(int32_t)));
+    BSM_TRY(offs.alloc((tasks + 1) * sizeof(int64_t)));
+    const uint64_t grid = (tasks + 3) / 4;
+    tiled_layout<false><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rp, col, vals, nw, rpw, nb, rw, pshift,
+                                                            counts.as<int32_t>(), nullptr, nullptr, nullptr);
+    BSM_HIP_TRY(hipGetLastError());
+    const uint64_t wsb = scan_workspace_bytes(tasks);
+    BSM_TRY(ws.alloc(wsb));
+    BSM_TRY(exclusive_scan_i32_to_i64(counts.as<int32_t>(), offs.as<int64_t>(), tasks, ws.p, wsb, s));
+    int64_t total = 0;
+    BSM_HIP_TRY(read_dev(&total, offs.as<int64_t>() + tasks, sizeof(total), s));
+    // a stream much longer than the matrix means rows too uneven for 64-row chunks
+    BSM_REQUIRE((flags & BSM_TILED_ANY_PADDING) ||
+                    (uint64_t)total * CHUNK <= nnz + nnz / 4 + tasks * PHASES * CHUNK + (uint64_t)CHUNK * 64,
+                BSM_ERR_UNSUPPORTED, "tiled: %lld chunks for %llu entries (rows too uneven)", (long long)total,
+                (unsigned long long)nnz);
+    const uint64_t slots = ((uint64_t)total + OVERREAD) * CHUNK;
+    size_t free_b = 0, total_b = 0;
+    BSM_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    BSM_REQUIRE(slots * 12 + (256ull << 20) < free_b, BSM_ERR_OOM, "tiled: %llu MB stream does not fit",
+                (unsigned long long)(slots * 12 >> 20));
+    DBuf meta, val, bar;
+    BSM_TRY(bar.alloc(8 * BAR_STRIDE * sizeof(unsigned)));
+    BSM_TRY(meta.alloc(slots * sizeof(uint32_t)));
+    BSM_TRY(val.alloc(slots * sizeof(double)));
+    tiled_layout<true><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rp, col, vals, nw, rpw, nb, rw, pshift, nullptr,
+                                                           offs.as<int64_t>(), meta.as<uint32_t>(),
+                                                           val.as<double>());
+    BSM_HIP_TRY(hipGetLastError());
+    // over-read padding: valid dummy entries (X row 0)
+    BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, OVERREAD * CHUNK * 4, s));
+    BSM_HIP_TRY(hipMemsetAsync(val.as<double>() + (uint64_t)total * CHUNK, 0, OVERREAD * CHUNK * 8, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    auto* t = new bsm_tiled;
+    t->device = dev;
+    t->rows = rows;
+    t->n_cols = n_cols;
+    t->nnz = nnz;
+    t->nw = nw;
+    t->rpw = rpw;
+    t->nb = nb;
+    t->rw = rw;
+    t->pshift = pshift;
+    t->chunks = (uint64_t)total;
+    t->offs = static_cast<int64_t*>(offs.release());
+    t->meta = static_cast<uint32_t*>(meta.release());
+    t->val = static_cast<double*>(val.release());
+    t->bar = static_cast<unsigned*>(bar.release());
+    *out = t;
+    return BSM_OK;
+}
+
+int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, hipStream_t s) {
+    BSM_REQUIRE(t && (t->rows == 0 || (x && y)), BSM_ERR_INVALID, "tiled: null argument");
+    if (t->rows == 0) return BSM_OK;
+    const size_t lds = (size_t)4 * (t->rw + 1) * 256;
+    unsigned* bar = nullptr;
+    if (t->bar && t->nb > 1 && env_u32("BSM_TILED_SYNC", 1)) {
+        BSM_HIP_TRY(hipMemsetAsync(t->bar, 0, 8 * BAR_STRIDE * sizeof(unsigned), s));
+        bar = t->bar;
+    }
+    spmm_tiled_k32<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
+                                                    static_cast<const double2*>(x), static_cast<double2*>(y),
+                                                    row_nnz, bar);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
+void tiled_destroy(bsm_tiled* t) {
+    if (!t) return;
+    if (t->offs) (void)hipFree(t->offs);
+    if (t->meta) (void)hipFree(t->meta);
+    if (t->val) (void)hipFree(t->val);
+    if (t->bar) (void)hipFree(t->bar);
+    delete t;
+}
+
+}  // namespace bsm

@@ -50,6 +50,7 @@ class DeviceCsrBlock:
     dtype: np.dtype
     panel_cols: int = 0  # column-panel plan (bsm_dev_spmm_plan), 0 = none
     seg: torch.Tensor | None = None
+    tiled: "TiledPlan | None" = None  # row-block x column-panel copy (bsm_dev_tiled_create)
 
     @property
     def nnz(self) -> int:
@@ -91,11 +92,40 @@ class DeviceCsrBlock:
             self.panel_cols, self.seg = w, seg
         return self.panel_cols
 
+    def plan_tiled(self, k: int, force: bool = False) -> "TiledPlan | None":
+        """Build the row-block x column-panel copy for k right-hand columns
+        when the library wants it for this shape (f64, k = 32, X > 1 GiB), or
+        whenever possible with force (any chunk padding accepted). Synchronous, once per matrix. Returns
+        the plan, or None (shape not served, or no memory for the copy)."""
+        lib = _lib.require_device()
+        self.tiled = None
+        if self.dtype != np.float64 or k != 32 or self.nnz == 0:
+            return None
+        if not force:
+            max_len = int((self.row_ptr[1:] - self.row_ptr[:-1]).max().item()) if self.rows else 0
+            if not lib.bsm_dev_tiled_wanted(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz, k,
+                                            max_len):
+                return None
+        h = ctypes.c_void_p()
+        rc = lib.bsm_dev_tiled_create(self.rows, self.n_cols, self.nnz, _p(self.row_ptr), _p(self.col),
+                                      _p(self.vals), _lib.BSM_TILED_ANY_PADDING if force else 0, ctypes.byref(h),
+                                      _stream())
+        if rc in (_lib.BSM_ERR_UNSUPPORTED, _lib.BSM_ERR_OOM):
+            return None
+        _lib.check(rc)
+        self.tiled = TiledPlan(h.value)
+        return self.tiled
+
     def spmm(self, x: torch.Tensor, y: torch.Tensor, row_nnz: torch.Tensor | None = None, stream=None) -> None:
         """Y = A X (x: n_cols x k row-major, y: rows x k row-major), async.
-        Uses the column-panel plan when one was built (same bits)."""
+        Uses the tiled copy or the column-panel plan when one was built (same
+        bits)."""
         lib = _lib.load()
         k = x.shape[1] if x.dim() == 2 else 1
+        if self.tiled is not None and k == 32:
+            _lib.check(lib.bsm_dev_spmm_tiled(self.tiled.handle, _p(x), _p(y),
+                                              _p(row_nnz) if row_nnz is not None else 0, _stream(stream)))
+            return
         if self.seg is not None:
             _lib.check(lib.bsm_dev_spmm_panelled(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz,
                                                  _p(self.row_ptr), _p(self.col), _p(self.vals), k, _p(x), _p(y),
@@ -105,6 +135,24 @@ class DeviceCsrBlock:
         _lib.check(lib.bsm_dev_spmm(_lib.DTYPE_CODES[self.dtype], self.rows, self.n_cols, self.nnz, _p(self.row_ptr),
                                     _p(self.col), _p(self.vals), k, _p(x), _p(y),
                                     _p(row_nnz) if row_nnz is not None else 0, _stream(stream)))
+
+
+class TiledPlan:
+    """Owner of a bsm_tiled handle (the row-block x column-panel copy)."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    def info(self) -> dict:
+        lib = _lib.load()
+        b, sl, pc = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(lib.bsm_tiled_info(self.handle, ctypes.byref(b), ctypes.byref(sl), ctypes.byref(pc)))
+        return {"bytes": b.value, "slots": sl.value, "panel_cols": pc.value}
+
+    def __del__(self):
+        if getattr(self, "handle", None) and _lib._lib is not None:
+            _lib._lib.bsm_tiled_destroy(self.handle)
+            self.handle = None
 
 
 def gen_dense(seed, row0, n, k, value_kind=_lib.VAL_UNIFORM, dtype=np.float64, device="cuda") -> torch.Tensor:

@@ -61,8 +61,10 @@ def b_gather(rows, nnz, k):
     return 8 * (rows + 1) + 12 * nnz + 8 * nnz * k + 8 * rows * k
 
 
-def kernel_label(rows, nnz, k, panel_cols):
+def kernel_label(rows, nnz, k, panel_cols, tiled=False):
     """The kernel launch_spmm (kernels_spmm.hip) picks for this shape."""
+    if tiled:
+        return "spmm_tiled_k32"
     if k == 1:
         return "spmv_rows<double,16>" if nnz <= 12 * rows else "spmv_stream<double,4>"
     if k == 32:
@@ -290,6 +292,9 @@ def main():
                     help="rows of the CPU baseline sample (configs with more rows are extrapolated)")
     ap.add_argument("--panel-cols", type=int, default=None,
                     help="column-panel width of the SpMM schedule (default: the library's choice; 0 = one pass)")
+    ap.add_argument("--schedule", default="auto", choices=("auto", "tiled", "panel"),
+                    help="SpMM schedule: auto = the library's choice (row-block x column-panel copy when "
+                         "wanted, else column panels), tiled = the copy whenever possible, panel = never the copy")
     ap.add_argument("--chunks", type=int, default=0,
                     help="rounds of the block-cyclic row partition (0: 1 at N=1, 4 at N>1)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
@@ -357,16 +362,31 @@ def main():
     torch.cuda.synchronize()
     log(f"rank {rank}: {my_rows:,} rows in {chunks} round(s) of {cr:,}, nnz {my_nnz:,} generated in "
         f"{time.perf_counter() - t0:.1f} s")
-    # column-panel plan: built once per matrix (like the matrix itself, outside
-    # the timed region; its cost is reported as plan_ms)
+    # the SpMM schedule's per-matrix preparation, built once per matrix like
+    # the matrix itself (outside the timed region; its cost is reported as
+    # plan_ms): the row-block x column-panel copy, or the column-panel plan
     t0 = time.perf_counter()
-    panel_cols = 0
-    for b in blks:
-        panel_cols = b.plan(k, args.panel_cols)
+    panel_cols, tiled, tiled_info = 0, False, None
+    if args.schedule != "panel" and k == 32:
+        plans = [b.plan_tiled(k, force=args.schedule == "tiled") for b in blks]
+        tiled = all(p is not None for p in plans)
+        if tiled:
+            infos = [p.info() for p in plans]
+            tiled_info = {"bytes": sum(i["bytes"] for i in infos), "slots": sum(i["slots"] for i in infos),
+                          "panel_cols": infos[0]["panel_cols"]}
+        else:
+            for b in blks:
+                b.tiled = None
+    if not tiled:
+        for b in blks:
+            panel_cols = b.plan(k, args.panel_cols)
     torch.cuda.synchronize()
     plan_ms = (time.perf_counter() - t0) * 1e3
     n_passes = -(-n_cols // panel_cols) if panel_cols else 1
-    log(f"rank {rank}: panel width {panel_cols} ({n_passes} passes), plan {plan_ms:.1f} ms")
+    if tiled:
+        log(f"rank {rank}: row-block x column-panel copy {tiled_info}, built in {plan_ms:.1f} ms")
+    else:
+        log(f"rank {rank}: panel width {panel_cols} ({n_passes} passes), plan {plan_ms:.1f} ms")
 
     ev_k0 = torch.cuda.Event(enable_timing=True)
     ev_k1 = torch.cuda.Event(enable_timing=True)
@@ -426,7 +446,7 @@ def main():
         if rank == 0:  # the whole product on one GPU, compared with the assembled one
             full = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64,
                                            device=dev)
-            full.plan(k, args.panel_cols)
+            full.plan(k, args.panel_cols)  # the other schedule than the tiled ranks use: same bits
             y_ref = torch.empty((rows, k), dtype=torch.float64, device=dev)
             nnz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
             full.spmm(x, y_ref, nnz_ref)
@@ -461,7 +481,8 @@ def main():
             # this config (separate runs), corrected per MI355X_MICROARCH.md
             with open(pmc_json) as f:
                 pmc = json.load(f)
-            if pmc.get("panel_cols", 0) == panel_cols:  # same schedule as this run
+            if pmc.get("panel_cols", 0) == panel_cols and pmc.get("schedule", "panel") == (
+                    "tiled" if tiled else "panel"):  # same schedule as this run
                 traffic = pmc["traffic_bytes_per_launch"] * pmc.get("launches_per_spmm", 1)
                 traffic_src = os.path.relpath(pmc_json, ROOT)
         line = {
@@ -487,7 +508,11 @@ def main():
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
                 "parallelism": f"row-block x{world}" + (f" (block-cyclic, {chunks} rounds) + overlapped all-gather"
                                                          if world > 1 else ""),
-                "panel_cols": panel_cols, "passes": n_passes, "plan_ms": round(plan_ms, 1),
+                "schedule": "row-block x column-panel copy (spmm_tiled_k32)" if tiled else
+                            ("column panels" if panel_cols else "one pass"),
+                "panel_cols": tiled_info["panel_cols"] if tiled else panel_cols, "passes": n_passes,
+                "plan_ms": round(plan_ms, 1),
+                "tiled_copy": tiled_info,
             },
             "nnz_per_s": round(nnz_total / (elapsed / args.steps), 1),
             "hbm_frac_of_peak": round(value / (world * HBM_PEAK_GBS), 5),
@@ -501,7 +526,7 @@ def main():
             "verified_vs_single_gpu": verified,
             "roofline": {
                 "bound": "hbm",
-                "kernel": kernel_label(my_rows, my_nnz, k, panel_cols),
+                "kernel": kernel_label(my_rows, my_nnz, k, panel_cols, tiled),
                 "model": "B_alg (SURVEY.md §8d canonical: X and Y counted once)",
                 "launches_per_spmm": n_passes,
                 "achieved": round(achieved, 2),

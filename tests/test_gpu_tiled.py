@@ -1,0 +1,170 @@
+"""Row-block x column-panel SpMM schedule (kernels_tiled.hip): the re-laid
+copy of the matrix must give the same Y and row_nnz as the one-row-per-wave
+kernels, bit for bit, and the oracle's values (Csr::mul_dense,
+src/sparse.rs:426-446). Cases: the C4 shape on a 2M-row block (every row
+compared with the panelled kernel, a row sample with the oracle), uneven and
+empty rows, rows shorter than the wave count, several batches per wave,
+unsorted rows (storage-order sums), signed values with exact cancellations,
+NaN/inf."""
+
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from basic_sparse_matrix_amd import _lib  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    from basic_sparse_matrix_amd import device
+
+    return device
+
+
+def _spmm(blk, x, tiled):
+    y = torch.full((blk.rows, x.shape[1]), float("nan"), dtype=torch.float64, device="cuda")
+    nnz = torch.full((blk.rows,), -1, dtype=torch.int32, device="cuda")
+    saved = blk.tiled
+    if not tiled:
+        blk.tiled = None
+    blk.spmm(x, y, nnz)
+    blk.tiled = saved
+    torch.cuda.synchronize()
+    return y, nnz
+
+
+def _same(a, b):
+    return torch.equal(a.view(torch.int64), b.view(torch.int64))
+
+
+def _block(rp, ci, v, n_cols):
+    device = _dev()
+    return device.DeviceCsrBlock(0, len(rp) - 1, n_cols, torch.as_tensor(rp, dtype=torch.int64, device="cuda"),
+                                 torch.as_tensor(ci, dtype=torch.int32, device="cuda"),
+                                 torch.as_tensor(v, dtype=torch.float64, device="cuda"), np.dtype(np.float64))
+
+
+@pytest.fixture
+def geometry(monkeypatch):
+    def set_geometry(rw=None, waves=None, pshift=None):
+        for name, val in (("BSM_TILED_RW", rw), ("BSM_TILED_WAVES", waves), ("BSM_TILED_PSHIFT", pshift)):
+            if val is None:
+                monkeypatch.delenv(name, raising=False)
+            else:
+                monkeypatch.setenv(name, str(val))
+
+    return set_geometry
+
+
+@pytest.mark.parametrize("rw,waves,pshift", [(None, None, None), (16, 64, 10), (144, 8, 6), (96, 4, 13)])
+def test_tiled_equals_rowwave_random(orc, geometry, rw, waves, pshift):
+    device = _dev()
+    geometry(rw, waves, pshift)
+    rows, n_cols, k = 30_000, 200_000, 32
+    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_UNIFORM, 0, 120)  # empty rows too
+    x = device.gen_dense(1001, 0, n_cols, k)
+    assert blk.plan_tiled(k, force=True) is not None
+    y1, n1 = _spmm(blk, x, tiled=True)
+    y0, n0 = _spmm(blk, x, tiled=False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+    info = blk.tiled.info()
+    assert info["slots"] >= blk.nnz and info["panel_cols"] == 1 << (pshift or 12)
+    # a row sample against the oracle
+    rp = blk.row_ptr.cpu().numpy().astype(np.uint64)
+    ci, v = blk.col.cpu().numpy(), blk.vals.cpu().numpy()
+    r0, r1 = 12_345, 12_645
+    sub_rp = (rp[r0:r1 + 1] - rp[r0]).astype(np.uint64)
+    x_cols = orc.gen_x_cols(1001, n_cols, k)
+    erp, eci, ev = orc.mul_dense(r1 - r0, n_cols, sub_rp, ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]], x_cols)
+    got = y1[r0:r1].cpu().numpy()
+    dense = np.zeros((r1 - r0, k))
+    for r in range(r1 - r0):
+        dense[r, eci[erp[r]:erp[r + 1]]] = ev[erp[r]:erp[r + 1]]
+    assert np.array_equal(got.view(np.uint64), dense.view(np.uint64))
+
+
+def test_tiled_tiny_and_uneven(geometry):
+    """Fewer rows than waves, one long row among short ones, empty matrix rows."""
+    geometry(None, 64, 8)
+    rng = np.random.default_rng(7)
+    n_cols, k = 5000, 32
+    lens = rng.integers(0, 6, size=50)
+    lens[17] = 3000  # long row: serialised one entry per chunk
+    lens[3] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, size=n, replace=False)) for n in lens]).astype(np.int32)
+    v = rng.standard_normal(rp[-1])
+    blk = _block(rp, ci, v, n_cols)
+    x = torch.as_tensor(rng.standard_normal((n_cols, k)), device="cuda")
+    assert blk.plan_tiled(k, force=True) is not None
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+
+
+def test_tiled_unsorted_rows_keep_storage_order(geometry):
+    """Columns in random order inside each row: the layout takes every row's
+    entries in storage order, so the sums match the in-order kernel."""
+    geometry(32, 16, 9)
+    rng = np.random.default_rng(11)
+    rows, n_cols, k = 3000, 40_000, 32
+    lens = rng.integers(1, 80, size=rows)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ci = np.concatenate([rng.permutation(rng.choice(n_cols, size=n, replace=False)) for n in lens]).astype(np.int32)
+    v = rng.standard_normal(rp[-1]) * 1e3
+    blk = _block(rp, ci, v, n_cols)
+    x = torch.as_tensor(rng.standard_normal((n_cols, k)), device="cuda")
+    assert blk.plan_tiled(k, force=True) is not None
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+
+
+def test_tiled_cancellation_zero_pattern_nan_inf(geometry):
+    """Small integers with exact cancellations (zeros that compaction drops),
+    -0.0 inputs, NaN and inf in X: the same bits and counts."""
+    geometry(24, 8, 7)
+    rng = np.random.default_rng(5)
+    rows, n_cols, k = 2000, 3000, 32
+    lens = rng.integers(0, 40, size=rows)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, size=n, replace=False)) for n in lens]).astype(np.int32)
+    v = rng.integers(-3, 4, size=rp[-1]).astype(np.float64)
+    v[v == 0] = -0.0
+    xs = rng.integers(-2, 3, size=(n_cols, k)).astype(np.float64)
+    xs[7, 3] = np.nan
+    xs[11, :] = np.inf
+    blk = _block(rp, ci, v, n_cols)
+    x = torch.as_tensor(xs, device="cuda")
+    assert blk.plan_tiled(k, force=True) is not None
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+    assert int((n0 < k).sum()) > 0  # the zero pattern is exercised
+
+
+def test_tiled_c4_shape_block_matches_panelled(orc):
+    """C4 shape (10M columns, 1000 nnz/row, k=32) on a 2M-row block with the
+    library's default geometry: every row equals the column-panel kernel
+    bench.py used before, and a row sample equals the oracle."""
+    device = _dev()
+    n_cols, k, row0, rows = 10_000_000, 32, 3_000_000, 2_000_000
+    blk = device.DeviceCsrBlock.generate(1000, row0, rows, n_cols, _lib.ROWLEN_CONST, 1000, 1000)
+    x = device.gen_dense(1001, 0, n_cols, k)
+    assert blk.plan_tiled(k) is not None  # wanted at this shape
+    y1, n1 = _spmm(blk, x, True)
+    blk.tiled = None
+    torch.cuda.empty_cache()
+    assert blk.plan(k) == 2_000_000
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+    assert int(n1.min()) == k
+    sr = 1_234_567
+    rp = np.zeros(row0 + sr + 3, dtype=np.uint64)
+    rp[row0 + sr:] = np.arange(3, dtype=np.uint64) * 1000
+    ci, v = orc.gen_entries(1000, rp, n_cols, r0=row0 + sr, r1=row0 + sr + 2)
+    erp, eci, ev = orc.mul_dense(2, n_cols, rp[row0 + sr:] - rp[row0 + sr], ci, v, orc.gen_x_cols(1001, n_cols, k))
+    assert np.array_equal(y1[sr:sr + 2].reshape(-1).cpu().numpy().view(np.uint64), ev.view(np.uint64))
