@@ -114,6 +114,7 @@ SIGNATURES = [
     ("bsm_dev_spmm_tiled", _int, [_vp, _vp, _vp, _vp, _vp]),
     ("bsm_tiled_info", _int, [_vp, _u64p, _u64p, _u64p]),
     ("bsm_tiled_destroy", None, [_vp]),
+    ("bsm_csr_tiled", _int, [_vp, ctypes.POINTER(_int)]),
     ("bsm_dev_compact", _int, [_int, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
 ]
 

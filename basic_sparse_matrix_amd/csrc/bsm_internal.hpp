@@ -148,6 +148,18 @@ struct DBuf {
 
 }  // namespace bsm
 
+// Row-block x column-panel copy of a matrix (kernels_tiled.hip).
+struct bsm_tiled {
+    int device = 0;
+    uint64_t rows = 0, n_cols = 0, nnz = 0;
+    uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
+    uint64_t chunks = 0;         // total, without the over-read padding (4 chunks)
+    int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
+    uint32_t* meta = nullptr;    // (chunks + OVERREAD) * 64
+    double* val = nullptr;       // (chunks + OVERREAD) * 64
+    unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
+};
+
 // Device-resident finalised Csr<T>.
 struct bsm_csr {
     int dtype = BSM_F64;
@@ -166,19 +178,11 @@ struct bsm_csr {
     mutable int32_t* plan_seg = nullptr;
     mutable uint64_t plan_cols = 0;
     mutable bool plan_usable = false;
+    // cached row-block x column-panel copy (kernels_tiled.hip), same mutex
+    mutable bsm_tiled* tiled = nullptr;
+    mutable bool tiled_tried = false;
 };
 
-// Row-block x column-panel copy of a matrix (kernels_tiled.hip).
-struct bsm_tiled {
-    int device = 0;
-    uint64_t rows = 0, n_cols = 0, nnz = 0;
-    uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
-    uint64_t chunks = 0;         // total, without the over-read padding (4 chunks)
-    int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
-    uint32_t* meta = nullptr;    // (chunks + OVERREAD) * 64
-    double* val = nullptr;       // (chunks + OVERREAD) * 64
-    unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
-};
 
 namespace bsm {
 int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz);

@@ -204,7 +204,20 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
         // one thread at a time builds and launches with the cached plan (a
         // rebuild frees the old plan; hipFree waits for launches using it)
         std::lock_guard<std::mutex> plan_lock(a->plan_mu);
-        if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
+        if (!a->tiled_tried && !spmm_wants_split(a->dtype, k, a->max_row_len) &&
+            tiled_wanted(a->dtype, rows, a->cols, a->nnz, k, a->max_row_len)) {
+            // the row-block x column-panel copy (once per matrix; declined
+            // shapes or no memory for the copy fall back to the plans below)
+            a->tiled_tried = true;
+            bsm_tiled* t = nullptr;
+            const int rc = tiled_create(rows, a->cols, a->nnz, a->row_ptr, a->col,
+                                        static_cast<const double*>(a->vals), 0, &t, s);
+            if (rc == BSM_OK) a->tiled = t;
+            else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
+        }
+        if (a->tiled && k == 32 && a->dtype == BSM_F64) {
+            BSM_TRY(tiled_spmm(a->tiled, x_dev, y.p, row_nnz.as<int32_t>(), s));
+        } else if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
             if (a->plan_seg) (void)hipFree(a->plan_seg);
             a->plan_seg = nullptr;
             a->plan_cols = 0;
@@ -217,7 +230,9 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
             a->plan_cols = w;
             a->plan_usable = usable != 0;
         }
-        if (spmm_wants_split(a->dtype, k, a->max_row_len))
+        if (a->tiled && k == 32 && a->dtype == BSM_F64)
+            ;  // done above
+        else if (spmm_wants_split(a->dtype, k, a->max_row_len))
             BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, y.p,
                                         row_nnz.as<int32_t>(), s));
         else if (w && a->plan_usable)
@@ -437,6 +452,7 @@ void bsm_csr_free(bsm_csr* m) {
     if (m->col) (void)hipFree(m->col);
     if (m->vals) (void)hipFree(m->vals);
     if (m->plan_seg) (void)hipFree(m->plan_seg);
+    if (m->tiled) tiled_destroy(m->tiled);
     delete m;
 }
 
@@ -675,6 +691,13 @@ int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_
 }
 
 void bsm_tiled_destroy(bsm_tiled* t) { tiled_destroy(t); }
+
+int bsm_csr_tiled(const bsm_csr* m, int* in_use) {
+    BSM_REQUIRE(m && in_use, BSM_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lock(m->plan_mu);
+    *in_use = m->tiled ? 1 : 0;
+    return BSM_OK;
+}
 
 int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y, const int32_t* row_nnz,
                     int64_t* out_row_ptr, int32_t* out_col, void* out_vals, void* workspace,

@@ -336,7 +336,14 @@ def main():
     # block-cyclic row partition (equal rows = equal nnz: constant row length):
     # `chunks` rounds, each finished by its own SpMM launch and all-gathered
     # asynchronously while the next round computes (N > 1)
-    chunks = args.chunks if args.chunks else (1 if world == 1 else 4)
+    # one round per rank when the tiled copy serves the shape: its persistent
+    # grid wants every CU (an all-gather kernel beside it would hold some and
+    # defeat its batch pacing), so the all-gather follows the SpMM instead of
+    # overlapping a next round
+    lib0 = _lib.load()
+    tiled_shape = args.schedule != "panel" and k == 32 and bool(lib0.bsm_dev_tiled_wanted(
+        _lib.DTYPE_CODES[np.dtype(np.float64)], rows, n_cols, rows * (nnz_r or 1), k, nnz_r or 1))
+    chunks = args.chunks if args.chunks else (1 if world == 1 or tiled_shape else 4)
     cr, pieces = partition_rows_cyclic(rows, world, chunks)
     mine = pieces[rank]
     my_rows = sum(n for _, n in mine)

@@ -227,6 +227,9 @@ int bsm_dev_tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int
 int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* row_nnz,
                        void* stream);
 int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols);
+/* Whether bsm_csr_mul_dense has built (and uses) the tiled copy for this
+ * handle; diagnostic. */
+int bsm_csr_tiled(const bsm_csr* m, int* in_use);
 void bsm_tiled_destroy(bsm_tiled* t);
 /* Compaction of a dense result into the reference's output Csr (insert's
  * zero skip, sparse.rs:229): out_row_ptr (rows+1), out_col/out_vals with

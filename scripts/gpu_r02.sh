@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-2 GPU session: scripts/gpu_r02.sh TAG STEP...
-# STEP: tests | smoke | bench:<config>[:extra bench args] | prof:<config> | c5
+# STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>
+#       | pmc:<config>:<COUNTER> | c5
 # Every step runs under its own time limit; the session stops at the first
 # failing step (no retries).
 set -u
@@ -31,6 +32,10 @@ for step in "$@"; do
     prof:*) cfg=${step#prof:}
             run prof_$cfg 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${cfg}_$TAG -o run \
                 --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e || exit $? ;;
+    pmc:*) IFS=: read -r _ cfg ctr <<< "$step"
+           run pmc_${cfg}_${ctr} 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${cfg}_${ctr}_$TAG -o run \
+               --output-format csv -- python bench.py --config $cfg --steps 2 --warmup 0 --no-cpu-baseline \
+               --no-e2e || exit $? ;;
     c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -168,3 +168,35 @@ def test_tiled_c4_shape_block_matches_panelled(orc):
     ci, v = orc.gen_entries(1000, rp, n_cols, r0=row0 + sr, r1=row0 + sr + 2)
     erp, eci, ev = orc.mul_dense(2, n_cols, rp[row0 + sr:] - rp[row0 + sr], ci, v, orc.gen_x_cols(1001, n_cols, k))
     assert np.array_equal(y1[sr:sr + 2].reshape(-1).cpu().numpy().view(np.uint64), ev.view(np.uint64))
+
+
+def test_public_mul_dense_uses_tiled_copy(orc, monkeypatch):
+    """Csr.mul_dense (the reference API) builds the tiled copy once per matrix
+    when the library wants it (forced here for a small shape) and returns the
+    oracle's Csr bit for bit; with the copy disabled, the same Csr."""
+    import ctypes
+
+    from basic_sparse_matrix_amd import Csr, Dense
+
+    rows, n_cols, k = 20_000, 60_000, 32
+    rp, ci, v = orc.gen_csr(1000, rows, n_cols, orc.ROWLEN_UNIFORM, 150, 250)
+    x_cols = orc.gen_x_cols(1001, n_cols, k)
+    monkeypatch.setenv("BSM_SPMM_TILED", "2")
+    monkeypatch.setenv("BSM_TILED_WAVES", "64")
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    got = a.mul_dense(Dense.from_columns(x_cols))
+    used = ctypes.c_int(-1)
+    _lib.check(_lib.load().bsm_csr_tiled(a._device().handle, ctypes.byref(used)))
+    assert used.value == 1
+    got2 = a.mul_dense(Dense.from_columns(x_cols))  # cached copy
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    for g in (got, got2):
+        assert np.array_equal(np.asarray(g.row_index), erp)
+        assert np.array_equal(np.asarray(g.col_index), eci)
+        assert np.array_equal(np.asarray(g.v).view(np.uint64), ev.view(np.uint64))
+    monkeypatch.setenv("BSM_SPMM_TILED", "0")
+    b = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    ref = b.mul_dense(Dense.from_columns(x_cols))
+    _lib.check(_lib.load().bsm_csr_tiled(b._device().handle, ctypes.byref(used)))
+    assert used.value == 0
+    assert np.array_equal(np.asarray(ref.v).view(np.uint64), ev.view(np.uint64))
