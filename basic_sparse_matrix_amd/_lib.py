@@ -78,6 +78,7 @@ _u64p = ctypes.POINTER(ctypes.c_uint64)
 SIGNATURES = [
     ("bsm_api_version", _int, []),
     ("bsm_last_error", ctypes.c_char_p, []),
+    ("bsm_stage_times", _int, [_int, ctypes.POINTER(_int), ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     ("bsm_device_count", _int, [ctypes.POINTER(_int)]),
     ("bsm_set_device", _int, [_int]),
     ("bsm_csr_upload", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
@@ -139,6 +140,21 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+def stage_times() -> dict:
+    """{stage: device ms} of the last solve on this thread (bsm_stage_times)."""
+    lib = load()
+    n = ctypes.c_int(0)
+    check(lib.bsm_stage_times(0, ctypes.byref(n), None, None))
+    names = ctypes.create_string_buffer(32 * max(1, n.value))
+    ms = (ctypes.c_double * max(1, n.value))()
+    check(lib.bsm_stage_times(n.value, ctypes.byref(n), names, ms))
+    out = {}
+    for i in range(n.value):
+        key = names.raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
+        out[key] = out.get(key, 0.0) + ms[i]
+    return out
 
 
 def last_error() -> str:

@@ -18,6 +18,9 @@ namespace bsm {
 // ---------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 const char* last_error();
+// stage timer of the solver (bsm_stage_times): reset, then mark the end of each stage
+void stage_reset(hipStream_t s);
+void stage_mark(const char* name, hipStream_t s);
 
 #define BSM_HIP_TRY(expr)                                                                   \
     do {                                                                                    \

@@ -25,6 +25,39 @@ void set_error(const char* fmt, ...) {
 }
 const char* last_error() { return g_err.c_str(); }
 
+// Stage timer of the solver entry points (bsm_stage_times): each mark records
+// an event on the stream; stage i spans marks i-1 .. i.
+namespace {
+struct Stage {
+    std::string name;
+    hipEvent_t ev = nullptr;
+};
+thread_local std::vector<Stage> g_stages;
+void stage_clear() {
+    for (auto& st : g_stages)
+        if (st.ev) (void)hipEventDestroy(st.ev);
+    g_stages.clear();
+}
+}  // namespace
+
+void stage_reset(hipStream_t s) {
+    stage_clear();
+    stage_mark("start", s);
+}
+void stage_mark(const char* name, hipStream_t s) {
+    // marks outside a solve (cholesky_decomp alone) extend the last solve's
+    // list; it is bounded
+    if (g_stages.size() >= 64) return;
+    Stage st;
+    st.name = name;
+    if (hipEventCreate(&st.ev) != hipSuccess) return;
+    if (hipEventRecord(st.ev, s) != hipSuccess) {
+        (void)hipEventDestroy(st.ev);
+        return;
+    }
+    g_stages.push_back(st);
+}
+
 namespace {
 std::mutex g_stream_mu;
 hipStream_t g_streams[64] = {};
@@ -285,6 +318,20 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
 using namespace bsm;
 
 extern "C" {
+
+int bsm_stage_times(int max, int* n, char* names, double* ms) {
+    BSM_REQUIRE(n && (max <= 0 || (names && ms)), BSM_ERR_INVALID, "null argument");
+    const int have = g_stages.empty() ? 0 : (int)g_stages.size() - 1;
+    *n = have;
+    for (int i = 0; i < have && i < max; ++i) {
+        BSM_HIP_TRY(hipEventSynchronize(g_stages[i + 1].ev));
+        float t = 0.0f;
+        BSM_HIP_TRY(hipEventElapsedTime(&t, g_stages[i].ev, g_stages[i + 1].ev));
+        ms[i] = t;
+        snprintf(names + 32 * i, 32, "%s", g_stages[i + 1].name.c_str());
+    }
+    return BSM_OK;
+}
 
 int bsm_api_version(void) { return BSM_API_VERSION; }
 

@@ -2569,6 +2569,7 @@ int band_setup(const bsm_csr* a, Band& bd, hipStream_t s, int64_t bw_max) {
 template <typename T>
 int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     BSM_TRY(band_setup<T>(a, bd, s, 64 * 17 - TR));  // accumulators per row pair lane set
+    stage_mark("band_setup", s);
     if (bd.n == 0) return BSM_OK;
     const int64_t bw = bd.b, need = bw + TR;
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
@@ -2612,6 +2613,7 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s, tr);
     else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s, tr);
     BSM_TRY(rc);
+    stage_mark("cholesky", s);
     if (tracing && v4) {
         std::vector<unsigned long long> h(17);
         BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -2757,6 +2759,7 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
 template <typename T>
 int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     BSM_TRY(band_setup<T>(a, bd, s, (int64_t)1 << 16));
+    stage_mark("band_setup", s);
     const int64_t n = bd.n, nb64 = (n + 63) / 64, DM = (63 + bd.b) / 64 + 1;
     BSM_TRY(dinv.alloc((size_t)(nb64 > 0 ? nb64 : 1) * 4096 * sizeof(T)));
     if (n == 0) return BSM_OK;
@@ -2785,6 +2788,7 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
                                                panels);
     BSM_HIP_TRY(hipGetLastError());
+    stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid);
     g_blk_phase = "blk_chol sync";
     int h = 0;
@@ -2938,6 +2942,7 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
         BSM_REQUIRE(a->rows == n, BSM_ERR_PANIC,
                     "solve: b has %llu rows but A has %llu (index out of bounds in the reference)",
                     (unsigned long long)n, (unsigned long long)a->rows);
+        stage_reset(s);
         Band bd;
         BSM_TRY(band_factor<T>(a, bd, s));
         // the reference's forward pass divides by the LAST stored entry of
@@ -3000,9 +3005,12 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
                         "%.0f cycles each, %.0f of them waiting for y\n",
                         h[0] / nb, h[3] / nb, h[4] / nb, h[1] / nb, h[2] / nb, h[7], h[5] / hb, h[6] / hb);
             }
+            stage_mark("forward", s);
             BSM_TRY(launch_backward<T>(n, k, bd.b, bd.ld, bd.cb.as<T>(), yc.as<T>(), xc.as<T>(), s));
+            stage_mark("backward", s);
         }
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
+        stage_mark("copy_out", s);
         BSM_HIP_TRY(hipStreamSynchronize(s));
         return BSM_OK;
     };
@@ -3021,6 +3029,7 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
                     "solve: b has %llu rows but A has %llu (index out of bounds in the reference)",
                     (unsigned long long)n, (unsigned long long)a->rows);
         blk_watch_start();
+        stage_reset(s);
         g_blk_phase = "band setup";
         Band bd;
         DBuf dinv;
@@ -3051,6 +3060,7 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
             blk_prep<T><<<(unsigned)nb64, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), g.as<T>(), h.as<T>(),
                                                       mf.as<T>(), mb.as<T>());
             BSM_HIP_TRY(hipGetLastError());
+            stage_mark("blk_prep", s);
             int dev = 0, cus = 0, per_cu = 0;
             BSM_HIP_TRY(hipGetDevice(&dev));
             BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -3062,11 +3072,13 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
                                                             mf.as<T>(), bc.as<T>(), (int64_t)n, yp.as<T>(), ff,
                                                             tix, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
+            stage_mark("forward", s);
             blk_watchdog(s, "blk_trsv forward", nullptr, (long long)(nb64 * k), (long long)grid);
             blk_trsv<T, false><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), h.as<T>(),
                                                              mb.as<T>(), yp.as<T>(), (int64_t)NP, xp.as<T>(), fb,
                                                              tix + 1, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
+            stage_mark("backward", s);
             blk_watchdog(s, "blk_trsv backward", nullptr, (long long)(nb64 * k), (long long)grid);
             int hst = 0;
             g_blk_phase = "trsv sync";
@@ -3078,6 +3090,7 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
         }
         g_blk_phase = "unpack + final sync";
         BSM_TRY(from_colmajor(a->dtype, n, k, xc.p, x_dev, s));
+        stage_mark("copy_out", s);
         BSM_HIP_TRY(hipStreamSynchronize(s));
         g_blk_phase = "idle";
         blk_watch_stop();

@@ -567,6 +567,47 @@ __global__ __launch_bounds__(256) void spmv_rows(int64_t rows, const int64_t* __
 }
 
 // ---------------------------------------------------------------------------
+// SpMV (k = 1) for short rows (C2: 10 entries): one thread per row, the
+// row's entries and their x gathers all in flight at once (U per pass,
+// indices clamped into the row so every load is unconditional), then the
+// products added in storage order in a register: no LDS, no barrier, two
+// dependent memory round trips after the row bounds. Rows longer than U take
+// more passes (the wave runs to its longest row).
+// ---------------------------------------------------------------------------
+template <typename T, int U>
+__global__ __launch_bounds__(256) void spmv_thread(int64_t rows, const int64_t* __restrict__ rp,
+                                                   const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                   const T* __restrict__ x, T* __restrict__ y,
+                                                   int32_t* __restrict__ row_nnz, bool neg_init) {
+    using A = Arith<T>;
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int64_t a = rp[r], b = rp[r + 1];
+    T acc = neg_init ? A::neg_zero() : A::zero();
+    for (int64_t base = a; base < b; base += U) {
+        const int n = (int)(b - base < U ? b - base : U);
+        int32_t c[U];
+        T v[U];
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const int64_t e = base + (i < n ? i : n - 1);
+            c[i] = col[e];
+            v[i] = val[e];
+        }
+        T xv[U];
+#pragma unroll
+        for (int i = 0; i < U; ++i) xv[i] = x[c[i]];
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const T t = A::add(acc, A::mul(v[i], xv[i]));
+            acc = i < n ? t : acc;
+        }
+    }
+    y[r] = acc;
+    if (row_nnz) row_nnz[r] = A::nz(acc) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
 // Compaction of dense Y (rows x k, row-major) into the output Csr: entry
 // (r, j) is kept iff Y[r][j] != 0 (insert's zero skip, sparse.rs:229), in
 // ascending j, at out_rp[r] + (kept entries of row r before j).
@@ -816,7 +857,15 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
     if (k == 1 && nnz <= SPMV_ROWS_AVG * rows && !(sv && atoi(sv) == 1)) {
         const uint64_t blocks = (rows + 255) / 256;
         BSM_REQUIRE(blocks < (1ull << 31), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
-        spmv_rows<T, 16><<<(unsigned)blocks, 256, 0, s>>>((int64_t)rows, rp, col, vals, x, y, row_nnz, neg_init);
+        const int64_t r = (int64_t)rows;
+        if (sv && atoi(sv) == 2)  // the workgroup-chunk version (A/B)
+            spmv_rows<T, 16><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (nnz <= 4 * rows)
+            spmv_thread<T, 4><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (nnz <= 8 * rows)
+            spmv_thread<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else
+            spmv_thread<T, 12><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     }

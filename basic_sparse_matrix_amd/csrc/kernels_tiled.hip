@@ -48,7 +48,7 @@ constexpr int CHUNK = 64;        // entries per chunk = 16 quads x 4 lane groups
 constexpr int PHASES = 6;        // pipeline unroll; task chunk counts are multiples of it
 constexpr int OVERREAD = 4;      // chunks the pipeline reads past a task's end
 constexpr uint32_t DONE = 0xffffffffu;
-constexpr uint32_t RW_MAX = 144;  // 4 waves x (RW+1) rows x 256 B <= 160 KiB of LDS
+constexpr uint32_t RW_MAX = 155;  // 4 waves x (RW+1) rows x 256 B <= 160 KiB of LDS
 constexpr uint32_t PSHIFT = 12;   // panel = 4096 columns = 1 MiB of X (C4 sweep: 2^10..2^12 flat, 2^13 +12 %, 2^14 +42 %)
 constexpr uint32_t PACE_PCT = 3;  // chunk budget per panel over the task's mean (padding ~ this; C4: 2 % +19 %, 6 % +2 %)
 

@@ -66,7 +66,9 @@ def kernel_label(rows, nnz, k, panel_cols, tiled=False):
     if tiled:
         return "spmm_tiled_k32"
     if k == 1:
-        return "spmv_rows<double,16>" if nnz <= 12 * rows else "spmv_stream<double,4>"
+        if nnz <= 12 * rows:
+            return f"spmv_thread<double,{4 if nnz <= 4 * rows else 8 if nnz <= 8 * rows else 12}>"
+        return "spmv_stream<double,4>"
     if k == 32:
         if nnz <= 24 * rows and not panel_cols:
             return "spmm_k32_f64_rows4<4>"

@@ -71,6 +71,10 @@ typedef struct bsm_csr bsm_csr;
 int bsm_api_version(void);
 /* Thread-local description of the last failure on this thread. */
 const char* bsm_last_error(void);
+/* Device time of the stages of the last bsm_solve / bsm_solve_blocked on
+ * this thread (HIP events on its stream): *n stages; the first min(max, *n)
+ * names (32 chars each, NUL-terminated) and durations in ms. Diagnostic. */
+int bsm_stage_times(int max, int* n, char* names, double* ms);
 int bsm_device_count(int* n);
 /* Select the device used by subsequent calls on this thread. */
 int bsm_set_device(int ordinal);

@@ -1,9 +1,26 @@
 #!/usr/bin/env python3
-"""C5: 2D 5-point Poisson (g x g grid, natural ordering), solve(A, b) on the
-GPU through the reference API (lib.rs:11-24). Prints wall time and accuracy;
-run under `rocprofv3 --kernel-trace --stats` for the per-kernel breakdown
-(band_chol / band_forward / band_backward)."""
+"""C5 (north_star config 5): 2D 5-point Poisson on a g x g grid (natural
+ordering, N = g^2, band b = g), b = A x_true, solve(A, b) on the GPU through
+the reference API (lib.rs:11-24): cholesky_decomp -> transpose -> forward ->
+backward substitution. Prints ONE JSON line per order (reference = bit-exact
+operation order; blocked = reassociated, within 1e-6 on f64) with
+
+* wall time through the public API (host b in, host x out) and the device
+  time of every stage (HIP events on the library's stream, bsm_stage_times);
+* the factor's flop roofline (N b^2 flops, the band Cholesky's multiply-add
+  pairs x 2, against the 78.6 TF/s f64 peak of MI355X_MICROARCH.md) and each
+  triangular solve's byte roofline (the band of L, 8 N (b+1) bytes, read
+  once, against 8 TB/s);
+* the CPU baseline: the oracle's band restatement of the same solve (the
+  reference's order, one thread; the literal O(N^4) reference loops are out
+  of reach beyond N ~ 256) timed here at g = 250 and g = 500 and extrapolated
+  to g = 1000 by the N b^2 = g^4 work law (labelled as extrapolated);
+* the error of x against x_true (and, for the reference order, bit-equality
+  with the committed full-size oracle fixture, tests/golden/c5_poisson_1000.json).
+"""
 import argparse
+import hashlib
+import json
 import os
 import sys
 import time
@@ -12,28 +29,114 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
-from basic_sparse_matrix_amd import Csr, Dense, solve  # noqa: E402
-from oracle import pyoracle as orc  # noqa: E402  (input generation + check only)
+from basic_sparse_matrix_amd import Csr, Dense, _lib, solve  # noqa: E402
+from oracle import pyoracle as orc  # noqa: E402  (inputs, the CPU baseline and the check only)
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--g", type=int, default=1000)
-ap.add_argument("--dtype", default="f64")
-ap.add_argument("--reps", type=int, default=1)
-ap.add_argument("--order", default="reference", choices=["reference", "blocked"])
-args = ap.parse_args()
-dt = np.float64 if args.dtype == "f64" else np.float32
-g = args.g
-n = g * g
-rp, ci, v = orc.poisson2d(g)
-x_true = orc.gen_x_cols(1002, n, 1)[0]
-rows = np.repeat(np.arange(n), np.diff(rp.astype(np.int64)))
-b = np.zeros(n)
-np.add.at(b, rows, v * x_true[ci.astype(np.int64)])
-A = Csr.from_csr_arrays((n, n), rp, ci, v.astype(dt))
-B = Dense.from_columns([b.astype(dt)])
-for r in range(args.reps):
-    t0 = time.perf_counter()
-    x = solve(A, B, order=args.order).get_col(0)
-    t = time.perf_counter() - t0
-    rel = np.linalg.norm(x.astype(np.float64) - x_true) / np.linalg.norm(x_true)
-    print(f"C5 g={g} N={n} {args.dtype} order={args.order}: solve wall {t:.3f} s (incl. H2D/D2H), rel err vs x_true {rel:.3e}", flush=True)
+F64_PEAK_TFS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+
+def system(g, dt):
+    rp, ci, v = orc.poisson2d(g)
+    n = g * g
+    x_true = orc.gen_x_cols(1002, n, 1)[0]
+    rows = np.repeat(np.arange(n), np.diff(rp.astype(np.int64)))
+    b = np.zeros(n)
+    np.add.at(b, rows, v * x_true[ci.astype(np.int64)])
+    return rp, ci, v.astype(dt), b.astype(dt), x_true
+
+
+def cpu_baseline(sizes=(250, 500), target=1000):
+    pts = {}
+    for g in sizes:
+        rp, ci, v, b, _ = system(g, np.float64)
+        t0 = time.perf_counter()
+        orc.solve(g * g, rp, ci, v, [b], band=True)
+        pts[g] = time.perf_counter() - t0
+    g_hi = max(sizes)
+    est = pts[g_hi] * (target / g_hi) ** 4
+    return {
+        "value_s": round(est, 2),
+        "unit": "s per solve",
+        "cores": 1,
+        "kind": "port",
+        "measured_s": {f"{g}x{g}": round(t, 3) for g, t in pts.items()},
+        "sample": f"oracle band restatement of solve (lib.rs:11-24, reference operation order, C, -O2 "
+                  f"-ffp-contract=off, 1 thread) measured at {', '.join(f'{g}^2' for g in sizes)}; "
+                  f"{target}^2 EXTRAPOLATED from {g_hi}^2 by the g^4 (= N b^2) work law",
+        "host_cpus": os.cpu_count(),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--g", type=int, default=1000)
+    ap.add_argument("--dtype", default="f64", choices=("f64", "f32"))
+    ap.add_argument("--reps", type=int, default=2, help="timed solves per order (after one warm-up)")
+    ap.add_argument("--orders", default="reference,blocked")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    dt = np.float64 if args.dtype == "f64" else np.float32
+    g = args.g
+    n = g * g
+    rp, ci, v, b, x_true = system(g, dt)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    B = Dense.from_columns([b])
+    fixture = None
+    fx_path = os.path.join(ROOT, "tests", "golden", f"c5_poisson_{g}.json")
+    if os.path.exists(fx_path) and args.dtype == "f64":
+        with open(fx_path) as f:
+            fixture = json.load(f)
+    cpu = None if args.no_cpu_baseline else cpu_baseline()
+    es = np.dtype(dt).itemsize
+    flops = float(n) * g * g  # sum over rows of b^2 / 2 multiply-add pairs, x 2
+    band_bytes = float(es) * n * (g + 1)
+    for order in args.orders.split(","):
+        solve(A, B, order=order)  # warm-up (first call uploads A and builds nothing else)
+        walls, stages = [], []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            x = solve(A, B, order=order).get_col(0)
+            walls.append(time.perf_counter() - t0)
+            stages.append(_lib.stage_times())
+        st = {k: round(float(np.mean([s[k] for s in stages])), 3) for k in stages[-1]}
+        rel = float(np.linalg.norm(x.astype(np.float64) - x_true) / np.linalg.norm(x_true))
+        line = {
+            "metric": "C5 solve: device ms per stage, flop/byte roofline per kernel",
+            "config": {"workload": f"c5: 2D 5-point Poisson {g}x{g} (N={n:,}, band {g}), natural ordering, "
+                                   f"b = A x_true (seed 1002), 1 RHS", "dtype": args.dtype, "order": order},
+            "wall_ms": round(1e3 * float(np.median(walls)), 2),
+            "stages_ms": st,
+            "device_ms_total": round(sum(st.values()), 2),
+            "factor": {"kernel": "band_chol4 (reference order)" if order == "reference" else "blk_chol (blocked)",
+                       "flops": flops, "ms": st.get("cholesky"),
+                       "achieved_TFs": round(flops / (st["cholesky"] * 1e-3) / 1e12, 3) if st.get("cholesky") else None,
+                       "peak_TFs": F64_PEAK_TFS,
+                       "frac": round(flops / (st["cholesky"] * 1e-3) / 1e12 / F64_PEAK_TFS, 5)
+                       if st.get("cholesky") else None},
+            "forward": {"bytes": band_bytes, "ms": st.get("forward"),
+                        "achieved_GBs": round(band_bytes / (st["forward"] * 1e-3) / 1e9, 1) if st.get("forward") else None,
+                        "peak_GBs": HBM_PEAK_GBS,
+                        "frac": round(band_bytes / (st["forward"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                        if st.get("forward") else None},
+            "backward": {"bytes": band_bytes, "ms": st.get("backward"),
+                         "achieved_GBs": round(band_bytes / (st["backward"] * 1e-3) / 1e9, 1) if st.get("backward") else None,
+                         "peak_GBs": HBM_PEAK_GBS,
+                         "frac": round(band_bytes / (st["backward"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                         if st.get("backward") else None},
+            "rel_err_vs_x_true": rel,
+            "cpu_baseline": cpu,
+            "vs_cpu": round(cpu["value_s"] / (float(np.median(walls))), 1) if cpu else None,
+        }
+        if fixture is not None:
+            h = hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).view(np.uint64).tobytes()).hexdigest()
+            line["x_bits_equal_oracle_fixture"] = h == fixture["sha256_x_f64_bits"]
+            ex = np.array([int(t, 16) for t in fixture["x_sample_bits"]], dtype=np.uint64).view(np.float64)
+            xs = x[::fixture["x_stride"]][:ex.size].astype(np.float64)
+            line["max_rel_dev_vs_oracle_x_sample"] = float(np.max(np.abs(xs - ex) / np.abs(ex)))
+            line["oracle_fixture_cpu_s"] = fixture.get("cpu_seconds")
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
