@@ -567,6 +567,59 @@ __global__ __launch_bounds__(256) void spmv_rows(int64_t rows, const int64_t* __
 }
 
 // ---------------------------------------------------------------------------
+// SpMV (k = 1), short rows, one WAVE per 64 rows: the rows' entries loaded
+// coalesced (lane l takes entry e0 + l + 64 i), their products written to the
+// wave's own LDS slice, then lane r adds row r's products in storage order.
+// LDS operations of one wave complete in order, so no barrier is needed and
+// the waves of a workgroup never wait for each other.
+// ---------------------------------------------------------------------------
+template <typename T, int ITEMS>
+__global__ __launch_bounds__(256) void spmv_wave(int64_t rows, const int64_t* __restrict__ rp,
+                                                 const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                 const T* __restrict__ x, T* __restrict__ y,
+                                                 int32_t* __restrict__ row_nnz, bool neg_init) {
+    using A = Arith<T>;
+    constexpr int CAP = WAVE * ITEMS;
+    __shared__ T prod_all[4][CAP];
+    T* prod = prod_all[threadIdx.x / WAVE];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + threadIdx.x / WAVE) * WAVE;
+    if (r0 >= rows) return;
+    const int64_t r1 = r0 + WAVE < rows ? r0 + WAVE : rows;
+    const int64_t rr = r0 + lane;
+    const bool live = rr < r1;
+    const int64_t e0 = rp[r0], e1 = rp[r1];
+    const int64_t ra = live ? rp[rr] : e1, rb = live ? rp[rr + 1] : e1;
+    T acc = neg_init ? A::neg_zero() : A::zero();
+    for (int64_t base = e0; base < e1; base += CAP) {
+        const int64_t n = e1 - base < CAP ? e1 - base : CAP;
+        const int nit = (int)((n + WAVE - 1) / WAVE);
+        int32_t c[ITEMS];
+        T v[ITEMS];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit) {
+                const int64_t e = base + min<int64_t>(it * WAVE + lane, n - 1);
+                c[it] = col[e];
+                v[it] = val[e];
+            }
+        T xv[ITEMS];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit) xv[it] = x[c[it]];
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it)
+            if (it < nit && it * WAVE + lane < n) prod[it * WAVE + lane] = A::mul(v[it], xv[it]);
+        const int64_t a = ra > base ? ra : base, b = rb < base + n ? rb : base + n;
+        for (int64_t i = a; i < b; ++i) acc = A::add(acc, prod[i - base]);
+    }
+    if (live) {
+        y[rr] = acc;
+        if (row_nnz) row_nnz[rr] = A::nz(acc) ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // SpMV (k = 1) for short rows (C2: 10 entries): one thread per row, the
 // row's entries and their x gathers all in flight at once (U per pass,
 // indices clamped into the row so every load is unconditional), then the
@@ -858,14 +911,19 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
         const uint64_t blocks = (rows + 255) / 256;
         BSM_REQUIRE(blocks < (1ull << 31), BSM_ERR_UNSUPPORTED, "too many rows for one launch");
         const int64_t r = (int64_t)rows;
-        if (sv && atoi(sv) == 2)  // the workgroup-chunk version (A/B)
+        const int svv = sv ? atoi(sv) : 0;
+        if (svv == 2)  // the workgroup-chunk version (A/B)
             spmv_rows<T, 16><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
-        else if (nnz <= 4 * rows)
-            spmv_thread<T, 4><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
-        else if (nnz <= 8 * rows)
-            spmv_thread<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
-        else
+        else if (svv == 3)
+            spmv_wave<T, 16><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (svv == 4)
+            spmv_wave<T, 12><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (svv == 5)
+            spmv_wave<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (svv == 6)
             spmv_thread<T, 12><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else  // default (C2: 111 us against 117-167 for the others, scripts/perf/spmv_variants.py)
+            spmv_wave<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     }

@@ -67,7 +67,7 @@ def kernel_label(rows, nnz, k, panel_cols, tiled=False):
         return "spmm_tiled_k32"
     if k == 1:
         if nnz <= 12 * rows:
-            return f"spmv_thread<double,{4 if nnz <= 4 * rows else 8 if nnz <= 8 * rows else 12}>"
+            return "spmv_wave<double,8>"
         return "spmv_stream<double,4>"
     if k == 32:
         if nnz <= 24 * rows and not panel_cols:
