@@ -111,7 +111,7 @@ SIGNATURES = [
     ("bsm_dev_spmm_plan", _int, [_u64, _u64, _vp, _vp, _u64, _vp, ctypes.POINTER(_int), _vp]),
     ("bsm_dev_spmm_panelled", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
     ("bsm_dev_tiled_wanted", _int, [_int, _u64, _u64, _u64, _u64, _u64]),
-    ("bsm_dev_tiled_create", _int, [_u64, _u64, _u64, _vp, _vp, _vp, _int, ctypes.POINTER(_vp), _vp]),
+    ("bsm_dev_tiled_create", _int, [_u64, _u64, _u64, _vp, _vp, _vp, _u64, _int, ctypes.POINTER(_vp), _vp]),
     ("bsm_dev_spmm_tiled", _int, [_vp, _vp, _vp, _vp, _vp]),
     ("bsm_tiled_info", _int, [_vp, _u64p, _u64p, _u64p]),
     ("bsm_tiled_destroy", None, [_vp]),

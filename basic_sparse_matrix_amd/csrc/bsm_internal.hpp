@@ -154,12 +154,15 @@ struct DBuf {
 // Row-block x column-panel copy of a matrix (kernels_tiled.hip).
 struct bsm_tiled {
     int device = 0;
+    uint64_t k = 32;             // right-hand columns the copy serves (32 or 1)
+    uint32_t overread = 4;       // chunks of dummy padding past the last task
+    uint32_t stage = 4;          // k = 1: chunks per pipeline stage
     uint64_t rows = 0, n_cols = 0, nnz = 0;
     uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
-    uint64_t chunks = 0;         // total, without the over-read padding (4 chunks)
+    uint64_t chunks = 0;         // total, without the over-read padding
     int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
-    uint32_t* meta = nullptr;    // (chunks + OVERREAD) * 64
-    double* val = nullptr;       // (chunks + OVERREAD) * 64
+    uint32_t* meta = nullptr;    // (chunks + overread) * 64
+    double* val = nullptr;       // (chunks + overread) * 64
     unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
 };
 
@@ -222,8 +225,8 @@ int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const
 // row-block x column-panel schedule (kernels_tiled.hip)
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len);
 int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, int flags, bsm_tiled** out, hipStream_t s);  // synchronous
-int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, hipStream_t s);
+                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s);  // synchronous
+int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, bool neg_init, hipStream_t s);
 void tiled_destroy(bsm_tiled* t);
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
                      int32_t* out_col, void* out_vals, hipStream_t s);

@@ -244,12 +244,12 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
             a->tiled_tried = true;
             bsm_tiled* t = nullptr;
             const int rc = tiled_create(rows, a->cols, a->nnz, a->row_ptr, a->col,
-                                        static_cast<const double*>(a->vals), 0, &t, s);
+                                        static_cast<const double*>(a->vals), k, 0, &t, s);
             if (rc == BSM_OK) a->tiled = t;
             else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
         }
-        if (a->tiled && k == 32 && a->dtype == BSM_F64) {
-            BSM_TRY(tiled_spmm(a->tiled, x_dev, y.p, row_nnz.as<int32_t>(), s));
+        if (a->tiled && a->tiled->k == k) {
+            BSM_TRY(tiled_spmm(a->tiled, x_dev, y.p, row_nnz.as<int32_t>(), false, s));
         } else if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
             if (a->plan_seg) (void)hipFree(a->plan_seg);
             a->plan_seg = nullptr;
@@ -263,7 +263,7 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
             a->plan_cols = w;
             a->plan_usable = usable != 0;
         }
-        if (a->tiled && k == 32 && a->dtype == BSM_F64)
+        if (a->tiled && a->tiled->k == k)
             ;  // done above
         else if (spmm_wants_split(a->dtype, k, a->max_row_len))
             BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, y.p,
@@ -720,17 +720,18 @@ int bsm_dev_tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz
 }
 
 int bsm_dev_tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* row_ptr,
-                         const int32_t* col, const double* vals, int flags, bsm_tiled** out, void* stream) {
-    return tiled_create(rows, n_cols, nnz, row_ptr, col, vals, flags, out, static_cast<hipStream_t>(stream));
+                         const int32_t* col, const double* vals, uint64_t k, int flags, bsm_tiled** out,
+                         void* stream) {
+    return tiled_create(rows, n_cols, nnz, row_ptr, col, vals, k, flags, out, static_cast<hipStream_t>(stream));
 }
 
 int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* row_nnz, void* stream) {
-    return tiled_spmm(t, x, y, row_nnz, static_cast<hipStream_t>(stream));
+    return tiled_spmm(t, x, y, row_nnz, false, static_cast<hipStream_t>(stream));
 }
 
 int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols) {
     BSM_REQUIRE(t, BSM_ERR_INVALID, "null argument");
-    const uint64_t n = (t->chunks + 4) * 64;
+    const uint64_t n = (t->chunks + t->overread) * 64;
     if (bytes) *bytes = n * 12 + ((uint64_t)t->nw * t->nb + 1) * 8;
     if (slots) *slots = t->chunks * 64;
     if (panel_cols) *panel_cols = 1ull << t->pshift;

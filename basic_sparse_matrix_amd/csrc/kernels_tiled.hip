@@ -37,6 +37,7 @@
 #include "bsm_internal.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 
@@ -65,9 +66,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // layout builder: one wave per task (gw, b). COUNT pass writes the task's
 // chunk count (a multiple of PHASES); WRITE pass fills its chunks from offs.
 // ---------------------------------------------------------------------------
-template <bool WRITE>
-__global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_cols, double pace,
-                                                    const int64_t* __restrict__ rp,
+template <bool WRITE, int SLOTS>
+__global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_cols, double pace, uint32_t rbits,
+                                                    uint32_t pad, const int64_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
                                                     const double* __restrict__ vals, uint32_t nw,
                                                     uint32_t rpw, uint32_t nb, uint32_t rw, uint32_t pshift,
@@ -81,10 +82,10 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
     const uint64_t w0 = gw * rpw;
     const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
     const uint64_t r0 = w0 + b * rw;
-    int64_t cur[3], end[3];
-    uint32_t h[3];
+    int64_t cur[SLOTS], end[SLOTS];
+    uint32_t h[SLOTS];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < SLOTS; ++j) {
         const uint32_t s = lane + WAVE * j;
         const bool live = s < rw && r0 + s < wend;
         cur[j] = live ? rp[r0 + s] : 0;
@@ -101,48 +102,48 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
     int64_t c = WRITE ? offs[task] : 0;
     int64_t n = 0;
     for (;;) {
-        bool sel[3] = {false, false, false};
-        int pos[3] = {0, 0, 0};
+        bool sel[SLOTS];
+        int pos[SLOTS];
+#pragma unroll
+        for (int j = 0; j < SLOTS; ++j) {
+            sel[j] = false;
+            pos[j] = 0;
+        }
         int taken = 0;
         const double pm = (double)n * inv_r;
         const uint32_t pmax = pm >= 4.0e9 ? DONE - 1 : (uint32_t)pm;
         bool done = false;
         while (taken < CHUNK) {  // the lowest panels first, ties by row
-            uint32_t m = min(min(sel[0] ? DONE : h[0], sel[1] ? DONE : h[1]), sel[2] ? DONE : h[2]);
+            uint32_t m = DONE;
+#pragma unroll
+            for (int j = 0; j < SLOTS; ++j) m = min(m, sel[j] ? DONE : h[j]);
             m = wave_min_u32(m);
             if (m == DONE) {
                 done = taken == 0;
                 break;
             }
             if (m > pmax) break;  // ahead of the pace: the rest of the chunk is padding
-            uint64_t bal[3];
-            int cnt[3];
+            int before = 0;  // candidates in the slots before j (slot order = row order)
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                bal[j] = __ballot(!sel[j] && h[j] == m);
-                cnt[j] = __popcll(bal[j]);
-            }
-            const int take = min(cnt[0] + cnt[1] + cnt[2], CHUNK - taken);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                if (!sel[j] && h[j] == m) {
-                    const int rank = (j > 0 ? cnt[0] : 0) + (j > 1 ? cnt[1] : 0) +
-                                     __popcll(bal[j] & lanemask_lt(lane));
-                    if (rank < take) {
-                        sel[j] = true;
-                        pos[j] = taken + rank;
-                    }
+            for (int j = 0; j < SLOTS; ++j) {
+                const bool cand = !sel[j] && h[j] == m;
+                const uint64_t bal = __ballot(cand);
+                const int rank = before + __popcll(bal & lanemask_lt(lane));
+                if (cand && taken + rank < CHUNK) {
+                    sel[j] = true;
+                    pos[j] = taken + rank;
                 }
+                before += __popcll(bal);
             }
-            taken += take;
+            taken = min(taken + before, CHUNK);
         }
         if (done) break;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < SLOTS; ++j) {
             if (sel[j]) {
                 const int64_t e = cur[j];
                 if (WRITE) {
-                    meta[c * CHUNK + pos[j]] = ((uint32_t)col[e] << 8) | (uint32_t)(lane + WAVE * j);
+                    meta[c * CHUNK + pos[j]] = ((uint32_t)col[e] << rbits) | (uint32_t)(lane + WAVE * j);
                     val[c * CHUNK + pos[j]] = vals[e];
                 }
                 cur[j] = e + 1;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
         ++c;
         ++n;
     }
-    const int64_t padded = (n + PHASES - 1) / PHASES * PHASES;
+    const int64_t padded = (n + pad - 1) / pad * pad;
     if (WRITE) {
         for (int64_t p = n; p < padded; ++p, ++c) {
             meta[c * CHUNK + lane] = rw;
@@ -296,6 +297,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
 }
 
+// ---------------------------------------------------------------------------
+// k = 1 (SpMV, C2's shape): the same copy with RW up to 2047 rows per wave (Y
+// is one double per row: 4 waves x 2048 x 8 B of LDS) and meta = col << 11 |
+// row, so an XCD holds ~125k rows and an X panel of 2 MiB (2^18 columns) is
+// re-read from L2 about 20 times per 128-B line. Lane l takes entry l of a
+// chunk; eight chunks make a stage; three stages are in flight (indices two
+// stages ahead, gathers one ahead). The 64 rows of a chunk are distinct, so
+// a chunk's LDS read-add-writes are one instruction each; the chunks of a
+// stage go in order.
+// ---------------------------------------------------------------------------
+constexpr int K1_STAGE_DEFAULT = 4;          // chunks per stage (4 or 8)
+constexpr uint32_t K1_RBITS = 11;
+constexpr uint32_t K1_RW_MAX = (1u << K1_RBITS) - 1;
+constexpr uint32_t K1_PSHIFT = 18;           // panel = 2^18 columns = 2 MiB of X
+constexpr uint32_t K1_WAVES_PER_CU = 4;      // one workgroup per CU (C2: 59 us against 69 at 12)
+
+template <int ST>
+struct Stage1 {
+    uint32_t m[ST];
+    double v[ST];
+    double x[ST];
+};
+template <int ST>
+__device__ __forceinline__ void k1_load(Stage1<ST>& st, const uint32_t* __restrict__ meta,
+                                        const double* __restrict__ val, int64_t c, int lane) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j) {
+        st.m[j] = meta[(c + j) * CHUNK + lane];
+        st.v[j] = val[(c + j) * CHUNK + lane];
+    }
+}
+template <int ST>
+__device__ __forceinline__ void k1_gather(Stage1<ST>& st, const double* __restrict__ X) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j) st.x[j] = X[st.m[j] >> K1_RBITS];
+}
+template <int ST>
+__device__ __forceinline__ void k1_sum(const Stage1<ST>& st, double* yl) {
+#pragma unroll
+    for (int j = 0; j < ST; ++j) {
+        double* yp = yl + (st.m[j] & K1_RW_MAX);
+        *yp = __dadd_rn(*yp, __dmul_rn(st.v[j], st.x[j]));
+    }
+}
+
+template <int K1_STAGE>
+__global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw,
+                                                     const int64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ meta,
+                                                     const double* __restrict__ val, const double* __restrict__ X,
+                                                     double* __restrict__ Y, int32_t* __restrict__ row_nnz,
+                                                     unsigned* bar, bool neg_init) {
+    extern __shared__ double y1lds[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = threadIdx.x / WAVE;
+    double* yl = y1lds + (size_t)wave * (rw + 1);
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+    const uint64_t w0 = gw * rpw;
+    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
+    const double init = neg_init ? -0.0 : 0.0;
+    bool sync = bar != nullptr;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t r0 = w0 + (uint64_t)b * rw;
+        if (r0 >= wend) {
+            if (sync) batch_arrive(bar, nb - b, lane);
+            break;
+        }
+        if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane);
+        const int nr = (int)min<uint64_t>(rw, wend - r0);
+        for (int r = lane; r < nr; r += WAVE) yl[r] = init;
+        const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
+        int64_t i = c0;
+        if (c1 - c0 >= 3 * K1_STAGE) {  // whole groups of three stages, pipelined
+            constexpr int K1_GROUP = 3 * K1_STAGE;
+            Stage1<K1_STAGE> S0, S1, S2;
+            k1_load(S0, meta, val, c0, lane);
+            k1_load(S1, meta, val, c0 + K1_STAGE, lane);
+            k1_gather(S0, X);
+            for (; i + K1_GROUP <= c1; i += K1_GROUP) {
+                k1_load(S2, meta, val, i + 2 * K1_STAGE, lane);
+                k1_gather(S1, X);
+                __builtin_amdgcn_sched_barrier(0);
+                k1_sum(S0, yl);
+                __builtin_amdgcn_sched_barrier(0);
+                k1_load(S0, meta, val, i + 3 * K1_STAGE, lane);
+                k1_gather(S2, X);
+                __builtin_amdgcn_sched_barrier(0);
+                k1_sum(S1, yl);
+                __builtin_amdgcn_sched_barrier(0);
+                k1_load(S1, meta, val, i + 4 * K1_STAGE, lane);
+                k1_gather(S0, X);
+                __builtin_amdgcn_sched_barrier(0);
+                k1_sum(S2, yl);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        for (; i < c1; ++i) {  // the task's last chunks, one at a time
+            const uint32_t m = meta[i * CHUNK + lane];
+            const double v = val[i * CHUNK + lane];
+            const double xv = X[m >> K1_RBITS];
+            double* yp = yl + (m & K1_RW_MAX);
+            *yp = __dadd_rn(*yp, __dmul_rn(v, xv));
+        }
+        for (int r = lane; r < nr; r += WAVE) {
+            const double y = yl[r];
+            Y[r0 + r] = y;
+            if (row_nnz) row_nnz[r0 + r] = y != 0.0 ? 1 : 0;
+        }
+        if (sync) batch_arrive(bar, 1, lane);
+    }
+}
+
 uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* e = getenv(name);
     return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
@@ -303,35 +416,46 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 
 }  // namespace
 
-// Shape test: f64, k = 32, X beyond the Infinity Cache, columns < 2^24, rows
-// at most a few times the mean length (a long row serialises its chunks).
+// Shape test. k = 32: f64, X beyond 1 GiB (the Infinity Cache holds less),
+// columns < 2^24. k = 1: f64, X beyond one XCD's 4 MiB L2, columns < 2^21.
+// Both: rows at most a few times their mean length (a long row serialises
+// its chunks, one entry per chunk).
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len) {
+    const bool shape = dtype == BSM_F64 && rows > 0 && nnz > 0 &&
+                       ((k == 32 && n_cols < (1u << 24)) || (k == 1 && n_cols < (1u << (32 - K1_RBITS))));
     if (const char* e = getenv("BSM_SPMM_TILED")) {
         if (atoi(e) == 0) return false;
-        if (atoi(e) == 2) return dtype == BSM_F64 && k == 32 && n_cols < (1u << 24) && rows > 0 && nnz > 0;
+        if (atoi(e) == 2) return shape;
     }
-    if (dtype != BSM_F64 || k != 32 || n_cols >= (1u << 24) || rows == 0 || nnz == 0) return false;
+    if (!shape) return false;
     const uint64_t x_bytes = n_cols * k * sizeof(double);
-    if (x_bytes <= (1ull << 30)) return false;
+    if (x_bytes <= (k == 32 ? (1ull << 30) : (4ull << 20))) return false;
     const uint64_t mean = (nnz + rows - 1) / rows;
     return max_row_len <= 2 * mean + 256;
 }
 
 int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, int flags, bsm_tiled** out, hipStream_t s) {
+                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s) {
     BSM_REQUIRE(out && rp && (nnz == 0 || (col && vals)), BSM_ERR_INVALID, "tiled: null argument");
-    BSM_REQUIRE(n_cols < (1u << 24), BSM_ERR_UNSUPPORTED, "tiled: columns must be < 2^24");
+    BSM_REQUIRE(k == 32 || k == 1, BSM_ERR_UNSUPPORTED, "tiled: k must be 32 or 1");
+    const uint32_t rbits = k == 1 ? K1_RBITS : 8;
+    BSM_REQUIRE(n_cols < (1ull << (32 - rbits)), BSM_ERR_UNSUPPORTED, "tiled: columns must be < 2^%u",
+                32 - rbits);
     *out = nullptr;
     int dev = 0;
     BSM_TRY(current_device(&dev));
     int cus = 0;
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const uint32_t nw = env_u32("BSM_TILED_WAVES", 4u * (uint32_t)cus);
-    uint32_t rw_max = env_u32("BSM_TILED_RW", RW_MAX);
-    rw_max = rw_max < 8u ? 8u : (rw_max > RW_MAX ? RW_MAX : rw_max);
-    const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", PSHIFT);
+    const uint32_t nw = env_u32("BSM_TILED_WAVES", (k == 1 ? K1_WAVES_PER_CU : 4u) * (uint32_t)cus);
+    const uint32_t k1_stage = env_u32("BSM_TILED_K1_STAGE", K1_STAGE_DEFAULT) == 8 ? 8u : 4u;
+    const uint32_t rw_cap = k == 1 ? K1_RW_MAX : RW_MAX;
+    uint32_t rw_max = env_u32("BSM_TILED_RW", rw_cap);
+    rw_max = rw_max < 8u ? 8u : (rw_max > rw_cap ? rw_cap : rw_max);
+    const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", k == 1 ? K1_PSHIFT : PSHIFT);
     const double pace = 1.0 + env_u32("BSM_TILED_PACE_PCT", PACE_PCT) / 100.0;
-    BSM_REQUIRE(nw >= 4 && nw % 4 == 0 && pshift < 24, BSM_ERR_INVALID, "tiled: bad geometry");
+    const uint32_t pad = k == 1 ? 1u : PHASES;  // k = 1 runs a task's tail chunks unpipelined
+    const uint32_t overread = k == 1 ? 2 * k1_stage : OVERREAD;
+    BSM_REQUIRE(nw >= 4 && nw % 4 == 0 && pshift < 32, BSM_ERR_INVALID, "tiled: bad geometry");
     const uint64_t rpw64 = (rows + nw - 1) / nw;
     BSM_REQUIRE(rpw64 < (1ull << 31), BSM_ERR_UNSUPPORTED, "tiled: too many rows per wave");
     const uint32_t rpw = rpw64 ? (uint32_t)rpw64 : 1u;
@@ -343,9 +467,18 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     BSM_TRY(counts.alloc(tasks * sizeof(int32_t)));
     BSM_TRY(offs.alloc((tasks + 1) * sizeof(int64_t)));
     const uint64_t grid = (tasks + 3) / 4;
-    tiled_layout<false><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rp, col, vals, nw, rpw, nb, rw, pshift,
-                                                            counts.as<int32_t>(), nullptr, nullptr, nullptr);
-    BSM_HIP_TRY(hipGetLastError());
+    auto layout = [&](auto write_tag, int32_t* cnt, const int64_t* of, uint32_t* me, double* va) -> int {
+        constexpr bool W = decltype(write_tag)::value;
+        if (k == 1)
+            tiled_layout<W, (K1_RW_MAX + 1) / WAVE><<<dim3((unsigned)grid), 256, 0, s>>>(
+                rows, n_cols, pace, rbits, pad, rp, col, vals, nw, rpw, nb, rw, pshift, cnt, of, me, va);
+        else
+            tiled_layout<W, 3><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rbits, pad, rp, col, vals, nw,
+                                                                  rpw, nb, rw, pshift, cnt, of, me, va);
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    };
+    BSM_TRY(layout(std::false_type{}, counts.as<int32_t>(), nullptr, nullptr, nullptr));
     const uint64_t wsb = scan_workspace_bytes(tasks);
     BSM_TRY(ws.alloc(wsb));
     BSM_TRY(exclusive_scan_i32_to_i64(counts.as<int32_t>(), offs.as<int64_t>(), tasks, ws.p, wsb, s));
@@ -353,10 +486,10 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     BSM_HIP_TRY(read_dev(&total, offs.as<int64_t>() + tasks, sizeof(total), s));
     // a stream much longer than the matrix means rows too uneven for 64-row chunks
     BSM_REQUIRE((flags & BSM_TILED_ANY_PADDING) ||
-                    (uint64_t)total * CHUNK <= nnz + nnz / 4 + tasks * PHASES * CHUNK + (uint64_t)CHUNK * 64,
+                    (uint64_t)total * CHUNK <= nnz + nnz / 4 + tasks * pad * CHUNK + (uint64_t)CHUNK * 64,
                 BSM_ERR_UNSUPPORTED, "tiled: %lld chunks for %llu entries (rows too uneven)", (long long)total,
                 (unsigned long long)nnz);
-    const uint64_t slots = ((uint64_t)total + OVERREAD) * CHUNK;
+    const uint64_t slots = ((uint64_t)total + overread) * CHUNK;
     size_t free_b = 0, total_b = 0;
     BSM_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     BSM_REQUIRE(slots * 12 + (256ull << 20) < free_b, BSM_ERR_OOM, "tiled: %llu MB stream does not fit",
@@ -365,16 +498,14 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     BSM_TRY(bar.alloc(8 * BAR_STRIDE * sizeof(unsigned)));
     BSM_TRY(meta.alloc(slots * sizeof(uint32_t)));
     BSM_TRY(val.alloc(slots * sizeof(double)));
-    tiled_layout<true><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rp, col, vals, nw, rpw, nb, rw, pshift, nullptr,
-                                                           offs.as<int64_t>(), meta.as<uint32_t>(),
-                                                           val.as<double>());
-    BSM_HIP_TRY(hipGetLastError());
+    BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.as<uint32_t>(), val.as<double>()));
     // over-read padding: valid dummy entries (X row 0)
-    BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, OVERREAD * CHUNK * 4, s));
-    BSM_HIP_TRY(hipMemsetAsync(val.as<double>() + (uint64_t)total * CHUNK, 0, OVERREAD * CHUNK * 8, s));
+    BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 4, s));
+    BSM_HIP_TRY(hipMemsetAsync(val.as<double>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 8, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     auto* t = new bsm_tiled;
     t->device = dev;
+    t->k = k;
     t->rows = rows;
     t->n_cols = n_cols;
     t->nnz = nnz;
@@ -384,6 +515,8 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     t->rw = rw;
     t->pshift = pshift;
     t->chunks = (uint64_t)total;
+    t->overread = overread;
+    t->stage = k1_stage;
     t->offs = static_cast<int64_t*>(offs.release());
     t->meta = static_cast<uint32_t*>(meta.release());
     t->val = static_cast<double*>(val.release());
@@ -392,18 +525,27 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     return BSM_OK;
 }
 
-int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, hipStream_t s) {
+int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, bool neg_init, hipStream_t s) {
     BSM_REQUIRE(t && (t->rows == 0 || (x && y)), BSM_ERR_INVALID, "tiled: null argument");
+    BSM_REQUIRE(!neg_init || t->k == 1, BSM_ERR_INVALID, "tiled: -0 init only for k = 1");
     if (t->rows == 0) return BSM_OK;
-    const size_t lds = (size_t)4 * (t->rw + 1) * 256;
     unsigned* bar = nullptr;
     if (t->bar && t->nb > 1 && env_u32("BSM_TILED_SYNC", 1)) {
         BSM_HIP_TRY(hipMemsetAsync(t->bar, 0, 8 * BAR_STRIDE * sizeof(unsigned), s));
         bar = t->bar;
     }
-    spmm_tiled_k32<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
-                                                    static_cast<const double2*>(x), static_cast<double2*>(y),
-                                                    row_nnz, bar);
+    if (t->k == 1) {
+        const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(double);
+        auto kern = t->stage == 8 ? spmm_tiled_k1<8> : spmm_tiled_k1<4>;
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
+                                              static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar,
+                                              neg_init);
+    } else {
+        const size_t lds = (size_t)4 * (t->rw + 1) * 256;
+        spmm_tiled_k32<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
+                                                        static_cast<const double2*>(x), static_cast<double2*>(y),
+                                                        row_nnz, bar);
+    }
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }

@@ -94,12 +94,13 @@ class DeviceCsrBlock:
 
     def plan_tiled(self, k: int, force: bool = False) -> "TiledPlan | None":
         """Build the row-block x column-panel copy for k right-hand columns
-        when the library wants it for this shape (f64, k = 32, X > 1 GiB), or
+        when the library wants it for this shape (f64; k = 32 and X > 1 GiB, or
+        k = 1 and X > 4 MiB), or
         whenever possible with force (any chunk padding accepted). Synchronous, once per matrix. Returns
         the plan, or None (shape not served, or no memory for the copy)."""
         lib = _lib.require_device()
         self.tiled = None
-        if self.dtype != np.float64 or k != 32 or self.nnz == 0:
+        if self.dtype != np.float64 or k not in (1, 32) or self.nnz == 0:
             return None
         if not force:
             max_len = int((self.row_ptr[1:] - self.row_ptr[:-1]).max().item()) if self.rows else 0
@@ -108,12 +109,12 @@ class DeviceCsrBlock:
                 return None
         h = ctypes.c_void_p()
         rc = lib.bsm_dev_tiled_create(self.rows, self.n_cols, self.nnz, _p(self.row_ptr), _p(self.col),
-                                      _p(self.vals), _lib.BSM_TILED_ANY_PADDING if force else 0, ctypes.byref(h),
-                                      _stream())
+                                      _p(self.vals), k, _lib.BSM_TILED_ANY_PADDING if force else 0,
+                                      ctypes.byref(h), _stream())
         if rc in (_lib.BSM_ERR_UNSUPPORTED, _lib.BSM_ERR_OOM):
             return None
         _lib.check(rc)
-        self.tiled = TiledPlan(h.value)
+        self.tiled = TiledPlan(h.value, k)
         return self.tiled
 
     def spmm(self, x: torch.Tensor, y: torch.Tensor, row_nnz: torch.Tensor | None = None, stream=None) -> None:
@@ -122,7 +123,7 @@ class DeviceCsrBlock:
         bits)."""
         lib = _lib.load()
         k = x.shape[1] if x.dim() == 2 else 1
-        if self.tiled is not None and k == 32:
+        if self.tiled is not None and k == self.tiled.k:
             _lib.check(lib.bsm_dev_spmm_tiled(self.tiled.handle, _p(x), _p(y),
                                               _p(row_nnz) if row_nnz is not None else 0, _stream(stream)))
             return
@@ -140,8 +141,9 @@ class DeviceCsrBlock:
 class TiledPlan:
     """Owner of a bsm_tiled handle (the row-block x column-panel copy)."""
 
-    def __init__(self, handle: int):
+    def __init__(self, handle: int, k: int = 32):
         self.handle = handle
+        self.k = k
 
     def info(self) -> dict:
         lib = _lib.load()

@@ -64,7 +64,7 @@ def b_gather(rows, nnz, k):
 def kernel_label(rows, nnz, k, panel_cols, tiled=False):
     """The kernel launch_spmm (kernels_spmm.hip) picks for this shape."""
     if tiled:
-        return "spmm_tiled_k32"
+        return f"spmm_tiled_k{k}"
     if k == 1:
         if nnz <= 12 * rows:
             return "spmv_wave<double,8>"
@@ -343,7 +343,7 @@ def main():
     # defeat its batch pacing), so the all-gather follows the SpMM instead of
     # overlapping a next round
     lib0 = _lib.load()
-    tiled_shape = args.schedule != "panel" and k == 32 and bool(lib0.bsm_dev_tiled_wanted(
+    tiled_shape = args.schedule != "panel" and k in (1, 32) and bool(lib0.bsm_dev_tiled_wanted(
         _lib.DTYPE_CODES[np.dtype(np.float64)], rows, n_cols, rows * (nnz_r or 1), k, nnz_r or 1))
     chunks = args.chunks if args.chunks else (1 if world == 1 or tiled_shape else 4)
     cr, pieces = partition_rows_cyclic(rows, world, chunks)
@@ -376,7 +376,7 @@ def main():
     # plan_ms): the row-block x column-panel copy, or the column-panel plan
     t0 = time.perf_counter()
     panel_cols, tiled, tiled_info = 0, False, None
-    if args.schedule != "panel" and k == 32:
+    if args.schedule != "panel" and k in (1, 32):
         plans = [b.plan_tiled(k, force=args.schedule == "tiled") for b in blks]
         tiled = all(p is not None for p in plans)
         if tiled:
@@ -517,7 +517,7 @@ def main():
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
                 "parallelism": f"row-block x{world}" + (f" (block-cyclic, {chunks} rounds) + overlapped all-gather"
                                                          if world > 1 else ""),
-                "schedule": "row-block x column-panel copy (spmm_tiled_k32)" if tiled else
+                "schedule": f"row-block x column-panel copy (spmm_tiled_k{k})" if tiled else
                             ("column panels" if panel_cols else "one pass"),
                 "panel_cols": tiled_info["panel_cols"] if tiled else panel_cols, "passes": n_passes,
                 "plan_ms": round(plan_ms, 1),

@@ -209,11 +209,12 @@ int bsm_dev_spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nn
                           const void* x, void* y, int32_t* row_nnz, uint64_t panel_cols,
                           const int32_t* seg, void* stream);
 /* Row-block x column-panel schedule of bsm_dev_spmm (Csr::mul_dense,
- * sparse.rs:426-446) for f64, k = 32 and X beyond the Infinity Cache (the C4
- * shape; DESIGN.md "SpMM: row blocks x column panels"). bsm_dev_tiled_create
+ * sparse.rs:426-446) for f64 with k = 32 and X beyond the Infinity Cache (the
+ * C4 shape), or k = 1 and X beyond an XCD's L2 (C2); the copy is built for
+ * one k (DESIGN.md "SpMM: row blocks x column panels"). bsm_dev_tiled_create
  * re-lays the matrix once (12 B per entry plus chunk padding, a copy beside
  * the CSR; synchronous on `stream`) and returns BSM_ERR_UNSUPPORTED for a
- * shape it does not serve (cols >= 2^24; rows so uneven that chunk padding
+ * shape it does not serve (cols >= 2^24 at k = 32, 2^21 at k = 1; rows so uneven that chunk padding
  * passes 25 % of the entries, unless flags has BSM_TILED_ANY_PADDING) or
  * BSM_ERR_OOM.
  * bsm_dev_spmm_tiled = bsm_dev_spmm on that copy: the same Y and row_nnz,
@@ -226,8 +227,8 @@ typedef struct bsm_tiled bsm_tiled;
 int bsm_dev_tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k,
                          uint64_t max_row_len);
 int bsm_dev_tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* row_ptr,
-                         const int32_t* col, const double* vals, int flags, bsm_tiled** out,
-                         void* stream);
+                         const int32_t* col, const double* vals, uint64_t k, int flags,
+                         bsm_tiled** out, void* stream);
 int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* row_nnz,
                        void* stream);
 int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols);

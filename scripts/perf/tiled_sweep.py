@@ -35,22 +35,23 @@ def timed(fn, reps=3):
 def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     variants = sys.argv[2:] or [""]
-    n_cols, k = 10_000_000, 32
+    c2 = os.environ.get("SWEEP_SHAPE") == "c2"  # C2: 1M x 1M, 10 nnz/row, k = 1
+    n_cols, k, nnz_r = (1_000_000, 1, 10) if c2 else (10_000_000, 32, 1000)
     torch.cuda.set_device(0)
     t0 = time.perf_counter()
-    blk = DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_CONST, 1000, 1000)
+    blk = DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_CONST, nnz_r, nnz_r)
     x = gen_dense(1001, 0, n_cols, k)
     y = torch.empty((rows, k), dtype=torch.float64, device="cuda")
     nnz = torch.empty(rows, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
-    scale = 10_000_000 / rows
+    scale = (1_000_000 if c2 else 10_000_000) / rows
     print(f"generated {rows:,} rows in {time.perf_counter() - t0:.1f} s", flush=True)
     ref = None
     if os.environ.get("SWEEP_REF", "1") == "1":
         blk.plan(k)
-        best, mean = timed(lambda: blk.spmm(x, y, nnz))
+        best, mean = timed(lambda: blk.spmm(x, y, nnz), reps=20 if c2 else 3)
         ref = y.clone()
-        print(f"panelled ({blk.panel_cols} cols): {best:.2f} ms (mean {mean:.2f}), C4-scaled {best * scale:.1f} ms",
+        print(f"untiled ({blk.panel_cols} panel cols): {best:.3f} ms (mean {mean:.3f}), scaled {best * scale:.3f} ms",
               flush=True)
         blk.seg, blk.panel_cols = None, 0
     for var in variants:
@@ -70,10 +71,10 @@ def main():
             print(f"{var or 'default'}: declined", flush=True)
             continue
         info = plan.info()
-        best, mean = timed(lambda: blk.spmm(x, y, nnz))
+        best, mean = timed(lambda: blk.spmm(x, y, nnz), reps=20 if c2 else 3)
         same = None if ref is None else bool(torch.equal(y.view(torch.int64), ref.view(torch.int64)))
-        print(f"{var or 'default'}: {best:.2f} ms (mean {mean:.2f}), C4-scaled {best * scale:.1f} ms, "
-              f"gather {rows * 1000 * 256 / best / 1e9:.2f} TB/s, padding {info['slots'] / blk.nnz - 1:.4f}, "
+        print(f"{var or 'default'}: {best:.3f} ms (mean {mean:.3f}), scaled {best * scale:.3f} ms, "
+              f"gather {rows * nnz_r * 8 * k / best / 1e9:.2f} TB/s, padding {info['slots'] / blk.nnz - 1:.4f}, "
               f"build {build_ms:.0f} ms, same bits {same}", flush=True)
         blk.tiled = None
         del plan

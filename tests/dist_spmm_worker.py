@@ -12,7 +12,8 @@ output Csr, and checks a sampled row range against the CPU oracle
 (Csr::mul_dense, src/sparse.rs:426-446). The verdict is written as JSON to
 argv[1].
 
-argv: out_json rows n_cols nnz_per_row k chunks panel_cols(0 = none)
+argv: out_json rows n_cols nnz_per_row k chunks panel_cols(0 = none, -1 = the
+tiled row-block x column-panel copy, forced, per piece)
 """
 
 import json
@@ -42,7 +43,10 @@ def main():
     cr, pieces = partition_rows_cyclic(rows, world, chunks)
     blks = [DeviceCsrBlock.generate(1000, r0, n, n_cols, _lib.ROWLEN_UNIFORM, 0, 2 * nnz_r, _lib.VAL_UNIFORM,
                                     np.float64, device=dev) for r0, n in pieces[rank]]
-    widths = [b.plan(k, panel) if panel else 0 for b in blks]
+    if panel == -1:
+        widths = [-1 if b.nnz and b.plan_tiled(k, force=True) is not None else 0 for b in blks]
+    else:
+        widths = [b.plan(k, panel) if panel else 0 for b in blks]
     x = gen_dense(1001, 0, n_cols, k, device=dev)
     y_local = torch.full((chunks, cr, k), float("nan"), dtype=torch.float64, device=dev)
     nnz_local = torch.full((chunks, cr), -1, dtype=torch.int32, device=dev)

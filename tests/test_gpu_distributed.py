@@ -34,6 +34,8 @@ def _free_port():
     (2, 20_011, 5_000, 12, 32, 3, 350),   # column-panel plan (15 panels of 350 columns)
     (3, 9_001, 3_000, 6, 1, 3, 0),        # SpMV arm (k = 1)
     (2, 4_099, 4_000, 40, 7, 3, 0),       # general-k kernel
+    (2, 20_011, 5_000, 12, 32, 3, -1),    # tiled copy per piece (k = 32), several batches: the batch pacing
+    (3, 9_001, 3_000, 6, 1, 2, -1),       # tiled copy, k = 1   barrier with two grids sharing the CUs
 ])
 def test_block_cyclic_spmm_on_gpu_matches_single(tmp_path, world, rows, n_cols, nnz_r, k, chunks, panel):
     port = _free_port()
@@ -42,6 +44,8 @@ def test_block_cyclic_spmm_on_gpu_matches_single(tmp_path, world, rows, n_cols, 
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if panel == -1:  # small batches so the pacing barrier is live
+            env.update(BSM_TILED_RW="64" if k == 32 else "40", BSM_TILED_WAVES="16")
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, str(outs[r]), str(rows), str(n_cols),
                                        str(nnz_r), str(k), str(chunks), str(panel)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -56,7 +60,9 @@ def test_block_cyclic_spmm_on_gpu_matches_single(tmp_path, world, rows, n_cols, 
                 p.kill()
     assert all(p.returncode == 0 for p in procs), logs
     res = json.loads(outs[0].read_text())
-    if panel:
+    if panel == -1:
+        assert any(w == -1 for w in res["widths"]), res  # the tiled kernel really ran
+    elif panel:
         assert all(w == panel for w in res["widths"]), res  # the panelled kernel really ran
     assert res["y_equal"] and res["nnz_equal"], res
     assert res["oracle_equal"], res

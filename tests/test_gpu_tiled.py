@@ -200,3 +200,41 @@ def test_public_mul_dense_uses_tiled_copy(orc, monkeypatch):
     _lib.check(_lib.load().bsm_csr_tiled(b._device().handle, ctypes.byref(used)))
     assert used.value == 0
     assert np.array_equal(np.asarray(ref.v).view(np.uint64), ev.view(np.uint64))
+
+
+@pytest.mark.parametrize("rw,waves,pshift", [(None, None, None), (300, 16, 12), (2047, 4, 15)])
+def test_tiled_k1_equals_spmv(geometry, rw, waves, pshift):
+    """k = 1 (SpMV): the copy with one LDS double per row gives the k = 1
+    kernels' y and counts bit for bit (uneven and empty rows, signed values)."""
+    geometry(rw, waves, pshift)
+    rng = np.random.default_rng(3)
+    rows, n_cols = 20_000, 300_000
+    lens = rng.integers(0, 25, size=rows)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, size=n, replace=False)) for n in lens]).astype(np.int32)
+    v = rng.standard_normal(rp[-1])
+    blk = _block(rp, ci, v, n_cols)
+    x = torch.as_tensor(rng.standard_normal((n_cols, 1)), device="cuda")
+    assert blk.plan_tiled(1, force=True) is not None
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+
+
+def test_tiled_k1_c2_shape(orc):
+    """C2 (1M x 1M, 10 nnz/row, k = 1): the library wants the copy at this
+    shape; every row equals the k = 1 kernel and a sample equals the oracle."""
+    device = _dev()
+    rows = n_cols = 1_000_000
+    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_CONST, 10, 10)
+    x = device.gen_dense(1001, 0, n_cols, 1)
+    assert blk.plan_tiled(1) is not None
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+    rp = blk.row_ptr.cpu().numpy().astype(np.uint64)
+    ci, v = blk.col.cpu().numpy(), blk.vals.cpu().numpy()
+    r0, r1 = 777_000, 778_000
+    sub = (rp[r0:r1 + 1] - rp[r0]).astype(np.uint64)
+    erp, eci, ev = orc.mul_dense(r1 - r0, n_cols, sub, ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]], orc.gen_x_cols(1001, n_cols, 1))
+    assert np.array_equal(y1[r0:r1, 0].cpu().numpy().view(np.uint64), ev.view(np.uint64))
