@@ -1931,11 +1931,11 @@ __device__ __forceinline__ float rsqrt_nr(float x) {
 // the ticket loop its 64 unrolled steps would share the register budget with
 // everything the compiler hoists there. P receives L (zero upper part), rd the
 // reciprocal pivots.
-template <typename T>
+template <typename T, int N = 64>
 __device__ __forceinline__ void blk_diag_factor(lds_t<T>* P, lds_t<T>* colb, lds_t<T>* rd, int* status, int ln) {
-    T a[64];
+    T a[N];
 #pragma unroll
-    for (int c = 0; c < 64; ++c) a[c] = P[ln * TLD + c];
+    for (int c = 0; c < N; ++c) a[c] = P[ln * TLD + c];  // lanes >= N: rows below, never written back
     bool pd = true;
     // one instantiation per column s: a[] is only ever indexed by constants
     auto step = [&]<int s>(std::integral_constant<int, s>) __attribute__((always_inline)) {
@@ -1947,13 +1947,13 @@ __device__ __forceinline__ void blk_diag_factor(lds_t<T>* P, lds_t<T>* colb, lds
         const T l = a[s] * rp;
         a[s] = l;
         rd[s] = rp;  // uniform value, every lane
-        if constexpr (s + 1 < 64) {
+        if constexpr (s + 1 < N) {
             // the next pivot's column first, by v_readlane: the chain from pivot to
             // pivot has no LDS round trip; the later columns take the LDS broadcast
             a[s + 1] = fma_t(-l, readlane_t(l, s + 1), a[s + 1]);
             colb[ln] = l;
 #pragma unroll
-            for (int c = s + 2; c < 64; ++c) {
+            for (int c = s + 2; c < N; ++c) {
                 if ((c & 31) == 0) asm volatile("" ::: "memory");  // at most 32 broadcast values in flight
                 a[c] = fma_t(-l, colb[c], a[c]);
             }
@@ -1962,27 +1962,130 @@ __device__ __forceinline__ void blk_diag_factor(lds_t<T>* P, lds_t<T>* colb, lds
     };
     [&]<int... ss>(std::integer_sequence<int, ss...>) __attribute__((always_inline)) {
         (step(std::integral_constant<int, ss>{}), ...);
-    }(std::make_integer_sequence<int, 64>{});
+    }(std::make_integer_sequence<int, N>{});
     if (ln == 0 && !pd) atomicOr(status, ST_NOT_PD);
+    if (ln < N) {
 #pragma unroll
-    for (int c = 0; c < 64; ++c) P[ln * TLD + c] = c <= ln ? a[c] : (T)0;
+        for (int c = 0; c < N; ++c) P[ln * TLD + c] = c <= ln ? a[c] : (T)0;
+    }
 }
 
-// Q[c * TLD + r] = Linv[r][c] for L in P (one wave, lane c forms column c of
-// the inverse, rows ascending)
-template <typename T>
+// Q[c * TLD + r] = Linv[r][c] for the N x N L in P (one wave, lane c < N forms
+// column c of the inverse, rows ascending; the dot products by four chains,
+// their LDS reads 16 at a time ahead of the FMAs)
+template <typename T, int N = 64>
 __device__ __forceinline__ void blk_diag_inverse(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* rd, int ln) {
-    T x[64];
+    asm volatile("" : "+v"(ln));  // opaque: keep the per-row masks out of the ticket loop
+    T x[N];
+    auto row = [&]<int r>(std::integral_constant<int, r>) __attribute__((always_inline)) {
+        T sa[4] = {(T)0, (T)0, (T)0, (T)0};
+        auto blk16 = [&]<int q0>(std::integral_constant<int, q0>) __attribute__((always_inline)) {
+            if constexpr (q0 < r) {
+                constexpr int m = r - q0 < 16 ? r - q0 : 16;
+                T hv[16];
+                [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
+                    ((hv[is] = ((volatile const lds_t<T>*)P)[r * TLD + q0 + is]), ...);  // volatile: not hoisted
+                }(std::make_integer_sequence<int, m>{});
+                __builtin_amdgcn_sched_barrier(0);
+                [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
+                    ((sa[(q0 + is) & 3] = fma_t(hv[is], x[q0 + is], sa[(q0 + is) & 3])), ...);
+                }(std::make_integer_sequence<int, m>{});
+            }
+        };
+        [&]<int... bs>(std::integer_sequence<int, bs...>) __attribute__((always_inline)) {
+            (blk16(std::integral_constant<int, 16 * bs>{}), ...);
+        }(std::make_integer_sequence<int, (N + 15) / 16>{});
+        x[r] = ((r == ln ? (T)1 : (T)0) - ((sa[0] + sa[1]) + (sa[2] + sa[3]))) *
+               ((volatile const lds_t<T>*)rd)[r];
+        // pin row r: its FMAs (pure, free to float in the DAG) complete before
+        // row r + 1's (volatile) reads, so at most 16 reads are live at once
+        asm volatile("" : "+v"(x[r]));
+    };
+    [&]<int... rs>(std::integer_sequence<int, rs...>) __attribute__((always_inline)) {
+        (row(std::integral_constant<int, rs>{}), ...);
+    }(std::make_integer_sequence<int, N>{});
+    if (ln < N) {
 #pragma unroll
-    for (int r = 0; r < 64; ++r) {
-        T s = (T)0;
+        for (int r = 0; r < N; ++r) Q[ln * TLD + r] = x[r];
+    }
+}
+
+// Factor AND invert the 64 x 64 tile S (P[r * TLD + c], lower part) as 2 x 2
+// blocks of 32 (the one-wave steps cost ~N^2 per pivot, so two 32-column
+// factors and inverses are a quarter of the 64-column ones):
+//   L11 = chol(S11), Linv11 (wave 0);  L21 = S21 Linv11^T;
+//   S22 -= L21 L21^T;  L22 = chol(S22), Linv22 (wave 0);
+//   Linv21 = -Linv22 (L21 Linv11)  (all waves; T = L21 Linv11 in Tm).
+// Out: P = L (zero upper part), Q[c * TLD + r] = Linv[r][c] (zero upper
+// part), rd = 1 / L[r][r]. colb: 64 scratch words; Tm: 32 x 32 scratch.
+// Every thread of the workgroup must call it (barriers inside).
+template <typename T>
+__device__ __noinline__ void blk_diag_2x2(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* rd, lds_t<T>* colb, lds_t<T>* Tm,
+                                             int* status, int tid) {
+    asm volatile("" : "+v"(tid));
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
+    const int gi = tid >> 3, gj = (tid & 7) * 4;  // this thread's outputs of a 32 x 32 product: row gi, cols gj..+3
+    lds_t<T>* P22 = P + 32 * TLD + 32;
+    if (w == 0) blk_diag_factor<T, 32>(P, colb, rd, status, ln);
+    __syncthreads();
+    if (w == 0) blk_diag_inverse<T, 32>(P, Q, rd, ln);
+    __syncthreads();
+    T o[4];
+    // L21[i][j] = sum_{q <= j} S21[i][q] Linv11[j][q]   (Linv11[j][q] = Q[q * TLD + j])
 #pragma unroll
-        for (int q = 0; q < r; ++q) s = fma_t(P[r * TLD + q], x[q], s);
-        x[r] = ((r == ln ? (T)1 : (T)0) - s) * rd[r];
-        asm volatile("" ::: "memory");  // keep row r's LDS reads in step r (else all 2016 are hoisted)
+    for (int u = 0; u < 4; ++u) o[u] = (T)0;
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) {
+        const T sv = P[(32 + gi) * TLD + q];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = fma_t(sv, Q[q * TLD + gj + u], o[u]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) P[(32 + gi) * TLD + gj + u] = o[u];
+    __syncthreads();
+    // S22[i][j] -= sum_q L21[i][q] L21[j][q]; T[i][j] = sum_{q >= j} L21[i][q] Linv11[q][j]
+    T t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        o[u] = (T)0;
+        t[u] = (T)0;
+    }
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) {
+        const T lv = P[(32 + gi) * TLD + q];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            o[u] = fma_t(lv, P[(32 + gj + u) * TLD + q], o[u]);
+            t[u] = fma_t(lv, Q[(gj + u) * TLD + q], t[u]);
+        }
     }
 #pragma unroll
-    for (int r = 0; r < 64; ++r) Q[ln * TLD + r] = x[r];
+    for (int u = 0; u < 4; ++u) {
+        P22[gi * TLD + gj + u] -= o[u];
+        Tm[gi * 32 + gj + u] = t[u];
+    }
+    __syncthreads();
+    if (w == 0) blk_diag_factor<T, 32>(P22, colb, rd + 32, status, ln);
+    __syncthreads();
+    if (w == 0) blk_diag_inverse<T, 32>(P22, Q + 32 * TLD + 32, rd + 32, ln);
+    __syncthreads();
+    // Linv21[i][j] = -sum_{p <= i} Linv22[i][p] T[p][j]  (Linv22[i][p] = Q[(32 + p) * TLD + 32 + i])
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[u] = (T)0;
+#pragma unroll 8
+    for (int p = 0; p < 32; ++p) {
+        const T lv = Q[(32 + p) * TLD + 32 + gi];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = fma_t(lv, Tm[p * 32 + gj + u], o[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        Q[(gj + u) * TLD + 32 + gi] = -o[u];  // Linv21
+        Q[(32 + gj + u) * TLD + gi] = (T)0;  // Linv12
+        P[gi * TLD + 32 + gj + u] = (T)0;    // L12
+    }
+    __syncthreads();
 }
 
 // The same inverse on all 4 waves: a quad of lanes per column c = 16w + (lane
@@ -2027,35 +2130,42 @@ __device__ __forceinline__ void blk_diag_inverse4(const lds_t<T>* P, lds_t<T>* Q
 // 16 x 16 diagonal blocks: diagonal blocks Di, zeros above, then the blocks
 // below by distance: Linv[p2][p1] = -Di[p2] sum_q L[p2][q] Linv[q][p1].
 // Q[c * TLD + r] = Linv[r][c]. All threads; barriers inside.
+typedef double bsm_d4 __attribute__((ext_vector_type(4)));
 template <typename T>
 __device__ __forceinline__ void blk_linv_from_blocks(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di,
                                                      lds_t<T>* Tb, int tid) {
-    for (int e = tid; e < 4096; e += 256) {
-        const int c = e >> 6, r = e & 63, pr = r >> 4, pc = c >> 4;
+    (void)Tb;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int e = tid + 256 * u, c = e >> 6, r = e & 63, pr = r >> 4, pc = c >> 4;
         Q[c * TLD + r] = pr == pc ? Di[pr * 256 + (r & 15) * 16 + (c & 15)] : (T)0;
     }
     __syncthreads();
+    // by distance dd, wave p1 forms block (p2, p1) = (p1 + dd, p1) on f64 MFMA
+    // 16x16x4 (lane l: A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result
+    // rows (l >> 4) + 4q, column l & 15):
+    //   T = sum_{qb = p1}^{p2 - 1} L[p2][qb] Linv[qb][p1];  Linv[p2][p1] = -Di[p2] T
+    // T's result registers are the second product's B operand as they stand
+    // (k step q is rows 4q + (l >> 4)).
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, m = l & 15, kq = l >> 4;
     for (int dd = 1; dd < 4; ++dd) {
-        // Tb[blk][rr][cc] = sum_q L[16 p2 + rr][q] Linv[q][16 p1 + cc], q in [16 p1, 16 p2)
-        for (int e = tid; e < (4 - dd) * 256; e += 256) {
-            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
-            T s = (T)0;
-            for (int qb = p1; qb < p2; ++qb) {  // 16 terms at a time: their loads in flight together
-                T s2 = (T)0;
+        if (w < 4 - dd) {
+            const int p1 = w, p2 = p1 + dd;
+            bsm_d4 t = {0.0, 0.0, 0.0, 0.0};
+            for (int qb = p1; qb < p2; ++qb) {
 #pragma unroll
-                for (int t = 0; t < 16; ++t)
-                    s2 = fma_t(P[(16 * p2 + rr) * TLD + 16 * qb + t], Q[(16 * p1 + cc) * TLD + 16 * qb + t], s2);
-                s += s2;
+                for (int k4 = 0; k4 < 4; ++k4) {
+                    const int k = 16 * qb + 4 * k4 + kq;
+                    t = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(16 * p2 + m) * TLD + k],
+                                                             (double)Q[(16 * p1 + m) * TLD + k], t, 0, 0, 0);
+                }
             }
-            Tb[e] = s;
-        }
-        __syncthreads();
-        for (int e = tid; e < (4 - dd) * 256; e += 256) {
-            const int p1 = e >> 8, p2 = p1 + dd, rr = (e >> 4) & 15, cc = e & 15;
-            T s = (T)0;
+            bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < 16; ++t) s = fma_t(Di[p2 * 256 + rr * 16 + t], Tb[p1 * 256 + t * 16 + cc], s);
-            Q[(16 * p1 + cc) * TLD + 16 * p2 + rr] = -s;
+            for (int k4 = 0; k4 < 4; ++k4)
+                o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)Di[p2 * 256 + m * 16 + 4 * k4 + kq], t[k4], o, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Q[(16 * p1 + m) * TLD + 16 * p2 + kq + 4 * q] = (T)o[q];
         }
         __syncthreads();
     }
@@ -2102,6 +2212,7 @@ __device__ __forceinline__ void blk_diag_inverse_blocked(const lds_t<T>* P, lds_
 //      into Di[p];
 //   2. the rows below: L[i][c0 + j] = sum_t S[i][c0 + t] Di[p][j][t];
 //   3. the trailing lower part: S[i][j] -= sum_t L[i][c0 + t] L[j][c0 + t].
+// Steps 2 and 3 are 16 x 16 blocks on f64 MFMA, one block per wave at a time.
 // Then Linv by block distance: Linv[p2][p1] = -Di[p2] sum_q L[p2][q] Linv[q][p1].
 // Q[c * TLD + r] = Linv[r][c] (zero above the diagonal); rd[r] = 1 / L[r][r].
 // Every thread of the workgroup must call it (barriers inside).
@@ -2152,57 +2263,74 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
         }
         __syncthreads();
-        // 2. rows below the block: thread (i, jq) forms L[i][c0 + 4jq .. + 3]
-        const int i = c0 + 16 + (tid >> 2), jq = tid & 3;
-        T o[4] = {(T)0, (T)0, (T)0, (T)0};
-        if (i < 64) {
+        // 2. rows below the block, one 16-row block per wave on f64 MFMA
+        //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
+        const int l = tid & 63, m = l & 15, kq = l >> 4;
+        if (w < 3 - p) {
+            const int r0 = 16 * (p + 1 + w);
+            bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const T sv = P[i * TLD + c0 + t];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] = fma_t(sv, Di[p * 256 + (4 * jq + k) * 16 + t], o[k]);
+            for (int k4 = 0; k4 < 4; ++k4) {
+                const int k = 4 * k4 + kq;
+                o = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(r0 + m) * TLD + c0 + k],
+                                                         (double)Di[p * 256 + m * 16 + k], o, 0, 0, 0);
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[(r0 + kq + 4 * q) * TLD + c0 + m] = (T)o[q];
         }
         __syncthreads();
-        if (i < 64) {
+        // 3. the trailing lower part by 16 x 16 blocks (pi, pj), p < pj <= pi:
+        //    S[pi][pj] -= L[pi][p] L[pj][p]^T, blocks dealt to the waves in turn
+        const int nbk = 3 - p;
+        for (int bk = w; bk < nbk * (nbk + 1) / 2; bk += 4) {
+            int pi = 0, pj = bk;  // bk -> (pi, pj), pj <= pi, both relative to p + 1
+            while (pj > pi) pj -= ++pi;
+            const int i0 = 16 * (p + 1 + pi), j0 = 16 * (p + 1 + pj);
+            bsm_d4 o;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) P[i * TLD + c0 + 4 * jq + k] = o[k];
-        }
-        __syncthreads();
-        // 3. trailing lower part, 4 x 4 tiles
-        const int nt = 12 - 4 * p;
-        if (tid < nt * nt) {
-            const int ti = tid / nt, tj = tid % nt;
-            if (ti >= tj) {
-                const int i0 = c0 + 16 + 4 * ti, j0 = c0 + 16 + 4 * tj;
-                T s4[4][4];
+            for (int q = 0; q < 4; ++q) o[q] = (double)P[(i0 + kq + 4 * q) * TLD + j0 + m];
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int bq = 0; bq < 4; ++bq) s4[a][bq] = P[(i0 + a) * TLD + j0 + bq];
-#pragma unroll 4
-                for (int t = 0; t < 16; ++t) {
-                    T la[4], lb[4];
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        la[a] = P[(i0 + a) * TLD + c0 + t];
-                        lb[a] = P[(j0 + a) * TLD + c0 + t];
-                    }
-#pragma unroll
-                    for (int a = 0; a < 4; ++a)
-#pragma unroll
-                        for (int bq = 0; bq < 4; ++bq) s4[a][bq] = fma_t(-la[a], lb[bq], s4[a][bq]);
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int bq = 0; bq < 4; ++bq) P[(i0 + a) * TLD + j0 + bq] = s4[a][bq];
+            for (int k4 = 0; k4 < 4; ++k4) {
+                const int k = 4 * k4 + kq;
+                o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)P[(i0 + m) * TLD + c0 + k],
+                                                         (double)P[(j0 + m) * TLD + c0 + k], o, 0, 0, 0);
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
         }
         __syncthreads();
     }
     if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
     blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
+}
+
+// X[cb][q] (element (row 16w + (lane >> 4) + 4q, column 16cb + (lane & 15)) of
+// a 64 x 64 tile) += (NEG ? -1 : 1) * sum_k AT[k][row] * B[k][col], one
+// v_mfma_f64_16x16x4 per 16 x 16 block and 4 k: wave w forms rows 16w..16w+15
+// (A operand: lane l holds A[l & 15][l >> 4]; B: B[l >> 4][l & 15]). Two LDS
+// reads per 4 x 16 x 16 FMAs instead of eight per 16 on the VALU. f32 tiles
+// are carried in f64.
+template <typename T, bool NEG>
+__device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B, T (&X)[4][4], int w, int lane) {
+    bsm_d4 c[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[cb][q] = (double)X[cb][q];
+    const int kq = lane >> 4, m = lane & 15;
+#pragma unroll 4
+    for (int k4 = 0; k4 < 16; ++k4) {
+        const int k = 4 * k4 + kq;
+        double a = (double)AT[k * TLD + 16 * w + m];
+        if (NEG) a = -a;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+            c[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)B[k * TLD + 16 * cb + m], c[cb], 0, 0, 0);
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[cb][q] = (T)c[cb][q];
 }
 
 template <typename T>
@@ -2218,7 +2346,6 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
     __shared__ int64_t tk;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int tr = tid >> 4, tc = tid & 15;  // this thread's 4 x 4 outputs: rows 4tr.., cols 4tc..
     const int64_t nb64 = (n + 63) / 64, DM = (63 + b) / 64 + 1;  // tiles per block column (incl. diagonal)
     auto wait_flag = [&](const int* f) {
         long long spins = 0;
@@ -2243,11 +2370,35 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
     auto band_idx = [&](int64_t I, int64_t K, int r, int c) -> int64_t {
         return (64 * K + c) * ld + 64 * (I - K) + r - c;
     };
-    // stage the transpose of tile (I, J) of L: X[t][r] = L[64I + r][64J + t] (sc1: other workgroups wrote it)
+    // stage the transpose of tile (I, J) of L: X[t][r] = L[64I + r][64J + t] (sc1: other workgroups wrote it).
+    // All 16 loads of a thread are in flight before the first LDS write (a loop
+    // of load, wait, write is 16 memory round trips); out-of-band elements load
+    // element 0 and are replaced by zero (a selected address is not a branch).
     auto stage = [&](T (*X)[TLD], int64_t I, int64_t J) {
-        for (int e = tid; e < 4096; e += 256) {
-            const int r = e & 63, t = e >> 6;
-            X[t][r] = in_band(I, J, r, t) ? ld_sc1(&CB[band_idx(I, J, r, t)]) : (T)0;
+        T v[16];
+        unsigned okm = 0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = tid + 256 * u, r = e & 63, t = e >> 6;
+            const bool ok = in_band(I, J, r, t);
+            okm |= (unsigned)ok << u;
+            v[u] = ld_sc1(&CB[band_idx(I, J, r, t) & -(int64_t)ok]);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = tid + 256 * u;
+            X[e >> 6][e & 63] = (okm >> u) & 1 ? v[u] : (T)0;
+        }
+    };
+    // X[q][l] = Dinv[Kd][q * 64 + l], the same way
+    auto stage_dinv = [&](T (*X)[TLD], int64_t Kd) {
+        T v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = ld_sc1(&Dinv[Kd * 4096 + tid + 256 * u]);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = tid + 256 * u;
+            X[e >> 6][e & 63] = v[u];
         }
     };
     for (;;) {
@@ -2267,24 +2418,29 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             continue;
         }
         const bool sub = d == 0 && K > 0 && DM > 1;  // this workgroup also forms tile (K, K - 1)
+        // this thread's 16 elements of a 64 x 64 tile, in the f64 MFMA accumulator
+        // layout: X[cb][q] = element (row rb + 4q, column 16cb + cm)
+        const int rb = 16 * w + (lane >> 4), cm = lane & 15;
+        lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
+        lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
         T acc[4][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int r = 4 * tr + i, c = 4 * tc + j;
+            for (int q = 0; q < 4; ++q) {
+                const int r = rb + 4 * q, c = 16 * cb + cm;
                 // A itself (band_fill; rows past n: identity on the diagonal)
                 T a = in_band(I, K, r, c) ? CB[band_idx(I, K, r, c)] : (T)0;
                 if (d == 0 && r == c && 64 * I + r >= n) a = (T)1;
-                acc[i][j] = a;
+                acc[cb][q] = a;
             }
         T acc2[4][4];  // sub: tile (K, K - 1) = A_{K,K-1} - sum_{J < K-1} L_{K,J} L_{K-1,J}^T
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int r = 4 * tr + i, c = 4 * tc + j;
-                acc2[i][j] = sub && in_band(K, K - 1, r, c) ? CB[band_idx(K, K - 1, r, c)] : (T)0;
+            for (int q = 0; q < 4; ++q) {
+                const int r = rb + 4 * q, c = 16 * cb + cm;
+                acc2[cb][q] = sub && in_band(K, K - 1, r, c) ? CB[band_idx(K, K - 1, r, c)] : (T)0;
             }
         // left-looking updates from block columns J in the band of both I and K
         // (with sub, J = K - 1 comes after tile (K, K - 1) is formed, below)
@@ -2297,93 +2453,58 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             if (d > 0) stage(QT, K, J);
             if (sub) stage(QT, K - 1, J);
             __syncthreads();
-            T (*Q)[TLD] = d > 0 ? QT : PT;
-#pragma unroll 4
-            for (int s = 0; s < 64; ++s) {
-                T pa[4], qb[4], q2[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    pa[i] = PT[s][4 * tr + i];
-                    qb[i] = Q[s][4 * tc + i];
-                    q2[i] = QT[s][4 * tc + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[i][j] = fma_t(-pa[i], qb[j], acc[i][j]);
-                        if (sub) acc2[i][j] = fma_t(-pa[i], q2[j], acc2[i][j]);
-                    }
-            }
+            mfma_tile<T, true>(PTl, d > 0 ? QTl : PTl, acc, w, lane);
+            if (sub) mfma_tile<T, true>(PTl, QTl, acc2, w, lane);
             __syncthreads();
         }
+        long long cw0 = 0, cw1 = 0, cs1 = 0, cs2 = 0, cs3 = 0;  // BSM_BLK_DEBUG: the chain's steps
         if (sub) {
             // L_{K,K-1} = S_{K,K-1} L_{K-1,K-1}^-T once diagonal tile K - 1 is done
+            if (dbg) cw0 = clock64();
             wait_flag(&flags[(K - 1) * DM]);
+            if (dbg) cw1 = clock64();
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = acc2[i][j];
-            for (int e = tid; e < 4096; e += 256) QT[e >> 6][e & 63] = ld_sc1(&Dinv[(K - 1) * 4096 + e]);
+                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
+            stage_dinv(QT, K - 1);
             __syncthreads();
-            T o[4][4];
+            if (dbg) cs1 = clock64();
+            T o[4][4] = {};
+            mfma_tile<T, false>(PTl, QTl, o, w, lane);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) o[i][j] = (T)0;
-#pragma unroll 4
-            for (int s = 0; s < 64; ++s) {
-                T pa[4], qb[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    pa[i] = PT[s][4 * tr + i];
-                    qb[i] = QT[s][4 * tc + i];
+                for (int q = 0; q < 4; ++q) {
+                    const int r = rb + 4 * q, c = 16 * cb + cm;
+                    if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
                 }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) o[i][j] = fma_t(pa[i], qb[j], o[i][j]);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = 4 * tr + i, c = 4 * tc + j;
-                    if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[i][j]);
-                }
+            if (dbg) cs2 = clock64();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (dbg) cs3 = clock64();
             // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t]
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = o[i][j];
+                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = o[cb][q];
             __syncthreads();
-#pragma unroll 4
-            for (int s = 0; s < 64; ++s) {
-                T pa[4], qb[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    pa[i] = PT[s][4 * tr + i];
-                    qb[i] = PT[s][4 * tc + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = fma_t(-pa[i], qb[j], acc[i][j]);
-            }
+            mfma_tile<T, true>(PTl, PTl, acc, w, lane);
             __syncthreads();
         }
         if (d == 0) {
             const long long c0 = dbg ? clock64() : 0;
             // S to LDS (PT[r][c]), then wave 0 factors it: lane r holds row r
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) PT[4 * tr + i][4 * tc + j] = acc[i][j];
+                for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
             __syncthreads();
-            if (panels) {  // factor and inverse by 16-column panels on all four waves
+            if (panels == 3) {  // 2 x 2 blocks of 32
+                blk_diag_2x2<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, (lds_t<T>*)Tb,
+                                (lds_t<T>*)Di, status, tid);
+            } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default)
                 blk_diag_panels<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
                                    (lds_t<T>*)rd, status, tid);
             } else {  // one-wave factor; the inverse below
@@ -2392,11 +2513,6 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 __syncthreads();
             }
             const long long c1 = dbg ? clock64() : 0;
-            // L_{K,K} to the band (write-through) by all threads
-            for (int e = tid; e < 4096; e += 256) {
-                const int r = e & 63, c = e >> 6;
-                if (r >= c && in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], PT[r][c]);
-            }
             if (!panels)
                 blk_diag_inverse_blocked<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
                                             tid);
@@ -2406,9 +2522,38 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 __hip_atomic_fetch_add(&dbg[4], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_fetch_add(&dbg[5], (unsigned long long)(c2 - c1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_fetch_add(&dbg[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (sub) {  // the chain: waiting for tile K - 1, then the sub-diagonal tile and its update
+                    __hip_atomic_fetch_add(&dbg[8], (unsigned long long)(cw1 - cw0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&dbg[9], (unsigned long long)(c0 - cw1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&dbg[10], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&dbg[14], (unsigned long long)(cs1 - cw1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&dbg[15], (unsigned long long)(cs2 - cs1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&dbg[16], (unsigned long long)(cs3 - cs2), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
             // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]
-            for (int e = tid; e < 4096; e += 256) st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u;
+                st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+            }
+            if (dbg) {  // the publication: stores drained, then the flag (below)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (tid == 0) {
+                    const long long c3 = clock64();
+                    __hip_atomic_fetch_add(&dbg[11], (unsigned long long)(c3 - c0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    // clock calibration: the constant 100 MHz counter at each diagonal tile's end
+                    const unsigned long long wc = wall_clock64();
+                    if (K == 0) __hip_atomic_store(&dbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (K == nb64 - 1) __hip_atomic_store(&dbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         } else {
             const long long c0 = dbg ? clock64() : 0;
             wait_flag(&fl[0]);  // L_{K,K} and its inverse
@@ -2417,40 +2562,33 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                        __HIP_MEMORY_SCOPE_SYSTEM);
             // PT[s][r] = S[r][s]; QT[s][c] = Linv[c][s] = Dinv[K][s * TLD + c]
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) PT[4 * tc + j][4 * tr + i] = acc[i][j];
-            for (int e = tid; e < 4096; e += 256) QT[e >> 6][e & 63] = ld_sc1(&Dinv[K * 4096 + e]);
+                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc[cb][q];
+            stage_dinv(QT, K);
             __syncthreads();
-            T o[4][4];
+            T o[4][4] = {};
+            mfma_tile<T, false>(PTl, QTl, o, w, lane);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) o[i][j] = (T)0;
-#pragma unroll 4
-            for (int s = 0; s < 64; ++s) {
-                T pa[4], qb[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    pa[i] = PT[s][4 * tr + i];
-                    qb[i] = QT[s][4 * tc + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) o[i][j] = fma_t(pa[i], qb[j], o[i][j]);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = 4 * tr + i, c = 4 * tc + j;
-                    if (in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], o[i][j]);
+                for (int q = 0; q < 4; ++q) {
+                    const int r = rb + 4 * q, c = 16 * cb + cm;
+                    if (in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], o[cb][q]);
                 }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_store(&fl[d], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {
+            // L_{K,K} to the band after the flag: no tile of this kernel reads it
+            // (they take Dinv), so its stores drain with the next tile's
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u, r = e & 63, c = e >> 6;
+                if (r >= c && in_band(I, K, r, c)) st_sc1(&CB[band_idx(I, K, r, c)], PT[r][c]);
+            }
+        }
         if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -2742,6 +2880,14 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
                 fprintf(stderr, "; per diagonal tile: factor %.0f cycles, inverse %.0f; tile (K+1, K) waits %.0f "
                         "for the diagonal", (double)hdbg[4] / hdbg[7], (double)hdbg[5] / hdbg[7],
                         (double)hdbg[6] / hdbg[7]);
+            if (hdbg && hdbg[10])
+                fprintf(stderr, "; chain: wait for K-1 %.0f cycles, sub tile + update %.0f, factor..drained %.0f; "
+                        "diagonal tiles 0..last %.3f ms (100 MHz clock, %.0f us per tile)",
+                        (double)hdbg[8] / hdbg[10], (double)hdbg[9] / hdbg[10], (double)hdbg[11] / hdbg[7],
+                        (hdbg[13] - hdbg[12]) * 1e-5, (hdbg[13] - hdbg[12]) * 1e-2 / (double)hdbg[7]);
+            if (hdbg && hdbg[10])
+                fprintf(stderr, "; sub tile: stage Linv %.0f, product + stores %.0f, drain + flag %.0f",
+                        (double)hdbg[14] / hdbg[10], (double)hdbg[15] / hdbg[10], (double)hdbg[16] / hdbg[10]);
             fprintf(stderr, "\n");
             return;
         }
@@ -2778,13 +2924,17 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > nb64 * DM) grid = nb64 * DM;
     unsigned long long* hdbg = nullptr;
-    if (getenv("BSM_BLK_DEBUG")) BSM_HIP_TRY(hipHostMalloc((void**)&hdbg, 8 * sizeof(unsigned long long), hipHostMallocCoherent));
-    if (hdbg) memset(hdbg, 0, 8 * sizeof(unsigned long long));
+    if (getenv("BSM_BLK_DEBUG")) BSM_HIP_TRY(hipHostMalloc((void**)&hdbg, 24 * sizeof(unsigned long long), hipHostMallocCoherent));
+    if (hdbg) memset(hdbg, 0, 24 * sizeof(unsigned long long));
     g_blk_phase = "blk_chol launch";
-    // BSM_BLK_PANELS=1: the diagonal tile by 16-column panels on four waves
-    // (A/B; 0.76 s at C5 against 0.73 s for the default one-wave factor)
+    // BSM_BLK_PANELS: 1 (default) the diagonal tile by 16-column panels on four
+    // waves, the products on f64 MFMA (C5 0.41 s); 0 the one-wave 64-column
+    // factor, then the block inverse (0.49 s); 3 the tile as 2 x 2 blocks of 32
+    // (0.57 s). Tried and dropped: the 64-column inverse formed on a second
+    // wave behind the factor, meeting it every 8 columns (0.98 s: the factor
+    // waits for the inverse's long rows at the barriers).
     const char* pe = getenv("BSM_BLK_PANELS");
-    const int panels = pe ? atoi(pe) : 0;
+    const int panels = pe ? atoi(pe) : 1;
     blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
                                                panels);
     BSM_HIP_TRY(hipGetLastError());
