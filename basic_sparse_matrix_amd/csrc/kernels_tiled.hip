@@ -329,9 +329,9 @@ __device__ __forceinline__ void k1_load(Stage1<ST>& st, const uint32_t* __restri
     }
 }
 template <int ST>
-__device__ __forceinline__ void k1_gather(Stage1<ST>& st, const double* __restrict__ X) {
+__device__ __forceinline__ void k1_gather(Stage1<ST>& st, const double* __restrict__ X, uint32_t xmask) {
 #pragma unroll
-    for (int j = 0; j < ST; ++j) st.x[j] = X[st.m[j] >> K1_RBITS];
+    for (int j = 0; j < ST; ++j) st.x[j] = X[(st.m[j] >> K1_RBITS) & xmask];
 }
 template <int ST>
 __device__ __forceinline__ void k1_sum(const Stage1<ST>& st, double* yl) {
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw
                                                      const uint32_t* __restrict__ meta,
                                                      const double* __restrict__ val, const double* __restrict__ X,
                                                      double* __restrict__ Y, int32_t* __restrict__ row_nnz,
-                                                     unsigned* bar, bool neg_init) {
+                                                     unsigned* bar, bool neg_init, uint32_t xmask) {
     extern __shared__ double y1lds[];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = threadIdx.x / WAVE;
@@ -374,20 +374,20 @@ __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw
             Stage1<K1_STAGE> S0, S1, S2;
             k1_load(S0, meta, val, c0, lane);
             k1_load(S1, meta, val, c0 + K1_STAGE, lane);
-            k1_gather(S0, X);
+            k1_gather(S0, X, xmask);
             for (; i + K1_GROUP <= c1; i += K1_GROUP) {
                 k1_load(S2, meta, val, i + 2 * K1_STAGE, lane);
-                k1_gather(S1, X);
+                k1_gather(S1, X, xmask);
                 __builtin_amdgcn_sched_barrier(0);
                 k1_sum(S0, yl);
                 __builtin_amdgcn_sched_barrier(0);
                 k1_load(S0, meta, val, i + 3 * K1_STAGE, lane);
-                k1_gather(S2, X);
+                k1_gather(S2, X, xmask);
                 __builtin_amdgcn_sched_barrier(0);
                 k1_sum(S1, yl);
                 __builtin_amdgcn_sched_barrier(0);
                 k1_load(S1, meta, val, i + 4 * K1_STAGE, lane);
-                k1_gather(S0, X);
+                k1_gather(S0, X, xmask);
                 __builtin_amdgcn_sched_barrier(0);
                 k1_sum(S2, yl);
                 __builtin_amdgcn_sched_barrier(0);
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw
         for (; i < c1; ++i) {  // the task's last chunks, one at a time
             const uint32_t m = meta[i * CHUNK + lane];
             const double v = val[i * CHUNK + lane];
-            const double xv = X[m >> K1_RBITS];
+            const double xv = X[(m >> K1_RBITS) & xmask];
             double* yp = yl + (m & K1_RW_MAX);
             *yp = __dadd_rn(*yp, __dmul_rn(v, xv));
         }
@@ -537,9 +537,12 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
     if (t->k == 1) {
         const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(double);
         auto kern = t->stage == 8 ? spmm_tiled_k1<8> : spmm_tiled_k1<4>;
+        // BSM_TILED_K1_PROBE=<mask> (measurement only, wrong results): gather
+        // X[col & mask], e.g. 0 (one line: the stream alone) or 4095 (a 32 KB window)
+        static const uint32_t xmask = env_u32("BSM_TILED_K1_PROBE", 0xffffffffu);
         kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
                                               static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar,
-                                              neg_init);
+                                              neg_init, xmask);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
         spmm_tiled_k32<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
