@@ -2205,6 +2205,40 @@ __device__ __forceinline__ void blk_diag_inverse_blocked(const lds_t<T>* P, lds_
     blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
 }
 
+// Block (p2, p1), p1 < p2, of Linv on one wave (f64 MFMA 16x16x4, as in
+// blk_linv_from_blocks): Linv[p2][p1] = -Di[p2] sum_{q = p1}^{p2 - 1} L[p2][q] Linv[q][p1],
+// from row blocks < p2 of Linv already in Q (Q[c * TLD + r] = Linv[r][c]).
+template <typename T>
+__device__ __forceinline__ void blk_linv_block(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di, int p2, int p1,
+                                               int l) {
+    const int m = l & 15, kq = l >> 4;
+    bsm_d4 t = {0.0, 0.0, 0.0, 0.0};
+    for (int qb = p1; qb < p2; ++qb) {
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const int k = 16 * qb + 4 * k4 + kq;
+            t = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(16 * p2 + m) * TLD + k],
+                                                     (double)Q[(16 * p1 + m) * TLD + k], t, 0, 0, 0);
+        }
+    }
+    bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4)
+        o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)Di[p2 * 256 + m * 16 + 4 * k4 + kq], t[k4], o, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Q[(16 * p1 + m) * TLD + 16 * p2 + kq + 4 * q] = (T)o[q];
+}
+
+// Q's diagonal block p = Di[p] (Di[p][row][col] -> Q[col * TLD + row]), one wave
+template <typename T>
+__device__ __forceinline__ void blk_linv_diag(lds_t<T>* Q, const lds_t<T>* Di, int p, int l) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = l + 64 * u, row = e >> 4, col = e & 15;
+        Q[(16 * p + col) * TLD + 16 * p + row] = Di[p * 256 + e];
+    }
+}
+
 // Factor AND invert the 64 x 64 tile S (P[r * TLD + c], lower part) on all
 // four waves, by 16-column panels p (columns c0 = 16p ...):
 //   1. wave 0 factors the 16 x 16 diagonal block (lane r & 15 = row, pivots
@@ -2213,18 +2247,28 @@ __device__ __forceinline__ void blk_diag_inverse_blocked(const lds_t<T>* P, lds_
 //   2. the rows below: L[i][c0 + j] = sum_t S[i][c0 + t] Di[p][j][t];
 //   3. the trailing lower part: S[i][j] -= sum_t L[i][c0 + t] L[j][c0 + t].
 // Steps 2 and 3 are 16 x 16 blocks on f64 MFMA, one block per wave at a time.
-// Then Linv by block distance: Linv[p2][p1] = -Di[p2] sum_q L[p2][q] Linv[q][p1].
-// Q[c * TLD + r] = Linv[r][c] (zero above the diagonal); rd[r] = 1 / L[r][r].
+// Linv by row blocks: row block p - 1 on waves 1-3 while wave 0 factors
+// block p, the last one at the end. rd[r] = 1 / L[r][r].
 // Every thread of the workgroup must call it (barriers inside).
 template <typename T>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
-                                                int* status, int tid) {
+                                                int* status, int tid, unsigned long long* tdbg = nullptr) {
+    long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
     asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     bool pd = true;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) Q[(tid >> 2) * TLD + 16 * (tid & 3) + u] = (T)0;  // rows of Linv^T
     for (int p = 0; p < 4; ++p) {
         const int c0 = 16 * p;
-        if (w == 0) {
+        const long long t0 = tdbg ? clock64() : 0;
+        if (w > 0) {
+            // while wave 0 factors block p: Linv's row block p - 1 (its blocks
+            // need row blocks < p - 1, Di[p - 1] and L's columns < p - 1, all
+            // complete) and diagonal block p - 1
+            if (p >= 2 && w - 1 < p - 1) blk_linv_block<T>(P, Q, Di, p - 1, w - 1, tid & 63);
+            if (p >= 1 && w == 3) blk_linv_diag<T>(Q, Di, p - 1, tid & 63);
+        } else {
             const int r = tid & 15;
             T dv[16], rps[16];
 #pragma unroll
@@ -2263,6 +2307,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
         }
         __syncthreads();
+        const long long t1 = tdbg ? clock64() : 0;
         // 2. rows below the block, one 16-row block per wave on f64 MFMA
         //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
         const int l = tid & 63, m = l & 15, kq = l >> 4;
@@ -2279,6 +2324,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int q = 0; q < 4; ++q) P[(r0 + kq + 4 * q) * TLD + c0 + m] = (T)o[q];
         }
         __syncthreads();
+        const long long t2 = tdbg ? clock64() : 0;
         // 3. the trailing lower part by 16 x 16 blocks (pi, pj), p < pj <= pi:
         //    S[pi][pj] -= L[pi][p] L[pj][p]^T, blocks dealt to the waves in turn
         const int nbk = 3 - p;
@@ -2299,9 +2345,23 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
         }
         __syncthreads();
+        if (tdbg) {
+            const long long t3 = clock64();
+            ta += t1 - t0;
+            tb += t2 - t1;
+            tc += t3 - t2;
+        }
     }
+    // Linv's last row block and diagonal block
+    if (w < 3) blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
+    else blk_linv_diag<T>(Q, Di, 3, tid & 63);
+    __syncthreads();
     if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
-    blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
+    if (tdbg && tid == 0) {
+        __hip_atomic_fetch_add(&tdbg[17], (unsigned long long)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&tdbg[18], (unsigned long long)tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&tdbg[19], (unsigned long long)tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // X[cb][q] (element (row 16w + (lane >> 4) + 4q, column 16cb + (lane & 15)) of
@@ -2310,7 +2370,8 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
 // (A operand: lane l holds A[l & 15][l >> 4]; B: B[l >> 4][l & 15]). Two LDS
 // reads per 4 x 16 x 16 FMAs instead of eight per 16 on the VALU. f32 tiles
 // are carried in f64.
-template <typename T, bool NEG>
+// TRI_B: B[k][c] = 0 for k > c (B = Linv^T), so column block cb stops at k = 16cb + 15.
+template <typename T, bool NEG, bool TRI_B = false>
 __device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B, T (&X)[4][4], int w, int lane) {
     bsm_d4 c[4];
 #pragma unroll
@@ -2318,14 +2379,16 @@ __device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B,
 #pragma unroll
         for (int q = 0; q < 4; ++q) c[cb][q] = (double)X[cb][q];
     const int kq = lane >> 4, m = lane & 15;
-#pragma unroll 4
+#pragma unroll
     for (int k4 = 0; k4 < 16; ++k4) {
         const int k = 4 * k4 + kq;
         double a = (double)AT[k * TLD + 16 * w + m];
         if (NEG) a = -a;
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
-            c[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)B[k * TLD + 16 * cb + m], c[cb], 0, 0, 0);
+            if (!TRI_B || k4 < 4 * (cb + 1))
+                c[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)B[k * TLD + 16 * cb + m], c[cb], 0, 0, 0);
+        if ((k4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // operand loads of 4 k-steps in flight, not all 16
     }
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
@@ -2337,7 +2400,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                 T* __restrict__ Dinv, int* __restrict__ flags,
                                                 int* __restrict__ ticket, int* __restrict__ status,
-                                                unsigned long long* __restrict__ dbg, int panels) {
+                                                unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
+                                                int panels) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
     __shared__ T rd[64];
@@ -2460,18 +2524,18 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
         long long cw0 = 0, cw1 = 0, cs1 = 0, cs2 = 0, cs3 = 0;  // BSM_BLK_DEBUG: the chain's steps
         if (sub) {
             // L_{K,K-1} = S_{K,K-1} L_{K-1,K-1}^-T once diagonal tile K - 1 is done
-            if (dbg) cw0 = clock64();
+            if (tdbg) cw0 = clock64();
             wait_flag(&flags[(K - 1) * DM]);
-            if (dbg) cw1 = clock64();
+            if (tdbg) cw1 = clock64();
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
             stage_dinv(QT, K - 1);
             __syncthreads();
-            if (dbg) cs1 = clock64();
+            if (tdbg) cs1 = clock64();
             T o[4][4] = {};
-            mfma_tile<T, false>(PTl, QTl, o, w, lane);
+            mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -2479,11 +2543,11 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                     const int r = rb + 4 * q, c = 16 * cb + cm;
                     if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
                 }
-            if (dbg) cs2 = clock64();
+            if (tdbg) cs2 = clock64();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (dbg) cs3 = clock64();
+            if (tdbg) cs3 = clock64();
             // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t]
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
@@ -2494,7 +2558,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             __syncthreads();
         }
         if (d == 0) {
-            const long long c0 = dbg ? clock64() : 0;
+            const long long c0 = tdbg ? clock64() : 0;
             // S to LDS (PT[r][c]), then wave 0 factors it: lane r holds row r
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
@@ -2506,34 +2570,35 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                 (lds_t<T>*)Di, status, tid);
             } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default)
                 blk_diag_panels<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
-                                   (lds_t<T>*)rd, status, tid);
+                                   (lds_t<T>*)rd, status, tid, tdbg);
             } else {  // one-wave factor; the inverse below
                 if (w == 0)
                     blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
                 __syncthreads();
             }
-            const long long c1 = dbg ? clock64() : 0;
+            const long long c1 = tdbg ? clock64() : 0;
             if (!panels)
                 blk_diag_inverse_blocked<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
                                             tid);
+
             __syncthreads();
-            if (dbg && tid == 0) {  // cycles: factor, inverse (BSM_BLK_DEBUG)
+            if (tdbg && tid == 0) {  // cycles: factor, inverse (BSM_BLK_DEBUG)
                 const long long c2 = clock64();
-                __hip_atomic_fetch_add(&dbg[4], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_fetch_add(&dbg[5], (unsigned long long)(c2 - c1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_fetch_add(&dbg[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_fetch_add(&tdbg[4], (unsigned long long)(c1 - c0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&tdbg[5], (unsigned long long)(c2 - c1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&tdbg[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (sub) {  // the chain: waiting for tile K - 1, then the sub-diagonal tile and its update
-                    __hip_atomic_fetch_add(&dbg[8], (unsigned long long)(cw1 - cw0), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_fetch_add(&dbg[9], (unsigned long long)(c0 - cw1), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_fetch_add(&dbg[10], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_fetch_add(&dbg[14], (unsigned long long)(cs1 - cw1), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_fetch_add(&dbg[15], (unsigned long long)(cs2 - cs1), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_fetch_add(&dbg[16], (unsigned long long)(cs3 - cs2), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&tdbg[8], (unsigned long long)(cw1 - cw0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[9], (unsigned long long)(c0 - cw1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[10], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[14], (unsigned long long)(cs1 - cw1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[15], (unsigned long long)(cs2 - cs1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[16], (unsigned long long)(cs3 - cs2), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]
@@ -2542,24 +2607,24 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 const int e = tid + 256 * u;
                 st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
             }
-            if (dbg) {  // the publication: stores drained, then the flag (below)
+            if (tdbg) {  // the publication: stores drained, then the flag (below)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (tid == 0) {
                     const long long c3 = clock64();
-                    __hip_atomic_fetch_add(&dbg[11], (unsigned long long)(c3 - c0), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_fetch_add(&tdbg[11], (unsigned long long)(c3 - c0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                     // clock calibration: the constant 100 MHz counter at each diagonal tile's end
                     const unsigned long long wc = wall_clock64();
-                    if (K == 0) __hip_atomic_store(&dbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (K == nb64 - 1) __hip_atomic_store(&dbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (K == 0) __hip_atomic_store(&tdbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (K == nb64 - 1) __hip_atomic_store(&tdbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         } else {
-            const long long c0 = dbg ? clock64() : 0;
+            const long long c0 = tdbg ? clock64() : 0;
             wait_flag(&fl[0]);  // L_{K,K} and its inverse
-            if (dbg && tid == 0 && d == 1)
-                __hip_atomic_fetch_add(&dbg[6], (unsigned long long)(clock64() - c0), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tdbg && tid == 0 && d == 1)
+                __hip_atomic_fetch_add(&tdbg[6], (unsigned long long)(clock64() - c0), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             // PT[s][r] = S[r][s]; QT[s][c] = Linv[c][s] = Dinv[K][s * TLD + c]
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
@@ -2568,7 +2633,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             stage_dinv(QT, K);
             __syncthreads();
             T o[4][4] = {};
-            mfma_tile<T, false>(PTl, QTl, o, w, lane);
+            mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -2871,23 +2936,26 @@ static void blk_watch_stop() { ++g_blk_gen; }
 // progress (mapped host counters) and end the process (a hung kernel would
 // otherwise hold the test until its timeout)
 static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hdbg, long long tickets,
-                         long long grid) {
+                         long long grid, const unsigned long long* tdev = nullptr) {
     if (!getenv("BSM_BLK_DEBUG")) return;
     for (int i = 0; i < 200; ++i) {
         if (hipStreamQuery(s) == hipSuccess) {
             fprintf(stderr, "[blk debug] %s done: tickets %lld grid %lld", what, tickets, grid);
-            if (hdbg && hdbg[7])
-                fprintf(stderr, "; per diagonal tile: factor %.0f cycles, inverse %.0f; tile (K+1, K) waits %.0f "
-                        "for the diagonal", (double)hdbg[4] / hdbg[7], (double)hdbg[5] / hdbg[7],
-                        (double)hdbg[6] / hdbg[7]);
-            if (hdbg && hdbg[10])
-                fprintf(stderr, "; chain: wait for K-1 %.0f cycles, sub tile + update %.0f, factor..drained %.0f; "
-                        "diagonal tiles 0..last %.3f ms (100 MHz clock, %.0f us per tile)",
-                        (double)hdbg[8] / hdbg[10], (double)hdbg[9] / hdbg[10], (double)hdbg[11] / hdbg[7],
-                        (hdbg[13] - hdbg[12]) * 1e-5, (hdbg[13] - hdbg[12]) * 1e-2 / (double)hdbg[7]);
-            if (hdbg && hdbg[10])
-                fprintf(stderr, "; sub tile: stage Linv %.0f, product + stores %.0f, drain + flag %.0f",
-                        (double)hdbg[14] / hdbg[10], (double)hdbg[15] / hdbg[10], (double)hdbg[16] / hdbg[10]);
+            unsigned long long t[24] = {};
+            if (tdev && hipMemcpy(t, tdev, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) t[7] = t[10] = 0;
+            if (t[7])
+                fprintf(stderr, "; per diagonal tile: factor %.0f cycles, inverse %.0f, factor..drained %.0f; "
+                        "diagonal tiles 0..last %.3f ms (100 MHz clock, %.2f us per tile)",
+                        (double)t[4] / t[7], (double)t[5] / t[7], (double)t[11] / t[7], (t[13] - t[12]) * 1e-5,
+                        (t[13] - t[12]) * 1e-2 / (double)t[7]);
+            if (t[10])
+                fprintf(stderr, "; chain: waits for K-1 %.0f, from K-1 visible to the factor %.0f (stage Linv %.0f, "
+                        "product + stores %.0f, drain + flag %.0f, update the rest)",
+                        (double)t[8] / t[10], (double)t[9] / t[10], (double)t[14] / t[10], (double)t[15] / t[10],
+                        (double)t[16] / t[10]);
+            if (t[7] && t[17])
+                fprintf(stderr, "; panel factor: wave 0's blocks %.0f, rows below %.0f, trailing %.0f",
+                        (double)t[17] / t[7], (double)t[18] / t[7], (double)t[19] / t[7]);
             fprintf(stderr, "\n");
             return;
         }
@@ -2923,9 +2991,19 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_chol does not fit a CU");
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > nb64 * DM) grid = nb64 * DM;
+    // BSM_BLK_DEBUG=1: watchdog counters in host memory and chain timers;
+    // =2: the chain timers alone (device memory: no PCIe atomics on the chain)
     unsigned long long* hdbg = nullptr;
-    if (getenv("BSM_BLK_DEBUG")) BSM_HIP_TRY(hipHostMalloc((void**)&hdbg, 24 * sizeof(unsigned long long), hipHostMallocCoherent));
-    if (hdbg) memset(hdbg, 0, 24 * sizeof(unsigned long long));
+    DBuf tdb;
+    const char* dbe = getenv("BSM_BLK_DEBUG");
+    if (dbe && atoi(dbe) != 2) {
+        BSM_HIP_TRY(hipHostMalloc((void**)&hdbg, 24 * sizeof(unsigned long long), hipHostMallocCoherent));
+        memset(hdbg, 0, 24 * sizeof(unsigned long long));
+    }
+    if (dbe) {
+        BSM_TRY(tdb.alloc(24 * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(tdb.p, 0, 24 * sizeof(unsigned long long), s));
+    }
     g_blk_phase = "blk_chol launch";
     // BSM_BLK_PANELS: 1 (default) the diagonal tile by 16-column panels on four
     // waves, the products on f64 MFMA (C5 0.41 s); 0 the one-wave 64-column
@@ -2936,10 +3014,10 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const char* pe = getenv("BSM_BLK_PANELS");
     const int panels = pe ? atoi(pe) : 1;
     blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
-                                               panels);
+                                               tdb.as<unsigned long long>(), panels);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
-    blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid);
+    blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());
     g_blk_phase = "blk_chol sync";
     int h = 0;
     BSM_HIP_TRY(read_dev(&h, st, sizeof(int), s));

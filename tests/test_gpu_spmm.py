@@ -86,8 +86,23 @@ def test_mul_dense_s_matches_mul_dense(golden):
     s = Csr.from_data(g["rows"])
     ds = DenseS.from_data(g["x_cols"])
     assert s.mul_dense_s(ds) == s.mul_dense(Dense.from_data(g["x_cols"]))
+    assert s.mul_dense_s(ds) == Csr.from_data(g["out_rows"])  # the golden itself (sparse.rs:1106-1108)
     with pytest.raises(MatErr):
         s.mul_dense_s(DenseS.new_default(3, 2, np.int32))
+
+
+@pytest.mark.parametrize("dtype,k", [(np.float64, 1), (np.float64, 32), (np.float32, 5), (np.int64, 3)])
+def test_mul_dense_s_random_vs_oracle(orc, dtype, k):
+    """mul_dense_s (sparse.rs:448-466) against the oracle's mul_dense on the
+    same columns, not against the GPU's own mul_dense."""
+    dt = np.dtype(dtype)
+    vk = orc.VAL_UNIFORM if dt.kind == "f" else orc.VAL_SMALLINT
+    rows, n_cols = 900, 400
+    rp, ci, v = orc.gen_csr(300 + k, rows, n_cols, kind=orc.ROWLEN_UNIFORM, a=0, b=30, value_kind=vk, dtype=dt)
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    x_cols = orc.gen_x_cols(301 + k, n_cols, k, value_kind=vk, dtype=dt)
+    ds = DenseS.from_data([list(c) for c in x_cols], dtype=dt)
+    assert_csr_bits(a.mul_dense_s(ds), *orc.mul_dense(rows, n_cols, rp, ci, v, x_cols))
 
 
 # ----------------------------------------------------- randomized parity
