@@ -126,12 +126,15 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
 }
 
 // Lane j of each 16-lane row to the whole row (DPP row_newbcast:j, gfx90a+; the
-// one DPP form 64-bit data may use): a VALU move, no LDS, no SGPR.
+// one DPP form 64-bit data may use): a VALU move, no LDS, no SGPR. Full masks
+// and bound_ctrl make the old value dead, so a double is ONE v_mov_b64_dpp
+// (with old = 0 and no bound_ctrl it was two v_mov_b32_dpp after two moves
+// initialising the destination).
 template <int J> __device__ __forceinline__ int rowbcast_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, true);
 }
 template <int J> __device__ __forceinline__ double rowbcast(double v) {
-    return __hiloint2double(rowbcast_i<J>(__double2hiint(v)), rowbcast_i<J>(__double2loint(v)));
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
 }
 template <int J> __device__ __forceinline__ float rowbcast(float v) {
     return __int_as_float(rowbcast_i<J>(__float_as_int(v)));
@@ -2290,6 +2293,9 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
 #pragma unroll
             for (int j = 0; j < 16; ++j) P[(c0 + r) * TLD + c0 + j] = j <= r ? dv[j] : (T)0;
             // inverse of the block: lane r forms column r; L[q2][q] of row q2 by row broadcast
+            // (re-broadcast: opaque rows keep the factor's 120 broadcasts from living on in AGPRs)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(dv[j]));
             T x[16];
             auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
                 T s = (T)0;
