@@ -1585,7 +1585,8 @@ __global__ __launch_bounds__(256) void band_to_csr(int64_t n, int64_t b, int64_t
 // forward: one workgroup per RHS column, 256-row blocks; far entries (col <
 // block start) summed first per row, then in-block entries column by column;
 // entries with col >= row read y == 0 in the reference (not yet computed) and
-// contribute +-0: skipped. Divisor = LAST stored entry of the row.
+// contribute +-0: skipped, unless one is inf/NaN (v * 0 = NaN: y[i] = NaN).
+// Divisor = LAST stored entry of the row.
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(FW_BLOCK) void csr_forward(int64_t n, const int64_t* __restrict__ rp,
@@ -1601,17 +1602,19 @@ __global__ __launch_bounds__(FW_BLOCK) void csr_forward(int64_t n, const int64_t
         const int64_t i = i0 + t;
         T s = A::zero();
         int64_t e = 0, e1 = 0;
+        bool tail_nan = false;  // an inf/NaN entry past the diagonal: its v * 0 is NaN
         if (i < n) {
             e = rp[i];
             e1 = rp[i + 1];
             if (e == e1) atomicOr(status, ST_EMPTY_ROW);
+            for (int64_t q = e1 - 1; q >= e && col[q] > i; --q) tail_nan |= !isfinite(val[q]);
             for (; e < e1 && col[e] < i0; ++e) s = A::add(s, A::mul(val[e], ld_sc1(&yc[col[e]])));
         }
         const int64_t nb = (n - i0 < FW_BLOCK) ? n - i0 : FW_BLOCK;
         for (int64_t tt = 0; tt < nb; ++tt) {
             const int64_t j = i0 + tt;
             if (t == tt && e1 > rp[i]) {
-                const T y = div_rn(A::sub(bc[i], s), val[e1 - 1]);
+                const T y = div_rn(A::sub(bc[i], tail_nan ? T(NAN) : s), val[e1 - 1]);
                 s_y[tt] = y;
                 st_sc1(&yc[i], y);
             } else if (t == tt) {
@@ -2919,6 +2922,174 @@ int band_to_csr_host(const Band& bd, int dtype, bsm_csr** out, hipStream_t s) {
     return BSM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// General exact Cholesky (dense, n <= CHOL_GENERAL_MAX): the inputs the band
+// kernels refuse -- a pivot <= 0 or not finite (the reference stores the NaN /
+// inf that powf(0.5) and 1/0 give and carries on, sparse.rs:703-710), rows
+// with unsorted or duplicate columns (get_row_complete's shifted vector,
+// sparse.rs:267-294), or a band too wide for the band kernels. A non-finite
+// pivot makes every later L[i][j] non-zero, so L is dense there: this path
+// keeps L dense, column-major (Lc[k*n + i] = L[i][k]), and runs the literal
+// loop nest of sparse.rs:687-711 one column per launch, every element's sum
+// in ascending k with every product kept (no band shortcut).
+// ---------------------------------------------------------------------------
+constexpr int64_t CHOL_GENERAL_MAX = 16384;
+
+// A as get_row_complete(i) presents it (sparse.rs:279-292): entry p lands at
+// position pos, which gains (col - prev_col) padding zeros when col > prev_col
+// and then 1; prev_col = col + 1. Positions increase strictly within a row.
+// Positions >= n are never read (j <= i < n). Ad is column-major.
+template <typename T>
+__global__ __launch_bounds__(256) void complete_rows(int64_t n, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ col, const T* __restrict__ v,
+                                                     T* __restrict__ Ad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t pos = 0, prev = 0;
+    for (int64_t p = rp[i]; p < rp[i + 1]; ++p) {
+        const int64_t c = col[p];
+        if (c > prev) pos += c - prev;
+        prev = c + 1;
+        if (pos >= n) break;
+        Ad[pos * n + i] = v[p];
+        ++pos;
+    }
+}
+
+// the zero-skipping insert (sparse.rs:229): a zero is not stored and reads
+// back as T::default() = +0
+template <typename T> __device__ __forceinline__ T stored(T v) { return v == T(0) ? T(0) : v; }
+
+// L[0][0] = powf(A[0][0], 0.5)
+template <typename T> __global__ void gchol_pivot0(const T* __restrict__ Ad, T* __restrict__ Lc) {
+    if (threadIdx.x == 0) Lc[0] = stored(pow_half(Ad[0]));
+}
+
+// column j: L[i][j] = (1 / L[j][j]) * (A[i][j] - sum_k<j L[i][k] L[j][k]) for
+// i > j (one thread per row); the thread of row j+1 then forms pivot
+// L[j+1][j+1] = powf(A[j+1][j+1] - sum_k<=j L[j+1][k]^2, 0.5), which the next
+// launch reads.
+template <typename T>
+__global__ __launch_bounds__(256) void gchol_column(int64_t n, int64_t j, const T* __restrict__ Ad,
+                                                    T* __restrict__ Lc) {
+    using A = Arith<T>;
+    const int64_t i = j + 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    T sum = A::zero();
+#pragma unroll 8
+    for (int64_t k = 0; k < j; ++k) sum = A::add(sum, A::mul(Lc[k * n + i], Lc[k * n + j]));
+    const T lij = stored(A::mul(div_rn(T(1), Lc[j * n + j]), A::sub(Ad[j * n + i], sum)));
+    Lc[j * n + i] = lij;
+    if (i == j + 1) {
+        T s2 = A::zero();
+#pragma unroll 8
+        for (int64_t k = 0; k < j; ++k) s2 = A::add(s2, A::mul(Lc[k * n + i], Lc[k * n + i]));
+        s2 = A::add(s2, A::mul(lij, lij));
+        Lc[i * n + i] = stored(pow_half(A::sub(Ad[i * n + i], s2)));
+    }
+}
+
+// per row of L: stored entries (j <= i, value != 0; NaN counts) and the first
+// stored column
+template <typename T>
+__global__ __launch_bounds__(256) void gchol_row_count(int64_t n, const T* __restrict__ Lc, int32_t* __restrict__ cnt,
+                                                       int32_t* __restrict__ first) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t c = 0, f = INT32_MAX;
+    for (int64_t j = 0; j <= i; ++j)
+        if (Lc[j * n + i] != T(0)) {
+            if (!c) f = (int32_t)j;
+            ++c;
+        }
+    cnt[i] = c;
+    first[i] = f;
+}
+
+// sparse.rs:707 `l.get_row_complete(j).unwrap()` is None when no row >= j of
+// the partial L is registered yet: row j empty and row j+1 has nothing stored
+// before column j (longer runs of empty rows contain this case).
+__global__ __launch_bounds__(256) void gchol_unregistered(int64_t n, const int32_t* __restrict__ cnt,
+                                                          const int32_t* __restrict__ first, int* status) {
+    const int64_t j = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j + 1 >= n) return;
+    if (cnt[j] == 0 && first[j + 1] >= j) atomicOr(status, ST_EMPTY_ROW);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gchol_to_csr(int64_t n, const T* __restrict__ Lc, const int64_t* __restrict__ rp,
+                                                    int32_t* __restrict__ col, T* __restrict__ val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t e = rp[i];
+    for (int64_t j = 0; j <= i; ++j) {
+        const T v = Lc[j * n + i];
+        if (v != T(0)) {
+            col[e] = (int32_t)j;
+            val[e] = v;
+            ++e;
+        }
+    }
+}
+
+template <typename T>
+int chol_general(const bsm_csr* a, int dtype, bsm_csr** out, hipStream_t s) {
+    const int64_t n = (int64_t)a->rows;
+    const size_t nn = (size_t)n * (size_t)n;
+    DBuf ad, lc, cnt, first, ws, rp, st;
+    BSM_TRY(ad.alloc(nn * sizeof(T)));
+    BSM_TRY(lc.alloc(nn * sizeof(T)));
+    BSM_TRY(cnt.alloc(n * sizeof(int32_t)));
+    BSM_TRY(first.alloc(n * sizeof(int32_t)));
+    BSM_TRY(ws.alloc(scan_workspace_bytes(n)));
+    BSM_TRY(rp.alloc((n + 1) * sizeof(int64_t)));
+    BSM_TRY(st.alloc(16));
+    BSM_HIP_TRY(hipMemsetAsync(ad.p, 0, nn * sizeof(T), s));
+    BSM_HIP_TRY(hipMemsetAsync(lc.p, 0, nn * sizeof(T), s));
+    BSM_HIP_TRY(hipMemsetAsync(st.p, 0, 16, s));
+    complete_rows<T><<<nblk(n, 256), 256, 0, s>>>(n, a->row_ptr, a->col, static_cast<const T*>(a->vals), ad.as<T>());
+    gchol_pivot0<T><<<1, 64, 0, s>>>(ad.as<T>(), lc.as<T>());
+    for (int64_t j = 0; j + 1 < n; ++j)
+        gchol_column<T><<<nblk(n - j - 1, 256), 256, 0, s>>>(n, j, ad.as<T>(), lc.as<T>());
+    gchol_row_count<T><<<nblk(n, 256), 256, 0, s>>>(n, lc.as<T>(), cnt.as<int32_t>(), first.as<int32_t>());
+    if (n > 2)
+        gchol_unregistered<<<nblk(n - 2, 256), 256, 0, s>>>(n, cnt.as<int32_t>(), first.as<int32_t>(), st.as<int>());
+    BSM_HIP_TRY(hipGetLastError());
+    int h = 0;
+    BSM_HIP_TRY(read_dev(&h, st.p, sizeof(int), s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    BSM_REQUIRE(!(h & ST_EMPTY_ROW), BSM_ERR_PANIC,
+                "cholesky: called `Option::unwrap()` on a `None` value (sparse.rs:707: no row >= j of L stored)");
+    BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), rp.as<int64_t>(), n, ws.p, ws.bytes, s));
+    int64_t nnz = 0;
+    BSM_HIP_TRY(read_dev(&nnz, rp.as<int64_t>() + n, sizeof(int64_t), s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    auto* m = new bsm_csr();
+    m->dtype = dtype;
+    m->rows = m->cols = (uint64_t)n;
+    m->nnz = (uint64_t)nnz;
+    BSM_HIP_TRY(hipGetDevice(&m->device));
+    DBuf c, v;
+    int rc = c.alloc((uint64_t)nnz * sizeof(int32_t));
+    if (rc == BSM_OK) rc = v.alloc((uint64_t)nnz * sizeof(T));
+    if (rc != BSM_OK) { delete m; return rc; }
+    m->row_ptr = static_cast<int64_t*>(rp.release());
+    m->col = static_cast<int32_t*>(c.release());
+    m->vals = v.release();
+    m->analysed = true;
+    m->rows_sorted = true;
+    gchol_to_csr<T><<<nblk(n, 256), 256, 0, s>>>(n, lc.as<T>(), m->row_ptr, m->col, static_cast<T*>(m->vals));
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        bsm_csr_free(m);
+        set_error("cholesky (general): %s", hipGetErrorString(e));
+        return BSM_ERR_HIP;
+    }
+    *out = m;
+    return BSM_OK;
+}
+
 // BSM_BLK_WATCH: a passive host thread that names the step a blocked solve
 // is in if it takes longer than 15 s, then ends the process (no GPU calls)
 static std::atomic<const char*> g_blk_phase{"idle"};
@@ -3055,11 +3226,24 @@ static int from_colmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor
     return pack_cols_to_rowmajor(dtype, n, k, colmajor, rowmajor, s);
 }
 
+// the general exact path takes what the band kernels refuse (non-finite or
+// non-positive pivots, unsorted rows, too wide a band) when L fits densely;
+// BSM_CHOL_GENERAL=1 forces it (A/B against the band kernels)
+static bool chol_general_forced(const bsm_csr* a) {
+    const char* e = getenv("BSM_CHOL_GENERAL");
+    return e && atoi(e) == 1 && a->rows >= 1 && (int64_t)a->rows <= CHOL_GENERAL_MAX;
+}
+static bool chol_general_fits(const bsm_csr* a) { return a->rows >= 1 && (int64_t)a->rows <= CHOL_GENERAL_MAX; }
+
 int solve_dispatch_cholesky(const bsm_csr* a, bsm_csr** out, hipStream_t s) {
     auto run = [&]<typename T>() -> int {
-        Band bd;
-        BSM_TRY(band_factor<T>(a, bd, s));
-        return band_to_csr_host<T>(bd, a->dtype, out, s);
+        if (!chol_general_forced(a)) {
+            Band bd;
+            const int rc = band_factor<T>(a, bd, s);
+            if (rc == BSM_OK) return band_to_csr_host<T>(bd, a->dtype, out, s);
+            if (rc != BSM_ERR_UNSUPPORTED || !chol_general_fits(a)) return rc;
+        }
+        return chol_general<T>(a, a->dtype, out, s);
     };
     if (a->dtype == BSM_F64) return run.template operator()<double>();
     if (a->dtype == BSM_F32) return run.template operator()<float>();
@@ -3113,6 +3297,27 @@ int solve_dispatch_trsv(const bsm_csr* m, bool lower, uint64_t k, uint64_t n, co
     if (m->dtype == BSM_F32) return run.template operator()<float>();
     set_error("triangular solve: f32/f64 only");
     return BSM_ERR_INVALID;
+}
+
+// solve (lib.rs:11-24) on the general factor: L dense-exact, L* =
+// transpose, then the general-CSR forward and backward solves, which divide
+// by the last / first stored entry of each row as the reference does
+template <typename T>
+static int solve_general(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
+    bsm_csr* l = nullptr;
+    bsm_csr* lt = nullptr;
+    BSM_TRY(chol_general<T>(a, a->dtype, &l, s));
+    stage_mark("cholesky", s);
+    int rc = transpose_dispatch(l, &lt, s);
+    DBuf y;
+    if (rc == BSM_OK) rc = y.alloc(n * k * sizeof(T));
+    if (rc == BSM_OK) rc = solve_dispatch_trsv(l, true, k, n, b_dev, y.p, s);
+    if (rc == BSM_OK) stage_mark("forward", s);
+    if (rc == BSM_OK) rc = solve_dispatch_trsv(lt, false, k, n, y.p, x_dev, s);
+    if (rc == BSM_OK) stage_mark("backward", s);
+    bsm_csr_free(l);
+    if (lt) bsm_csr_free(lt);
+    return rc;
 }
 
 // band backward solve: the lane-hopping chain (band_backward_hop) for b up
@@ -3178,7 +3383,13 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
                     (unsigned long long)n, (unsigned long long)a->rows);
         stage_reset(s);
         Band bd;
-        BSM_TRY(band_factor<T>(a, bd, s));
+        const int frc = chol_general_forced(a) ? BSM_ERR_UNSUPPORTED : band_factor<T>(a, bd, s);
+        if (frc == BSM_ERR_UNSUPPORTED && chol_general_fits(a)) {
+            bd.cb.reset();
+            bd.r.reset();
+            return solve_general<T>(a, k, n, b_dev, x_dev, s);
+        }
+        BSM_TRY(frc);
         // the reference's forward pass divides by the LAST stored entry of
         // each L row and its backward pass by the FIRST of each L^T row: with
         // every pivot > 0 (checked) both are L_ii, as used below.
