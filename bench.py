@@ -397,15 +397,15 @@ def main():
     else:
         log(f"rank {rank}: panel width {panel_cols} ({n_passes} passes), plan {plan_ms:.1f} ms")
 
-    ev_k0 = torch.cuda.Event(enable_timing=True)
-    ev_k1 = torch.cuda.Event(enable_timing=True)
-    ev_c0 = torch.cuda.Event(enable_timing=True)
-    ev_c1 = torch.cuda.Event(enable_timing=True)
+    # one set of events per timed step, read after the timed region: no host
+    # synchronisation between steps (small configs would time the bubble)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     kern_ms, comm_ms, comp_ms = [], [], []
     round_rows = world * cr
 
     def step(timed):
         if timed:
+            ev_k0, ev_k1, ev_c0, ev_c1 = evs[timed - 1]
             ev_k0.record()
         works = []
         for c, b in enumerate(blks):
@@ -432,17 +432,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-        torch.cuda.synchronize()  # events of this step are complete
-        kern_ms.append(ev_k0.elapsed_time(ev_k1))
-        comm_ms.append(ev_k1.elapsed_time(ev_c0))
-        comp_ms.append(ev_c0.elapsed_time(ev_c1))
+    for i in range(args.steps):
+        step(i + 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    for ev_k0, ev_k1, ev_c0, ev_c1 in evs:
+        kern_ms.append(ev_k0.elapsed_time(ev_k1))
+        comm_ms.append(ev_k1.elapsed_time(ev_c0))
+        comp_ms.append(ev_c0.elapsed_time(ev_c1))
     if world > 1:
         t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -137,7 +137,11 @@ int bsm_csr_sub_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out);
  * order) with row j of b.transpose(), kept when nonzero. */
 int bsm_csr_mul_sparse(const bsm_csr* a, const bsm_csr* b, bsm_csr** out);
 /* impl Csr<f32>::cholesky_decomp (sparse.rs:682-714); F64 is this build's
- * addition. Square check -> BSM_ERR_NON_SQUARE. */
+ * addition. Square check -> BSM_ERR_NON_SQUARE.
+ * Non-SPD inputs store the reference's NaN/inf, unsorted rows are read as
+ * get_row_complete does, the :707 unwrap on an unregistered L row ->
+ * BSM_ERR_PANIC; those (and bands > 1073) need n <= 16384, else
+ * BSM_ERR_UNSUPPORTED. bsm_solve follows the same rules. */
 int bsm_csr_cholesky(const bsm_csr* a, bsm_csr** out);
 /* forward_substitution (lib.rs:28-46): solve L y = b for k RHS columns of n. */
 int bsm_forward_substitution(const bsm_csr* l, uint64_t k, uint64_t n,
