@@ -689,6 +689,28 @@ __global__ __launch_bounds__(256) void compact_wave(int64_t rows, int k, const T
     }
 }
 
+// k <= 32: KL = pow2 >= k lanes per row, 64 / KL rows per wave (C3's k = 32:
+// two rows per wave instead of one with half the lanes idle)
+template <typename T, int KL>
+__global__ __launch_bounds__(256) void compact_seg(int64_t rows, int k, const T* __restrict__ Y,
+                                                   const int64_t* __restrict__ out_rp, int32_t* __restrict__ out_col,
+                                                   T* __restrict__ out_val) {
+    using A = Arith<T>;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int j = lane & (KL - 1);
+    const int64_t row = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE)) * (WAVE / KL) + lane / KL;
+    const bool in = row < rows && j < k;
+    const T v = in ? Y[row * (int64_t)k + j] : A::zero();
+    const bool keep = in && A::nz(v);
+    const uint64_t m = __ballot(keep);
+    if (keep) {
+        const uint64_t seg = (KL == 64 ? ~0ull : ((1ull << KL) - 1)) << (lane & ~(KL - 1));
+        const int64_t p = out_rp[row] + __popcll(m & seg & lanemask_lt(lane));
+        out_col[p] = j;
+        out_val[p] = v;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void compact_k1(int64_t rows, const T* __restrict__ y,
                                                   const int64_t* __restrict__ out_rp,
@@ -1195,6 +1217,16 @@ int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const 
         if (k == 1) {
             compact_k1<T><<<grid1d(rows, 256), 256, 0, s>>>((int64_t)rows, static_cast<const T*>(y),
                                                            out_rp, out_col, static_cast<T*>(out_vals));
+        } else if (k <= 32) {
+            auto seg = [&]<int KL>() {
+                compact_seg<T, KL><<<grid1d(rows, 4 * (WAVE / KL)), 256, 0, s>>>(
+                    (int64_t)rows, (int)k, static_cast<const T*>(y), out_rp, out_col, static_cast<T*>(out_vals));
+            };
+            if (k <= 2) seg.template operator()<2>();
+            else if (k <= 4) seg.template operator()<4>();
+            else if (k <= 8) seg.template operator()<8>();
+            else if (k <= 16) seg.template operator()<16>();
+            else seg.template operator()<32>();
         } else {
             compact_wave<T><<<grid1d(rows, 4), 256, 0, s>>>((int64_t)rows, (int)k,
                                                            static_cast<const T*>(y), out_rp, out_col,
