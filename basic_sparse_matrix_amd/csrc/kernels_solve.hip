@@ -2553,18 +2553,20 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                     if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
                 }
             if (tdbg) cs2 = clock64();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tdbg) cs3 = clock64();
-            // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t]
+            // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t].
+            // The stores above drain meanwhile: the tile's flag (read by tiles
+            // below, not by this chain) goes out after the update.
+            __syncthreads();  // every wave has read PT (the product) before it is overwritten
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = o[cb][q];
             __syncthreads();
             mfma_tile<T, true>(PTl, PTl, acc, w, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tdbg) cs3 = clock64();
         }
         if (d == 0) {
             const long long c0 = tdbg ? clock64() : 0;
@@ -3127,7 +3129,7 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
                         (t[13] - t[12]) * 1e-2 / (double)t[7]);
             if (t[10])
                 fprintf(stderr, "; chain: waits for K-1 %.0f, from K-1 visible to the factor %.0f (stage Linv %.0f, "
-                        "product + stores %.0f, drain + flag %.0f, update the rest)",
+                        "product + stores %.0f, update + drain + flag %.0f, the rest)",
                         (double)t[8] / t[10], (double)t[9] / t[10], (double)t[14] / t[10], (double)t[15] / t[10],
                         (double)t[16] / t[10]);
             if (t[7] && t[17])
