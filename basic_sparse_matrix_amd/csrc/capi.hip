@@ -141,6 +141,37 @@ static void* pinned(size_t bytes) {
     return buf;
 }
 
+// Per-call temporaries of small calls (the uploaded X, Y, row counts, scan
+// workspace) come from a per-thread grow-only device arena: no hipMalloc /
+// hipFree per call (hipFree waits for the device). Calls larger than
+// SCRATCH_MAX allocate as before. The arena is left to the process exit.
+constexpr size_t SCRATCH_MAX = 64ull << 20;
+static void* scratch(int slot, size_t bytes) {
+    struct Slot {
+        void* p = nullptr;
+        size_t cap = 0;
+        int dev = -1;
+    };
+    static thread_local Slot sl[4];
+    int dev = 0;
+    if (slot < 0 || slot >= 4 || bytes > SCRATCH_MAX || hipGetDevice(&dev) != hipSuccess) return nullptr;
+    Slot& x = sl[slot];
+    if (bytes > x.cap || dev != x.dev) {
+        if (x.p) (void)hipFree(x.p);
+        x.p = nullptr;
+        x.cap = 0;
+        const size_t want = std::max<size_t>(bytes, 1 << 20);
+        if (hipMalloc(&x.p, want) != hipSuccess) {
+            x.p = nullptr;
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        x.cap = want;
+        x.dev = dev;
+    }
+    return x.p;
+}
+
 hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s) {
     static thread_local void* bounce = nullptr;
     if (bytes > 4096) {
@@ -160,31 +191,42 @@ hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s) {
     return e;
 }
 
-// Upload k host columns (each n values) into a device ROW-major n x k array.
+// Upload k host columns (each n values) into a device ROW-major n x k array
+// at *data: `out` (allocated here), or, when the caller offers dst_small
+// (scratch) and the pinned path serves the call, dst_small with the copy left
+// in flight -- the caller then synchronises the stream before it returns
+// (the pinned buffer is reused by the next call) and *synced is false.
 static int upload_columns(int dtype, uint64_t n, uint64_t k, const void* const* cols, DBuf& out,
-                          hipStream_t s) {
+                          hipStream_t s, void** data = nullptr, void* dst_small = nullptr,
+                          bool* synced = nullptr) {
     const size_t es = dtype_size(dtype);
-    BSM_TRY(out.alloc(n * k * es));
-    if (n == 0 || k == 0) return BSM_OK;
-    for (uint64_t j = 0; j < k; ++j)
+    if (synced) *synced = true;
+    for (uint64_t j = 0; j < k && n; ++j)
         BSM_REQUIRE(cols[j] != nullptr, BSM_ERR_INVALID, "null column pointer %llu", (unsigned long long)j);
-    if (n * k * es <= PIN_MAX) {
-        if (char* pin = static_cast<char*>(pinned(n * k * es))) {  // pack row-major on the host, one copy
-            if (k == 1) {
-                std::memcpy(pin, cols[0], n * es);
-            } else {
-                for (uint64_t j = 0; j < k; ++j) {
-                    const char* c = static_cast<const char*>(cols[j]);
-                    for (uint64_t r = 0; r < n; ++r) std::memcpy(pin + (r * k + j) * es, c + r * es, es);
-                }
+    char* pin = n * k * es <= PIN_MAX && n && k ? static_cast<char*>(pinned(n * k * es)) : nullptr;
+    void* dst = dst_small && pin && synced ? dst_small : nullptr;
+    if (!dst) {
+        BSM_TRY(out.alloc(n * k * es));
+        dst = out.p;
+    }
+    if (data) *data = dst;
+    if (n == 0 || k == 0) return BSM_OK;
+    if (pin) {  // pack row-major on the host, one copy
+        if (k == 1) {
+            std::memcpy(pin, cols[0], n * es);
+        } else {
+            for (uint64_t j = 0; j < k; ++j) {
+                const char* c = static_cast<const char*>(cols[j]);
+                for (uint64_t r = 0; r < n; ++r) std::memcpy(pin + (r * k + j) * es, c + r * es, es);
             }
-            BSM_HIP_TRY(hipMemcpyAsync(out.p, pin, n * k * es, hipMemcpyHostToDevice, s));
-            BSM_HIP_TRY(hipStreamSynchronize(s));  // the pinned buffer is reused by the next call
-            return BSM_OK;
         }
+        BSM_HIP_TRY(hipMemcpyAsync(dst, pin, n * k * es, hipMemcpyHostToDevice, s));
+        if (dst == dst_small) *synced = false;
+        else BSM_HIP_TRY(hipStreamSynchronize(s));  // the pinned buffer is reused by the next call
+        return BSM_OK;
     }
     if (k == 1) {
-        BSM_HIP_TRY(hipMemcpyAsync(out.p, cols[0], n * es, hipMemcpyHostToDevice, s));
+        BSM_HIP_TRY(hipMemcpyAsync(dst, cols[0], n * es, hipMemcpyHostToDevice, s));
         return BSM_OK;
     }
     DBuf staging;
@@ -192,7 +234,7 @@ static int upload_columns(int dtype, uint64_t n, uint64_t k, const void* const* 
     for (uint64_t j = 0; j < k; ++j)
         BSM_HIP_TRY(hipMemcpyAsync(static_cast<char*>(staging.p) + j * n * es, cols[j], n * es,
                                    hipMemcpyHostToDevice, s));
-    BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, staging.p, out.p, s));
+    BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, staging.p, dst, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // staging dies here
     return BSM_OK;
 }
@@ -223,15 +265,29 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     const size_t es = dtype_size(a->dtype);
     const uint64_t rows = a->rows;
     DBuf y, row_nnz, ws;
-    BSM_TRY(y.alloc(rows * k * es));
-    BSM_TRY(row_nnz.alloc(rows * sizeof(int32_t)));
-    BSM_TRY(ws.alloc(scan_workspace_bytes(rows)));
+    // small calls: temporaries from the per-thread arena, and the result's
+    // col / vals sized for every entry (rows x k), so that the scan, the
+    // compaction and the read of nnz share ONE synchronisation
+    const size_t y_b = rows * k * es, nz_b = rows * sizeof(int32_t), ws_b = scan_workspace_bytes(rows);
+    const bool small = y_b + rows * k * (es + sizeof(int32_t)) <= SCRATCH_MAX && nz_b + ws_b <= SCRATCH_MAX;
+    void* yp = small ? scratch(0, y_b) : nullptr;
+    const size_t nz_al = (nz_b + 255) / 256 * 256;
+    void* nzp = yp ? scratch(1, nz_al + ws_b) : nullptr;
+    if (!nzp) {
+        BSM_TRY(y.alloc(y_b));
+        BSM_TRY(row_nnz.alloc(nz_b));
+        BSM_TRY(ws.alloc(ws_b));
+        yp = y.p;
+        nzp = row_nnz.p;
+    }
+    int32_t* const nz = static_cast<int32_t*>(nzp);
+    void* const wsp = ws.p ? ws.p : static_cast<char*>(nzp) + nz_al;
     bsm_csr* r = nullptr;
     // out row_ptr is allocated first (nnz unknown until the scan completes)
     DBuf out_rp;
     BSM_TRY(out_rp.alloc((rows + 1) * sizeof(int64_t)));
     if (k == 0) {
-        BSM_HIP_TRY(hipMemsetAsync(row_nnz.p, 0, rows * sizeof(int32_t), s));
+        BSM_HIP_TRY(hipMemsetAsync(nz, 0, rows * sizeof(int32_t), s));
     } else {
         const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
         // one thread at a time builds and launches with the cached plan (a
@@ -249,7 +305,7 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
             else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
         }
         if (a->tiled && a->tiled->k == k) {
-            BSM_TRY(tiled_spmm(a->tiled, x_dev, y.p, row_nnz.as<int32_t>(), false, s));
+            BSM_TRY(tiled_spmm(a->tiled, x_dev, yp, nz, false, s));
         } else if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
             if (a->plan_seg) (void)hipFree(a->plan_seg);
             a->plan_seg = nullptr;
@@ -266,28 +322,27 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
         if (a->tiled && a->tiled->k == k)
             ;  // done above
         else if (spmm_wants_split(a->dtype, k, a->max_row_len))
-            BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, y.p,
-                                        row_nnz.as<int32_t>(), s));
+            BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, yp, nz, s));
         else if (w && a->plan_usable)
             BSM_TRY(spmm_panelled(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
-                                  y.p, row_nnz.as<int32_t>(), w, a->plan_seg, s));
+                                  yp, nz, w, a->plan_seg, s));
         else
             BSM_TRY(spmm_dispatch(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
-                                  y.p, row_nnz.as<int32_t>(), false, s));
+                                  yp, nz, false, s));
     }
-    BSM_TRY(exclusive_scan_i32_to_i64(row_nnz.as<int32_t>(), out_rp.as<int64_t>(), rows, ws.p,
-                                      ws.bytes, s));
+    const size_t wsb = ws.p ? ws.bytes : ws_b;
+    BSM_TRY(exclusive_scan_i32_to_i64(nz, out_rp.as<int64_t>(), rows, wsp, wsb, s));
     int64_t out_nnz = 0;
-    BSM_HIP_TRY(read_dev(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t), s));
+    if (!small || yp == y.p) BSM_HIP_TRY(read_dev(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t), s));
+    const uint64_t cap = small && yp != y.p ? rows * k : (uint64_t)out_nnz;
     r = new bsm_csr();
     r->dtype = a->dtype;
     r->device = a->device;
     r->rows = rows;
     r->cols = k;
-    r->nnz = (uint64_t)out_nnz;
     DBuf oc, ov;
-    int rc = oc.alloc((uint64_t)out_nnz * sizeof(int32_t));
-    if (rc == BSM_OK) rc = ov.alloc((uint64_t)out_nnz * es);
+    int rc = oc.alloc(cap * sizeof(int32_t));
+    if (rc == BSM_OK) rc = ov.alloc(cap * es);
     if (rc != BSM_OK) {
         delete r;
         return rc;
@@ -297,7 +352,15 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     r->vals = ov.release();
     r->analysed = true;
     r->rows_sorted = true;
-    rc = compact_dispatch(a->dtype, rows, k, y.p, r->row_ptr, r->col, r->vals, s);
+    rc = compact_dispatch(a->dtype, rows, k, yp, r->row_ptr, r->col, r->vals, s);
+    if (rc == BSM_OK && small && yp != y.p) {  // nnz with the one synchronisation of the call
+        hipError_t e = read_dev(&out_nnz, r->row_ptr + rows, sizeof(int64_t), s);
+        if (e != hipSuccess) {
+            set_error("read nnz: %s", hipGetErrorString(e));
+            rc = BSM_ERR_HIP;
+        }
+    }
+    r->nnz = (uint64_t)out_nnz;
     if (rc == BSM_OK) {
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
@@ -511,8 +574,13 @@ int bsm_csr_mul_dense(const bsm_csr* a, uint64_t k, uint64_t x_rows, const void*
     hipStream_t s;
     BSM_TRY(ctx_stream(&s));
     DBuf x;
-    BSM_TRY(upload_columns(a->dtype, x_rows, k, x_cols, x, s));
-    return mul_dense_device(a, k, x.p, out, s);
+    void* xp = nullptr;
+    bool synced = true;
+    const size_t x_b = x_rows * k * dtype_size(a->dtype);
+    int rc = upload_columns(a->dtype, x_rows, k, x_cols, x, s, &xp, scratch(3, x_b), &synced);
+    if (rc == BSM_OK) rc = mul_dense_device(a, k, xp, out, s);
+    if (!synced) (void)hipStreamSynchronize(s);  // the pinned upload buffer is free again on every path
+    return rc;
 }
 
 int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void* out,
