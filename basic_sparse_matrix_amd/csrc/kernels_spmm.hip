@@ -1015,11 +1015,14 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
 // serialises the whole product. Integer sums wrap (Cargo.toml:18) and are
 // therefore order-free: each wave takes a fixed slice of SPLIT_CHUNK entries,
 // sums its part of every row it touches (lanes (s, c): entry slot s, output
-// column c, then an xor-butterfly over s) and stores rows it covers entirely
-// or atomically adds partial rows into a zeroed Y. Floating point keeps the
-// in-order row-wave kernels: its sums are not associative.
+// column c, then an xor-butterfly over s) and stores rows it covers entirely.
+// A row cut by the slices leaves one partial per slice (slot 1 in the slice
+// where it starts, slot 0 in the later ones) and split_reduce adds them: no
+// atomics (the bench's one long row made ~4,400 atomics on one cache line,
+// 131 us a call). Floating point keeps the in-order row-wave kernels: its sums
+// are not associative.
 // ---------------------------------------------------------------------------
-constexpr int64_t SPLIT_CHUNK = 2048;   // entries per wave
+constexpr int64_t SPLIT_CHUNK = 512;    // entries per wave
 constexpr uint64_t SPLIT_MIN_ROW = 8192;  // use the split kernel when some row is longer
 
 template <typename T> struct UnsignedOf;
@@ -1031,7 +1034,8 @@ template <> struct UnsignedOf<uint64_t> { using type = unsigned long long; };
 template <typename T, int KL>
 __global__ __launch_bounds__(256) void spmm_split_int(int64_t rows, int64_t nnz, const int64_t* __restrict__ rp,
                                                       const int32_t* __restrict__ col, const T* __restrict__ val,
-                                                      int k, const T* __restrict__ X, T* __restrict__ Y) {
+                                                      int k, const T* __restrict__ X, T* __restrict__ Y,
+                                                      T* __restrict__ part) {
     using U = typename UnsignedOf<T>::type;
     constexpr int S = WAVE / KL;
     const int lane = threadIdx.x & (WAVE - 1);
@@ -1052,19 +1056,41 @@ __global__ __launch_bounds__(256) void spmm_split_int(int64_t rows, int64_t nnz,
             const int jc = cb + c;
             const bool cval = jc < k;
             U acc = 0;
+#pragma unroll 4
             for (int64_t e = a + s; e < b; e += S) {
                 if (cval) acc += (U)val[e] * (U)X[(int64_t)col[e] * k + jc];
             }
 #pragma unroll
             for (int off = KL; off < WAVE; off <<= 1) acc += (U)__shfl_xor(acc, off, WAVE);
             if (s == 0 && cval) {
-                T* dst = &Y[r * (int64_t)k + jc];
                 if (whole)
-                    *dst = (T)acc;
-                else
-                    atomicAdd(reinterpret_cast<U*>(dst), acc);
+                    Y[r * (int64_t)k + jc] = (T)acc;
+                else  // slot 0: the row started before this slice; 1: it starts in it
+                    part[(w * 2 + (a == e0 && rs < e0 ? 0 : 1)) * (int64_t)k + jc] = (T)acc;
             }
         }
+    }
+}
+
+// rows cut by the slices: Y[r] = the sum of their partials (one wave per row)
+template <typename T>
+__global__ __launch_bounds__(256) void split_reduce(int64_t rows, const int64_t* __restrict__ rp, int k,
+                                                    const T* __restrict__ part, T* __restrict__ Y) {
+    using U = typename UnsignedOf<T>::type;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+    if (r >= rows) return;
+    const int64_t rs = rp[r], re = rp[r + 1];
+    if (re == rs) return;
+    const int64_t wf = rs / SPLIT_CHUNK, wl = (re - 1) / SPLIT_CHUNK;
+    if (wf == wl) return;  // stored whole by its slice
+    for (int j = 0; j < k; ++j) {
+        U acc = 0;
+        for (int64_t w = wf + lane; w <= wl; w += WAVE)
+            acc += (U)part[(w * 2 + (w == wf ? 1 : 0)) * (int64_t)k + j];
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) acc += (U)__shfl_xor(acc, off, WAVE);
+        if (lane == 0) Y[r * (int64_t)k + j] = (T)acc;
     }
 }
 
@@ -1095,13 +1121,18 @@ int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* r
     const uint64_t blocks = (waves + 3) / 4;
     BSM_REQUIRE(blocks < (1ull << 31) && k < (1ull << 31), BSM_ERR_UNSUPPORTED, "split SpMM: too large");
     const int ki = (int)k;
+    DBuf part;  // two partial rows per slice
+    BSM_TRY(part.alloc(waves * 2 * k * es));
     return dispatch_dtype(dtype, [&]<typename T>() -> int {
         if constexpr (std::is_integral_v<T>) {
             auto go = [&]<int KL>() {
-                if (blocks)
+                if (blocks) {
                     spmm_split_int<T, KL><<<(unsigned)blocks, 256, 0, s>>>(
                         (int64_t)rows, (int64_t)nnz, rp, col, static_cast<const T*>(vals), ki,
-                        static_cast<const T*>(x), static_cast<T*>(y));
+                        static_cast<const T*>(x), static_cast<T*>(y), part.as<T>());
+                    split_reduce<T><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>((int64_t)rows, rp, ki,
+                                                                              part.as<T>(), static_cast<T*>(y));
+                }
             };
             if (k <= 2) go.template operator()<2>();
             else if (k <= 4) go.template operator()<4>();
