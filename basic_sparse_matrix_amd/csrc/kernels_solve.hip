@@ -1881,12 +1881,18 @@ __global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld
                 wait_flag(&fl[Ja]);
                 const T v = ld_sc1(&Yc[Ja * 64 + lane]);
                 T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+                // the neighbour's 64 values to every lane through LDS (one
+                // write, broadcast reads) rather than 64 v_readlane pairs
+                rv[lane] = v;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
                 for (int q = 0; q < 64; q += 4) {
-                    s0 = fma_t(madj[q], readlane_t(v, q), s0);
-                    s1 = fma_t(madj[q + 1], readlane_t(v, q + 1), s1);
-                    s2 = fma_t(madj[q + 2], readlane_t(v, q + 2), s2);
-                    s3 = fma_t(madj[q + 3], readlane_t(v, q + 3), s3);
+                    s0 = fma_t(madj[q], rv[q], s0);
+                    s1 = fma_t(madj[q + 1], rv[q + 1], s1);
+                    s2 = fma_t(madj[q + 2], rv[q + 2], s2);
+                    s3 = fma_t(madj[q + 3], rv[q + 3], s3);
                 }
                 u = u - ((s0 + s1) + (s2 + s3));
             }
