@@ -1932,11 +1932,19 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
     }
     return y;
 }
+// one Newton step (the panel factor's pivots; BSM_BLK_PANELS=4 keeps two for A/B):
+// the estimate's error squared once
+__device__ __forceinline__ double rsqrt_nr1(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    const double h = __fma_rn(-x * y, y, 1.0);
+    return __fma_rn(0.5 * y, h, y);
+}
 __device__ __forceinline__ float rsqrt_nr(float x) {
     float y = __builtin_amdgcn_rsqf(x);
     const float h = __fmaf_rn(-x * y, y, 1.0f);
     return __fmaf_rn(0.5f * y, h, y);
 }
+__device__ __forceinline__ float rsqrt_nr1(float x) { return rsqrt_nr(x); }
 
 // Factor the 64 x 64 tile S (P[r * TLD + c], lower part) in one wave, lane r =
 // row r: right-looking, column s broadcast through LDS (colb). Out of line: in
@@ -2262,7 +2270,7 @@ __device__ __forceinline__ void blk_linv_diag(lds_t<T>* Q, const lds_t<T>* Di, i
 // Linv by row blocks: row block p - 1 on waves 1-3 while wave 0 factors
 // block p, the last one at the end. rd[r] = 1 / L[r][r].
 // Every thread of the workgroup must call it (barriers inside).
-template <typename T>
+template <typename T, bool NR1 = false>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
                                                 int* status, int tid, unsigned long long* tdbg = nullptr) {
     long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
@@ -2288,7 +2296,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
                 const T piv = rowbcast<t>(dv[t]);
                 pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
-                const T rp = rsqrt_nr(piv);
+                const T rp = NR1 ? rsqrt_nr1(piv) : rsqrt_nr(piv);
                 rps[t] = rp;
                 const T l = dv[t] * rp;  // lane t: the pivot's square root
                 dv[t] = l;
@@ -2585,9 +2593,13 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             if (panels == 3) {  // 2 x 2 blocks of 32
                 blk_diag_2x2<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, (lds_t<T>*)Tb,
                                 (lds_t<T>*)Di, status, tid);
-            } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default)
-                blk_diag_panels<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
-                                   (lds_t<T>*)rd, status, tid, tdbg);
+            } else if (panels == 4) {  // A/B: the panels with two Newton steps per pivot (round-2 form)
+                blk_diag_panels<T, false>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
+                                          (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg);
+            } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default);
+                // one Newton step per pivot: C5 factor 317 -> 311 ms, x error 8.8e-11 -> 9.7e-11
+                blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
+                                         (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg);
             } else {  // one-wave factor; the inverse below
                 if (w == 0)
                     blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
@@ -3193,7 +3205,8 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     // BSM_BLK_PANELS: 1 (default) the diagonal tile by 16-column panels on four
     // waves, the products on f64 MFMA (C5 0.41 s); 0 the one-wave 64-column
     // factor, then the block inverse (0.49 s); 3 the tile as 2 x 2 blocks of 32
-    // (0.57 s). Tried and dropped: the 64-column inverse formed on a second
+    // (0.57 s); 4 the panels with two Newton steps per pivot (A/B). Tried and
+    // dropped: the 64-column inverse formed on a second
     // wave behind the factor, meeting it every 8 columns (0.98 s: the factor
     // waits for the inverse's long rows at the barriers).
     const char* pe = getenv("BSM_BLK_PANELS");
