@@ -632,6 +632,14 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             }
             for (int64_t l = 0; l < n_long; ++l) ps[l + 1] = ps[l] + std::min(cnt_side[2 * l], cnt_side[2 * l + 1]) + 1;
             n_pieces = ps[n_long];
+            if (getenv("BSM_SS_DEBUG")) {  // the long rows' cut: M occurrences per side and the pieces
+                for (int64_t l = 0; l < n_long && l < 4; ++l)
+                    fprintf(stderr, "[bsm ss debug] long row %lld: extents a %lld b %lld, M count a %lld b %lld\n",
+                            (long long)l, (long long)(hx[4 * l + 1] - hx[4 * l]), (long long)(hx[4 * l + 3] - hx[4 * l + 2]),
+                            (long long)cnt_side[2 * l], (long long)cnt_side[2 * l + 1]);
+                fprintf(stderr, "[bsm ss debug] long rows %lld, chunks %lld, pieces %lld\n", (long long)n_long,
+                        (long long)n_chunks, (long long)n_pieces);
+            }
             BSM_HIP_TRY(hipMemcpyAsync(pstart.p, ps.data(), (n_long + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
             BSM_TRY(pieces.alloc(n_pieces * sizeof(Piece)));
             BSM_TRY(pcnt.alloc(n_pieces * sizeof(int32_t)));
