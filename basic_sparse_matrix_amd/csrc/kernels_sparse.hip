@@ -266,8 +266,8 @@ __device__ __forceinline__ double rl(double v, int l) {
 }
 
 // One WAVE per piece. The merge itself is uniform scalar control flow: both
-// stretches are read 64 entries at a time into a lane window (next window
-// prefetched), the current entries come out with v_readlane, and the kept
+// stretches are read 64 entries at a time into a lane window, the current
+// entries come out with v_readlane, and the kept
 // outputs collect one per lane until 64 are stored at once. Outputs go to a
 // scratch slot at a0 + b0 (pieces' slots never overlap: a piece emits at
 // most its two lengths plus one pair); piece_copy moves them into place.
@@ -311,10 +311,14 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
             x = side_b ? bv[e] : av[e];
         }
     };
-    int32_t caw, can, cbw, cbn;
-    T vaw, van, vbw, vbn;
-    if (ea > pc.a0) { load(false, wa, caw, vaw); load(false, wa + 64, can, van); }
-    if (eb > pc.b0) { load(true, wb, cbw, vbw); load(true, wb + 64, cbn, vbn); }
+    // windows are loaded when the merge reaches them, not prefetched: a
+    // prefetch into a second register set made the compiler rotate the sets
+    // every step, with a wait for the outstanding loads in each (~550 ns a
+    // step); now one wait per 64 steps
+    int32_t caw = 0, cbw = 0;
+    T vaw = A::zero(), vbw = A::zero();
+    if (ea > pc.a0) load(false, wa, caw, vaw);
+    if (eb > pc.b0) load(true, wb, cbw, vbw);
     int64_t o = pc.a0 + pc.b0;
     int nbuf = 0;
     int32_t cnt = 0, oc = 0;
@@ -337,15 +341,11 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
     while (ia < ea && ib < eb) {
         if (ia - wa == 64) {
             wa += 64;
-            caw = can;
-            vaw = van;
-            if (wa + 64 < ea) load(false, wa + 64, can, van);
+            load(false, wa, caw, vaw);
         }
         if (ib - wb == 64) {
             wb += 64;
-            cbw = cbn;
-            vbw = vbn;
-            if (wb + 64 < eb) load(true, wb + 64, cbn, vbn);
+            load(true, wb, cbw, vbw);
         }
         const int32_t ca = rl(caw, (int)(ia - wa)), cb = rl(cbw, (int)(ib - wb));
         if (ca > cb) {
