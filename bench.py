@@ -443,6 +443,7 @@ def main():
         kern_ms.append(ev_k0.elapsed_time(ev_k1))
         comm_ms.append(ev_k1.elapsed_time(ev_c0))
         comp_ms.append(ev_c0.elapsed_time(ev_c1))
+    log(f"rank {rank}: SpMM kernel ms per timed step: {[round(t, 2) for t in kern_ms]}")
     if world > 1:
         t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
