@@ -9,11 +9,13 @@ hand-written HIP kernels through the C-ABI in include/bsm.h
 
 from .dense import Dense
 from .dense_static import DenseS
+from .multi import set_gpus
 from .solver import backward_substitution, forward_substitution, solve
 from .sparse import COO, COOEntry, Csr, CsrEntry
 from .util import GetDims, MatDim, MatErr, MatErrKind, Panic
 
 __all__ = [
+    "set_gpus",
     "COO",
     "COOEntry",
     "Csr",

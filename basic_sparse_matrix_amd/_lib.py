@@ -50,6 +50,8 @@ BSM_ERR_UNSUPPORTED = 7
 BSM_TILED_ANY_PADDING = 1
 BSM_ERR_NO_DEVICE = 8
 BSM_ERR_OUT_OF_BOUNDS = 9
+BSM_ERR_COMM = 10
+BSM_UNIQUE_ID_BYTES = 128
 
 # generator families (bsm_synth.h)
 ROWLEN_CONST, ROWLEN_UNIFORM, ROWLEN_BINOMIAL = 0, 1, 2
@@ -78,6 +80,7 @@ _u64p = ctypes.POINTER(ctypes.c_uint64)
 SIGNATURES = [
     ("bsm_api_version", _int, []),
     ("bsm_last_error", ctypes.c_char_p, []),
+    ("bsm_stage_timing", _int, [_int]),
     ("bsm_stage_times", _int, [_int, ctypes.POINTER(_int), ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     ("bsm_device_count", _int, [ctypes.POINTER(_int)]),
     ("bsm_set_device", _int, [_int]),
@@ -117,6 +120,26 @@ SIGNATURES = [
     ("bsm_tiled_destroy", None, [_vp]),
     ("bsm_csr_tiled", _int, [_vp, ctypes.POINTER(_int)]),
     ("bsm_dev_compact", _int, [_int, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp]),
+    # multi-GPU (row blocks + RCCL all-gather)
+    ("bsm_multi_create", _int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_vp)]),
+    ("bsm_multi_unique_id", _int, [_vp]),
+    ("bsm_multi_create_rank", _int, [_vp, _int, _int, _int, ctypes.POINTER(_vp)]),
+    ("bsm_multi_info", _int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    ("bsm_multi_broadcast", _int, [_vp, _pp, _u64, _int]),
+    ("bsm_multi_destroy", None, [_vp]),
+    ("bsm_mcsr_upload", _int, [_vp, _int, _u64, _u64, _u64, _vp, _vp, _vp, _u32, ctypes.POINTER(_vp)]),
+    ("bsm_mcsr_generate", _int, [_vp, _int, _u64, _u64, _u32, _int, _u32, _u32, _int, _u32, ctypes.POINTER(_vp)]),
+    ("bsm_mcsr_info", _int, [_vp, _u64p, _u64p, _u64p, ctypes.POINTER(_u32), _u64p, _vp]),
+    ("bsm_mcsr_prepare", _int, [_vp, _u64, _int, ctypes.POINTER(ctypes.c_double)]),
+    ("bsm_mcsr_plan_info", _int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), _u64p, _u64p]),
+    ("bsm_mcsr_mul_dense", _int, [_vp, _u64, _u64, _pp, ctypes.POINTER(_vp)]),
+    ("bsm_mcsr_step", _int, [_vp, _pp]),
+    ("bsm_mcsr_sync", _int, [_vp]),
+    ("bsm_mcsr_step_times", _int, [_vp, _int, _int, ctypes.POINTER(_int), ctypes.POINTER(ctypes.c_double)]),
+    ("bsm_mcsr_reset_times", None, [_vp]),
+    ("bsm_mcsr_copy_y", _int, [_vp, _int, _vp, _vp]),
+    ("bsm_mcsr_output", _int, [_vp, ctypes.POINTER(_vp)]),
+    ("bsm_mcsr_free", None, [_vp]),
 ]
 
 _lock = threading.Lock()
@@ -142,8 +165,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         return lib
 
 
+def stage_timing(on: bool = True) -> None:
+    """Arm (or disarm) the solver's per-stage HIP-event timer (bsm_stage_timing)."""
+    check(load().bsm_stage_timing(1 if on else 0))
+
+
 def stage_times() -> dict:
-    """{stage: device ms} of the last solve on this thread (bsm_stage_times)."""
+    """{stage: device ms} of the last solve on this thread (bsm_stage_times;
+    arm it first with stage_timing())."""
     lib = load()
     n = ctypes.c_int(0)
     check(lib.bsm_stage_times(0, ctypes.byref(n), None, None))

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -191,8 +192,35 @@ struct bsm_csr {
 
 
 namespace bsm {
+// Host-side phase times of a schedule build (bsm_mcsr_prepare's plan_ms).
+struct PlanTimes {
+    double total_ms = 0, count_ms = 0, scan_ms = 0, alloc_ms = 0, write_ms = 0, panel_ms = 0, buffers_ms = 0;
+};
+inline std::chrono::steady_clock::time_point host_now() { return std::chrono::steady_clock::now(); }
+inline double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz);
 int csr_analyse(bsm_csr* m, hipStream_t s);
+// mul_dense's schedule (capi.hip): build once per handle and k (synchronous;
+// schedule 0 auto, 1 the tiled copy whenever possible, 2 never), then launch.
+// The caller holds a->plan_mu for both.
+int spmm_prepare_locked(const bsm_csr* a, uint64_t k, int schedule, uint64_t reserve, hipStream_t s,
+                        PlanTimes* pt);
+int spmm_launch_locked(const bsm_csr* a, uint64_t k, bool allow_tiled, const void* x, void* y, int32_t* nz,
+                       hipStream_t s);
+// pinned host staging / per-thread device arena (capi.hip)
+void* pinned(size_t bytes);
+// host columns (Dense::get_col) -> a device ROW-major n x k array in `out`
+// (synchronous) (capi.hip)
+int upload_dense_cols(int dtype, uint64_t n, uint64_t k, const void* const* cols, DBuf& out, hipStream_t s);
+// staged pinned pipelines (transfer.hip); all synchronous
+int h2d_staged(void* dst, const void* src, size_t bytes, hipStream_t s);
+int d2h_staged(void* dst, const void* src, size_t bytes, hipStream_t s);
+int h2d_cols_narrow(int32_t* dst, const uint64_t* src, uint64_t n, uint64_t cols, uint64_t* bad, hipStream_t s);
+int h2d_row_ptr(int64_t* dst, const uint64_t* src, uint64_t n, uint64_t base, hipStream_t s);
+int d2h_cols_widen(uint64_t* dst, const int32_t* src, uint64_t n, hipStream_t s);
 
 // kernels (kernels_*.hip), all async on stream s
 uint64_t scan_workspace_bytes(uint64_t n);
@@ -224,8 +252,11 @@ int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const
                   int32_t* row_nnz, uint64_t panel_cols, const int32_t* seg, hipStream_t s);
 // row-block x column-panel schedule (kernels_tiled.hip)
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len);
+// synchronous; the copy must leave `reserve` device bytes free; pt (may be
+// null) receives host times of its phases
 int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s);  // synchronous
+                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve = 0,
+                 PlanTimes* pt = nullptr);
 int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, bool neg_init, hipStream_t s);
 void tiled_destroy(bsm_tiled* t);
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,

@@ -2,7 +2,9 @@
 //
 // Host-buffer entry points mirror the reference crate's hot-path methods
 // (src/sparse.rs, src/lib.rs); each is synchronous and owns no caller memory.
+#include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -38,16 +40,27 @@ void stage_clear() {
         if (st.ev) (void)hipEventDestroy(st.ev);
     g_stages.clear();
 }
+// Off unless armed (bsm_stage_timing or env BSM_STAGE_TIMES=1): no events are
+// created on calls nobody times.
+std::atomic<int> g_stage_on{-1};
+bool stage_on() {
+    int v = g_stage_on.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("BSM_STAGE_TIMES");
+        v = (e && atoi(e) != 0) ? 1 : 0;
+        g_stage_on.store(v, std::memory_order_relaxed);
+    }
+    return v != 0;
+}
 }  // namespace
 
+// Every public entry point that marks stages starts its own list.
 void stage_reset(hipStream_t s) {
     stage_clear();
-    stage_mark("start", s);
+    if (stage_on()) stage_mark("start", s);
 }
 void stage_mark(const char* name, hipStream_t s) {
-    // marks outside a solve (cholesky_decomp alone) extend the last solve's
-    // list; it is bounded
-    if (g_stages.size() >= 64) return;
+    if (!stage_on() || g_stages.empty() || g_stages.size() >= 64) return;
     Stage st;
     st.name = name;
     if (hipEventCreate(&st.ev) != hipSuccess) return;
@@ -127,35 +140,57 @@ int csr_analyse(bsm_csr* m, hipStream_t s) {
 // pinned buffer and moved with one copy (profiles/r01_z_api_overhead.log).
 // One buffer per thread (the library's calls are synchronous per thread).
 constexpr size_t PIN_MAX = 32ull << 20;
-static void* pinned(size_t bytes) {
-    static thread_local void* buf = nullptr;
-    static thread_local size_t cap = 0;
-    if (bytes > cap) {
+namespace {
+// Per-thread buffers are released when their thread exits (worker
+// threads of the multi-GPU path must not leak them).
+struct PinnedHolder {
+    void* buf = nullptr;
+    size_t cap = 0;
+    ~PinnedHolder() {
         if (buf) (void)hipHostFree(buf);
-        buf = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(bytes, 1 << 20);
-        if (hipHostMalloc(&buf, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-        cap = want;
     }
-    return buf;
+};
+struct ScratchSlot {
+    void* p = nullptr;
+    size_t cap = 0;
+    int dev = -1;
+};
+struct ScratchHolder {
+    ScratchSlot sl[4];
+    ~ScratchHolder() {
+        for (auto& x : sl)
+            if (x.p) (void)hipFree(x.p);
+    }
+};
+}  // namespace
+
+void* pinned(size_t bytes) {
+    static thread_local PinnedHolder h;
+    if (bytes > h.cap) {
+        if (h.buf) (void)hipHostFree(h.buf);
+        h.buf = nullptr;
+        h.cap = 0;
+        size_t want = std::max<size_t>(bytes, 1 << 20);
+        if (hipHostMalloc(&h.buf, want, hipHostMallocDefault) != hipSuccess) {
+            h.buf = nullptr;
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        h.cap = want;
+    }
+    return h.buf;
 }
 
 // Per-call temporaries of small calls (the uploaded X, Y, row counts, scan
 // workspace) come from a per-thread grow-only device arena: no hipMalloc /
 // hipFree per call (hipFree waits for the device). Calls larger than
-// SCRATCH_MAX allocate as before. The arena is left to the process exit.
+// SCRATCH_MAX allocate as before.
 constexpr size_t SCRATCH_MAX = 64ull << 20;
 static void* scratch(int slot, size_t bytes) {
-    struct Slot {
-        void* p = nullptr;
-        size_t cap = 0;
-        int dev = -1;
-    };
-    static thread_local Slot sl[4];
+    static thread_local ScratchHolder holder;
     int dev = 0;
     if (slot < 0 || slot >= 4 || bytes > SCRATCH_MAX || hipGetDevice(&dev) != hipSuccess) return nullptr;
-    Slot& x = sl[slot];
+    ScratchSlot& x = holder.sl[slot];
     if (bytes > x.cap || dev != x.dev) {
         if (x.p) (void)hipFree(x.p);
         x.p = nullptr;
@@ -173,17 +208,19 @@ static void* scratch(int slot, size_t bytes) {
 }
 
 hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s) {
-    static thread_local void* bounce = nullptr;
+    static thread_local PinnedHolder holder;
     if (bytes > 4096) {
         hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s);
         return e != hipSuccess ? e : hipStreamSynchronize(s);
     }
+    void*& bounce = holder.buf;
     if (!bounce) {
         hipError_t e = hipHostMalloc(&bounce, 4096, hipHostMallocDefault);
         if (e != hipSuccess) {
             bounce = nullptr;
             return e;
         }
+        holder.cap = 4096;
     }
     hipError_t e = hipMemcpyAsync(bounce, dev, bytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -203,40 +240,43 @@ static int upload_columns(int dtype, uint64_t n, uint64_t k, const void* const* 
     if (synced) *synced = true;
     for (uint64_t j = 0; j < k && n; ++j)
         BSM_REQUIRE(cols[j] != nullptr, BSM_ERR_INVALID, "null column pointer %llu", (unsigned long long)j);
-    char* pin = n * k * es <= PIN_MAX && n && k ? static_cast<char*>(pinned(n * k * es)) : nullptr;
+    const size_t bytes = n * k * es;
+    char* pin = bytes <= PIN_MAX && n && k ? static_cast<char*>(pinned(bytes)) : nullptr;
     void* dst = dst_small && pin && synced ? dst_small : nullptr;
     if (!dst) {
-        BSM_TRY(out.alloc(n * k * es));
+        BSM_TRY(out.alloc(bytes));
         dst = out.p;
     }
     if (data) *data = dst;
     if (n == 0 || k == 0) return BSM_OK;
-    if (pin) {  // pack row-major on the host, one copy
-        if (k == 1) {
-            std::memcpy(pin, cols[0], n * es);
-        } else {
-            for (uint64_t j = 0; j < k; ++j) {
-                const char* c = static_cast<const char*>(cols[j]);
-                for (uint64_t r = 0; r < n; ++r) std::memcpy(pin + (r * k + j) * es, c + r * es, es);
-            }
+    // the columns go over as they are (column-major, memcpy per column) and
+    // are packed to row-major on the device: a host-side pack is one
+    // element-sized copy per value
+    if (pin) {  // small: one pinned buffer, one DMA
+        void* cm = k == 1 ? dst : scratch(2, bytes);
+        DBuf cm_own;
+        if (!cm) {
+            BSM_TRY(cm_own.alloc(bytes));
+            cm = cm_own.p;
         }
-        BSM_HIP_TRY(hipMemcpyAsync(dst, pin, n * k * es, hipMemcpyHostToDevice, s));
-        if (dst == dst_small) *synced = false;
+        for (uint64_t j = 0; j < k; ++j) std::memcpy(pin + j * n * es, cols[j], n * es);
+        BSM_HIP_TRY(hipMemcpyAsync(cm, pin, bytes, hipMemcpyHostToDevice, s));
+        if (k > 1) BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, cm, dst, s));
+        if (dst == dst_small && !cm_own.p) *synced = false;
         else BSM_HIP_TRY(hipStreamSynchronize(s));  // the pinned buffer is reused by the next call
         return BSM_OK;
     }
-    if (k == 1) {
-        BSM_HIP_TRY(hipMemcpyAsync(dst, cols[0], n * es, hipMemcpyHostToDevice, s));
-        return BSM_OK;
-    }
+    if (k == 1) return h2d_staged(dst, cols[0], n * es, s);
     DBuf staging;
-    BSM_TRY(staging.alloc(n * k * es));
-    for (uint64_t j = 0; j < k; ++j)
-        BSM_HIP_TRY(hipMemcpyAsync(static_cast<char*>(staging.p) + j * n * es, cols[j], n * es,
-                                   hipMemcpyHostToDevice, s));
+    BSM_TRY(staging.alloc(bytes));
+    for (uint64_t j = 0; j < k; ++j) BSM_TRY(h2d_staged(static_cast<char*>(staging.p) + j * n * es, cols[j], n * es, s));
     BSM_TRY(pack_cols_to_rowmajor(dtype, n, k, staging.p, dst, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // staging dies here
     return BSM_OK;
+}
+
+int upload_dense_cols(int dtype, uint64_t n, uint64_t k, const void* const* cols, DBuf& out, hipStream_t s) {
+    return upload_columns(dtype, n, k, cols, out, s);
 }
 
 // Download a device ROW-major n x k array into k host columns.
@@ -244,19 +284,101 @@ static int download_columns(int dtype, uint64_t n, uint64_t k, const void* dev, 
                             hipStream_t s) {
     const size_t es = dtype_size(dtype);
     if (n == 0 || k == 0) return BSM_OK;
-    if (k == 1) {
-        BSM_HIP_TRY(hipMemcpyAsync(cols[0], dev, n * es, hipMemcpyDeviceToHost, s));
-        BSM_HIP_TRY(hipStreamSynchronize(s));
-        return BSM_OK;
-    }
+    if (k == 1) return d2h_staged(cols[0], dev, n * es, s);
     DBuf staging;
     BSM_TRY(staging.alloc(n * k * es));
     BSM_TRY(unpack_rowmajor_to_cols(dtype, n, k, dev, staging.p, s));
     for (uint64_t j = 0; j < k; ++j)
-        BSM_HIP_TRY(hipMemcpyAsync(cols[j], static_cast<const char*>(staging.p) + j * n * es, n * es,
-                                   hipMemcpyDeviceToHost, s));
-    BSM_HIP_TRY(hipStreamSynchronize(s));
+        BSM_TRY(d2h_staged(cols[j], static_cast<const char*>(staging.p) + j * n * es, n * es, s));
     return BSM_OK;
+}
+
+// Rows [r0, r1) of a host finalised Csr (absolute usize row_ptr) as a new
+// handle on the current device: row_ptr rebased to 0, columns narrowed to
+// int32 and checked on the device (an out-of-range column is the reference's
+// index panic, sparse.rs:437), values copied.
+int csr_upload_rows(int dtype, uint64_t r0, uint64_t r1, uint64_t cols, const uint64_t* row_ptr,
+                    const uint64_t* col_idx, const void* vals, bsm_csr** out, hipStream_t s) {
+    const uint64_t base = row_ptr[r0], nnz = row_ptr[r1] - base, rows = r1 - r0;
+    const size_t es = dtype_size(dtype);
+    bsm_csr* m = nullptr;
+    BSM_TRY(csr_alloc(&m, dtype, rows, cols, nnz));
+    uint64_t bad = 0;
+    int rc = h2d_row_ptr(m->row_ptr, row_ptr + r0, rows + 1, base, s);
+    if (rc == BSM_OK) rc = h2d_cols_narrow(m->col, col_idx + base, nnz, cols, &bad, s);
+    if (rc == BSM_OK && bad) {
+        set_error("column index out of bounds (>= cols %llu) in %llu entries", (unsigned long long)cols,
+                  (unsigned long long)bad);
+        rc = BSM_ERR_PANIC;
+    }
+    if (rc == BSM_OK) rc = h2d_staged(m->vals, static_cast<const char*>(vals) + base * es, nnz * es, s);
+    if (rc == BSM_OK) rc = csr_analyse(m, s);
+    if (rc != BSM_OK) {
+        bsm_csr_free(m);
+        return rc;
+    }
+    *out = m;
+    return BSM_OK;
+}
+
+// The SpMM schedule of a handle for k right-hand columns, built once per
+// matrix (like the matrix itself): the row-block x column-panel copy when
+// wanted (schedule 0) or possible (1), else the column-panel plan. Declined
+// shapes or no memory for the copy (with `reserve` bytes left free for the
+// call's own buffers) fall back to the plans. Caller holds a->plan_mu.
+int spmm_prepare_locked(const bsm_csr* a, uint64_t k, int schedule, uint64_t reserve, hipStream_t s,
+                        PlanTimes* pt) {
+    if (k == 0) return BSM_OK;
+    const auto t_start = host_now();
+    if (schedule != 2 && !a->tiled_tried && !spmm_wants_split(a->dtype, k, a->max_row_len) &&
+        (schedule == 1 ? a->dtype == BSM_F64 && (k == 1 || k == 32) && a->nnz > 0
+                       : tiled_wanted(a->dtype, a->rows, a->cols, a->nnz, k, a->max_row_len))) {
+        a->tiled_tried = true;
+        bsm_tiled* t = nullptr;
+        const int rc = tiled_create(a->rows, a->cols, a->nnz, a->row_ptr, a->col, static_cast<const double*>(a->vals),
+                                    k, schedule == 1 ? BSM_TILED_ANY_PADDING : 0, &t, s, reserve, pt);
+        if (rc == BSM_OK) a->tiled = t;
+        else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
+    }
+    if (schedule != 2 && a->tiled && a->tiled->k == k) {
+        if (pt) pt->total_ms += ms_since(t_start);
+        return BSM_OK;
+    }
+    const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
+    if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
+        const auto t0 = host_now();
+        if (a->plan_seg) (void)hipFree(a->plan_seg);
+        a->plan_seg = nullptr;
+        a->plan_cols = 0;
+        DBuf seg;
+        BSM_TRY(seg.alloc(spmm_plan_bytes(a->rows, a->cols, w)));
+        int usable = 0;
+        BSM_TRY(spmm_plan(a->rows, a->cols, a->row_ptr, a->col, w, seg.as<int32_t>(), &usable, s));
+        a->plan_seg = seg.as<int32_t>();
+        seg.release();
+        a->plan_cols = w;
+        a->plan_usable = usable != 0;
+        if (pt) pt->panel_ms += ms_since(t0);
+    }
+    if (pt) pt->total_ms += ms_since(t_start);
+    return BSM_OK;
+}
+
+// Launch Y = A X with the schedule spmm_prepare_locked built (async on s).
+int spmm_launch_locked(const bsm_csr* a, uint64_t k, bool allow_tiled, const void* x, void* y, int32_t* nz,
+                       hipStream_t s) {
+    if (k == 0) {
+        if (nz && a->rows) BSM_HIP_TRY(hipMemsetAsync(nz, 0, a->rows * sizeof(int32_t), s));
+        return BSM_OK;
+    }
+    const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
+    if (allow_tiled && a->tiled && a->tiled->k == k) return tiled_spmm(a->tiled, x, y, nz, false, s);
+    if (spmm_wants_split(a->dtype, k, a->max_row_len))
+        return spmm_split_dispatch(a->dtype, a->rows, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, s);
+    if (w && a->plan_usable && a->plan_cols == w)
+        return spmm_panelled(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, w,
+                             a->plan_seg, s);
+    return spmm_dispatch(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, false, s);
 }
 
 // mul_dense core on device operands: Y = A X, then compaction into a Csr.
@@ -286,49 +408,15 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     // out row_ptr is allocated first (nnz unknown until the scan completes)
     DBuf out_rp;
     BSM_TRY(out_rp.alloc((rows + 1) * sizeof(int64_t)));
-    if (k == 0) {
-        BSM_HIP_TRY(hipMemsetAsync(nz, 0, rows * sizeof(int32_t), s));
-    } else {
-        const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
+    {
         // one thread at a time builds and launches with the cached plan (a
-        // rebuild frees the old plan; hipFree waits for launches using it)
+        // rebuild frees the old plan; hipFree waits for launches using it).
+        // The copy must leave room for this call's output: col + vals of up
+        // to rows x k entries (no OOM after a copy that fit).
         std::lock_guard<std::mutex> plan_lock(a->plan_mu);
-        if (!a->tiled_tried && !spmm_wants_split(a->dtype, k, a->max_row_len) &&
-            tiled_wanted(a->dtype, rows, a->cols, a->nnz, k, a->max_row_len)) {
-            // the row-block x column-panel copy (once per matrix; declined
-            // shapes or no memory for the copy fall back to the plans below)
-            a->tiled_tried = true;
-            bsm_tiled* t = nullptr;
-            const int rc = tiled_create(rows, a->cols, a->nnz, a->row_ptr, a->col,
-                                        static_cast<const double*>(a->vals), k, 0, &t, s);
-            if (rc == BSM_OK) a->tiled = t;
-            else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
-        }
-        if (a->tiled && a->tiled->k == k) {
-            BSM_TRY(tiled_spmm(a->tiled, x_dev, yp, nz, false, s));
-        } else if (w && a->plan_cols != w) {  // build (once per matrix and width) the column-panel plan
-            if (a->plan_seg) (void)hipFree(a->plan_seg);
-            a->plan_seg = nullptr;
-            a->plan_cols = 0;
-            DBuf seg;
-            BSM_TRY(seg.alloc(spmm_plan_bytes(rows, a->cols, w)));
-            int usable = 0;
-            BSM_TRY(spmm_plan(rows, a->cols, a->row_ptr, a->col, w, seg.as<int32_t>(), &usable, s));
-            a->plan_seg = seg.as<int32_t>();
-            seg.release();
-            a->plan_cols = w;
-            a->plan_usable = usable != 0;
-        }
-        if (a->tiled && a->tiled->k == k)
-            ;  // done above
-        else if (spmm_wants_split(a->dtype, k, a->max_row_len))
-            BSM_TRY(spmm_split_dispatch(a->dtype, rows, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev, yp, nz, s));
-        else if (w && a->plan_usable)
-            BSM_TRY(spmm_panelled(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
-                                  yp, nz, w, a->plan_seg, s));
-        else
-            BSM_TRY(spmm_dispatch(a->dtype, rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x_dev,
-                                  yp, nz, false, s));
+        const uint64_t reserve = small ? 0 : rows * k * (es + sizeof(int32_t)) + (rows + 1) * sizeof(int64_t);
+        BSM_TRY(spmm_prepare_locked(a, k, 0, reserve, s, nullptr));
+        BSM_TRY(spmm_launch_locked(a, k, true, x_dev, yp, nz, s));
     }
     const size_t wsb = ws.p ? ws.bytes : ws_b;
     BSM_TRY(exclusive_scan_i32_to_i64(nz, out_rp.as<int64_t>(), rows, wsp, wsb, s));
@@ -352,6 +440,7 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     r->vals = ov.release();
     r->analysed = true;
     r->rows_sorted = true;
+    r->max_row_len = k;  // a bound: at most k entries per output row
     rc = compact_dispatch(a->dtype, rows, k, yp, r->row_ptr, r->col, r->vals, s);
     if (rc == BSM_OK && small && yp != y.p) {  // nnz with the one synchronisation of the call
         hipError_t e = read_dev(&out_nnz, r->row_ptr + rows, sizeof(int64_t), s);
@@ -381,6 +470,12 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
 using namespace bsm;
 
 extern "C" {
+
+int bsm_stage_timing(int on) {
+    g_stage_on.store(on ? 1 : 0, std::memory_order_relaxed);
+    if (!on) stage_clear();
+    return BSM_OK;
+}
 
 int bsm_stage_times(int max, int* n, char* names, double* ms) {
     BSM_REQUIRE(n && (max <= 0 || (names && ms)), BSM_ERR_INVALID, "null argument");
@@ -424,42 +519,10 @@ int bsm_csr_upload(int dtype, uint64_t rows, uint64_t cols, uint64_t nnz, const 
     for (uint64_t r = 0; r < rows; ++r)
         BSM_REQUIRE(row_ptr[r] <= row_ptr[r + 1], BSM_ERR_PANIC, "row_ptr not monotone at row %llu",
                     (unsigned long long)r);
+    BSM_REQUIRE(dtype_size(dtype) != 0, BSM_ERR_INVALID, "unknown dtype %d", dtype);
     hipStream_t s;
     BSM_TRY(ctx_stream(&s));
-    bsm_csr* m = nullptr;
-    BSM_TRY(csr_alloc(&m, dtype, rows, cols, nnz));
-    std::vector<int64_t> rp64(rows + 1);
-    for (uint64_t r = 0; r <= rows; ++r) rp64[r] = (int64_t)row_ptr[r];
-    std::vector<int32_t> c32(nnz);
-    for (uint64_t e = 0; e < nnz; ++e) {
-        if (col_idx[e] >= cols) {
-            bsm_csr_free(m);
-            set_error("column index %llu >= cols %llu at entry %llu", (unsigned long long)col_idx[e],
-                      (unsigned long long)cols, (unsigned long long)e);
-            return BSM_ERR_PANIC;
-        }
-        c32[e] = (int32_t)col_idx[e];
-    }
-    int rc = BSM_OK;
-    auto cp = [&](void* d, const void* h, size_t b) {
-        if (rc == BSM_OK && b) {
-            hipError_t e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, s);
-            if (e != hipSuccess) {
-                set_error("hipMemcpyAsync: %s", hipGetErrorString(e));
-                rc = BSM_ERR_HIP;
-            }
-        }
-    };
-    cp(m->row_ptr, rp64.data(), (rows + 1) * sizeof(int64_t));
-    cp(m->col, c32.data(), nnz * sizeof(int32_t));
-    cp(m->vals, vals, nnz * dtype_size(dtype));
-    if (rc == BSM_OK) rc = csr_analyse(m, s);  // syncs: host vectors may die after this
-    if (rc != BSM_OK) {
-        bsm_csr_free(m);
-        return rc;
-    }
-    *out = m;
-    return BSM_OK;
+    return csr_upload_rows(dtype, 0, rows, cols, row_ptr, col_idx, vals, out, s);
 }
 
 int bsm_csr_from_inserts(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const uint64_t* row,
@@ -527,21 +590,16 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     const size_t es = dtype_size(m->dtype);
     const size_t rp_b = (m->rows + 1) * sizeof(int64_t), col_b = m->nnz * sizeof(int32_t), val_b = m->nnz * es;
     char* pin = rp_b + col_b + val_b <= PIN_MAX ? static_cast<char*>(pinned(rp_b + col_b + val_b)) : nullptr;
-    std::vector<int64_t> rp_v;
-    std::vector<int32_t> c_v;
-    int64_t* rp64;
-    int32_t* c32;
-    char* vdst = static_cast<char*>(vals);
-    if (pin) {  // small: three copies into one pinned buffer, one sync
-        rp64 = reinterpret_cast<int64_t*>(pin);
-        c32 = reinterpret_cast<int32_t*>(pin + rp_b);
-        vdst = pin + rp_b + col_b;
-    } else {
-        rp_v.resize(m->rows + 1);
-        c_v.resize(m->nnz);
-        rp64 = rp_v.data();
-        c32 = c_v.data();
+    if (!pin) {  // large: staged pipelines, columns widened to usize on the device
+        if (row_ptr) BSM_TRY(d2h_staged(row_ptr, m->row_ptr, rp_b, s));  // int64 >= 0: the same bits as u64
+        if (col_idx) BSM_TRY(d2h_cols_widen(col_idx, m->col, m->nnz, s));
+        if (vals) BSM_TRY(d2h_staged(vals, m->vals, val_b, s));
+        return BSM_OK;
     }
+    // small: three copies into one pinned buffer, one sync
+    int64_t* rp64 = reinterpret_cast<int64_t*>(pin);
+    int32_t* c32 = reinterpret_cast<int32_t*>(pin + rp_b);
+    char* vdst = pin + rp_b + col_b;
     BSM_HIP_TRY(hipMemcpyAsync(rp64, m->row_ptr, rp_b, hipMemcpyDeviceToHost, s));
     if (m->nnz) {
         BSM_HIP_TRY(hipMemcpyAsync(c32, m->col, col_b, hipMemcpyDeviceToHost, s));
@@ -552,7 +610,7 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
         for (uint64_t r = 0; r <= m->rows; ++r) row_ptr[r] = (uint64_t)rp64[r];
     if (col_idx)
         for (uint64_t e = 0; e < m->nnz; ++e) col_idx[e] = (uint64_t)c32[e];
-    if (pin && vals && val_b) std::memcpy(vals, vdst, val_b);
+    if (vals && val_b) std::memcpy(vals, vdst, val_b);
     return BSM_OK;
 }
 
@@ -577,7 +635,9 @@ int bsm_csr_mul_dense(const bsm_csr* a, uint64_t k, uint64_t x_rows, const void*
     void* xp = nullptr;
     bool synced = true;
     const size_t x_b = x_rows * k * dtype_size(a->dtype);
-    int rc = upload_columns(a->dtype, x_rows, k, x_cols, x, s, &xp, scratch(3, x_b), &synced);
+    // the arena slot only serves the pinned (small) upload path
+    void* small_x = x_b && x_b <= PIN_MAX ? scratch(3, x_b) : nullptr;
+    int rc = upload_columns(a->dtype, x_rows, k, x_cols, x, s, &xp, small_x, &synced);
     if (rc == BSM_OK) rc = mul_dense_device(a, k, xp, out, s);
     if (!synced) (void)hipStreamSynchronize(s);  // the pinned upload buffer is free again on every path
     return rc;
@@ -658,6 +718,7 @@ int bsm_csr_cholesky(const bsm_csr* a, bsm_csr** out) {
                 "cholesky_decomp is defined for f32 (reference) and f64 only");
     hipStream_t s;
     BSM_TRY(ctx_stream(&s));
+    stage_reset(s);
     return solve_dispatch_cholesky(a, out, s);
 }
 

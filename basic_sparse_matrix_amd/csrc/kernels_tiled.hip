@@ -96,7 +96,10 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
     // per chunk at the task's own density plus a margin, so that the waves of a
     // batch (equal work at C4) stay on the same panels in step without talking
     // to each other; a wave that falls behind catches up by the margin
-    const int64_t t0 = rp[r0], t1 = rp[min<uint64_t>(r0 + rw, wend)];
+    // a task past the last row (rows < nw, or a wave's trailing batches) is
+    // empty: it must not read row_ptr beyond rows + 1 entries
+    const bool any = r0 < wend;
+    const int64_t t0 = any ? rp[r0] : 0, t1 = any ? rp[min<uint64_t>(r0 + rw, wend)] : 0;
     const double np = (double)(((n_cols - 1) >> pshift) + 1);
     const double inv_r = t1 > t0 ? (double)CHUNK * np / ((double)(t1 - t0) * pace) : 1e30;
     int64_t c = WRITE ? offs[task] : 0;
@@ -435,7 +438,8 @@ bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint6
 }
 
 int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s) {
+                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve,
+                 PlanTimes* pt) {
     BSM_REQUIRE(out && rp && (nnz == 0 || (col && vals)), BSM_ERR_INVALID, "tiled: null argument");
     BSM_REQUIRE(k == 32 || k == 1, BSM_ERR_UNSUPPORTED, "tiled: k must be 32 or 1");
     const uint32_t rbits = k == 1 ? K1_RBITS : 8;
@@ -478,12 +482,24 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     };
+    // phase timers (bsm_mcsr_prepare's plan_ms): host clock around each
+    // phase, the stream synchronised at its end (the phases are long)
+    auto t_phase = host_now();
+    auto phase_end = [&](double* acc) -> int {
+        if (!pt) return BSM_OK;
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        *acc += ms_since(t_phase);
+        t_phase = host_now();
+        return BSM_OK;
+    };
     BSM_TRY(layout(std::false_type{}, counts.as<int32_t>(), nullptr, nullptr, nullptr));
+    BSM_TRY(phase_end(pt ? &pt->count_ms : nullptr));
     const uint64_t wsb = scan_workspace_bytes(tasks);
     BSM_TRY(ws.alloc(wsb));
     BSM_TRY(exclusive_scan_i32_to_i64(counts.as<int32_t>(), offs.as<int64_t>(), tasks, ws.p, wsb, s));
     int64_t total = 0;
     BSM_HIP_TRY(read_dev(&total, offs.as<int64_t>() + tasks, sizeof(total), s));
+    BSM_TRY(phase_end(pt ? &pt->scan_ms : nullptr));
     // a stream much longer than the matrix means rows too uneven for 64-row chunks
     BSM_REQUIRE((flags & BSM_TILED_ANY_PADDING) ||
                     (uint64_t)total * CHUNK <= nnz + nnz / 4 + tasks * pad * CHUNK + (uint64_t)CHUNK * 64,
@@ -492,17 +508,20 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     const uint64_t slots = ((uint64_t)total + overread) * CHUNK;
     size_t free_b = 0, total_b = 0;
     BSM_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    BSM_REQUIRE(slots * 12 + (256ull << 20) < free_b, BSM_ERR_OOM, "tiled: %llu MB stream does not fit",
-                (unsigned long long)(slots * 12 >> 20));
+    BSM_REQUIRE(slots * 12 + (256ull << 20) + reserve < free_b, BSM_ERR_OOM,
+                "tiled: %llu MB stream (+%llu MB reserved) does not fit", (unsigned long long)(slots * 12 >> 20),
+                (unsigned long long)(reserve >> 20));
     DBuf meta, val, bar;
     BSM_TRY(bar.alloc(8 * BAR_STRIDE * sizeof(unsigned)));
     BSM_TRY(meta.alloc(slots * sizeof(uint32_t)));
     BSM_TRY(val.alloc(slots * sizeof(double)));
+    BSM_TRY(phase_end(pt ? &pt->alloc_ms : nullptr));
     BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.as<uint32_t>(), val.as<double>()));
     // over-read padding: valid dummy entries (X row 0)
     BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 4, s));
     BSM_HIP_TRY(hipMemsetAsync(val.as<double>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 8, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
+    BSM_TRY(phase_end(pt ? &pt->write_ms : nullptr));
     auto* t = new bsm_tiled;
     t->device = dev;
     t->k = k;

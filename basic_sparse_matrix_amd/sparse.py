@@ -23,6 +23,7 @@ from typing import Any, List, Optional
 import numpy as np
 
 from . import _lib
+from . import multi as _multi
 from .dense import Dense, _infer_dtype
 from .dense_static import DenseS
 from .util import GetDims, MatDim, MatErr, MatErrKind, Panic
@@ -116,7 +117,7 @@ def _raise_for(code: int) -> None:
 
 class Csr(GetDims):
     __slots__ = ("dims", "dtype", "v", "col_index", "row_index", "is_finalised", "iter_v_index",
-                 "iter_row_index", "_dev")
+                 "iter_row_index", "_dev", "_mdev")
 
     # ------------------------------------------------------------------ ctor
     def __init__(self, dims, dtype=np.int32, capacity: int = 0):
@@ -130,6 +131,7 @@ class Csr(GetDims):
         self.iter_v_index = 0
         self.iter_row_index = 0
         self._dev = None
+        self._mdev = None  # (gpus, chunks, MultiCsr) of the multi-GPU path
 
     @classmethod
     def new(cls, dims, dtype=np.int32) -> "Csr":
@@ -378,6 +380,22 @@ class Csr(GetDims):
             self._dev = dev
         return dev
 
+    def _multi_device(self):
+        """The matrix partitioned over the multi-GPU context (set_gpus), cached
+        like the single-GPU copy for a finalised (immutable) matrix."""
+        key = (_multi.gpus(), _multi.chunks())
+        if self._mdev is not None and self._mdev[0] == key:
+            return self._mdev[1]
+        if self.dtype not in GPU_DTYPES:
+            raise TypeError(f"Csr<{self.dtype}> has no GPU path (supported: f64 f32 i32 u32 i64 u64)")
+        rp, ci, v = self._csr_arrays()
+        if ci.size and int(ci.max()) >= self.dims.cols:
+            raise Panic(f"index out of bounds: column {int(ci.max())} >= {self.dims.cols}")
+        m = _multi.MultiCsr.upload(_multi.context(), self.dims.rows, self.dims.cols, rp, ci, v, chunks=key[1])
+        if self.is_finalised:
+            self._mdev = (key, m)
+        return m
+
     @classmethod
     def _from_device(cls, dev: "_lib.DeviceCsr") -> "Csr":
         rp, ci, v = dev.download()
@@ -423,6 +441,8 @@ class Csr(GetDims):
                     raise Panic(f"index out of bounds: the len is {a.shape[0]} but the index is {int(ci.max())}")
                 a = np.concatenate([a, np.zeros(x_rows - a.shape[0], dtype=a.dtype)])
             arrs.append(np.ascontiguousarray(a[:x_rows]))
+        if _multi.gpus() is not None:  # row blocks on n GPUs + RCCL all-gather (csrc/multi.hip)
+            return Csr._from_device(self._multi_device().mul_dense_cols(arrs, x_rows))
         out = ctypes.c_void_p()
         _raise_for(lib.bsm_csr_mul_dense(dev.handle, len(arrs), x_rows, _lib.ptr_array(arrs), ctypes.byref(out)))
         return Csr._from_device(_lib.DeviceCsr(out.value))
@@ -524,6 +544,7 @@ class Csr(GetDims):
         m.is_finalised = self.is_finalised
         m.iter_v_index, m.iter_row_index = self.iter_v_index, self.iter_row_index
         m._dev = self._dev
+        m._mdev = self._mdev
         return m
 
     def __repr__(self) -> str:  # Debug (sparse.rs:797-805)

@@ -5,19 +5,26 @@
 Workload (BASELINE.json north_star target / configs[3]): A = 10M x 10M
 synthetic random CSR, 1000 nnz per row (0.01 % density, nnz = 1e10), f64,
 times a dense 10M x 32 f64 RHS. It fits one MI355X (A 120 GB + X/Y 5 GB of
-288 GB HBM), so N=1 runs the whole matrix on one GPU. For N > 1 the rows are
-split block-cyclically (one process per GPU): `--chunks` rounds of N equal
-row blocks, rank g owning block g of every round (equal rows = equal nnz). X
-is replicated (every rank generates the same X from its seed -- no transfer)
-and the dense result Y is assembled on every rank with RCCL all-gathers over
-xGMI, as north_star specifies: one async all-gather per round, issued as soon
-as that round's SpMM is enqueued, so it overlaps the next round's SpMM and
-lands in global row order. Total work is fixed as N grows ("strong").
+288 GB HBM), so N=1 runs the whole matrix on one GPU.
+
+The measured path is the library's multi-GPU C-ABI (include/bsm.h
+"multi-GPU", csrc/multi.hip), the same entry points a Rust `mul_dense`
+binds: one process per GPU, each rank's context made by
+bsm_multi_create_rank from an RCCL id that rank 0 ships through
+torch.distributed (backend nccl = RCCL), or, run without a launcher, by
+bsm_multi_create(1) (ncclCommInitAll over the one GPU). The CSR is cut into
+`--chunks` x N nnz-balanced row blocks (block c*N + g on rank g, computed in
+round c), generated on each rank's device. X is generated on rank 0 and
+replicated by the library's ncclBroadcast (untimed setup). Every round's Y
+blocks are all-gathered in place by the library's own RCCL communicator on a
+communication stream, overlapping the next round's SpMM, and every rank
+compacts the assembled Y into the output Csr. Total work is fixed as N grows
+("strong").
 
 One step = the hot path of Csr::mul_dense (src/sparse.rs:426-446) over the
-whole matrix: SpMM kernel (Y block) -> [all-gather of Y blocks] ->
-compaction of Y into the output Csr (zero-dropping insert, sparse.rs:229).
-Inputs are resident in HBM before timing starts.
+whole matrix: SpMM rounds -> RCCL all-gathers of Y and of the per-row
+nonzero counts -> compaction of Y into the output Csr (zero-dropping insert,
+sparse.rs:229). Inputs are resident in HBM before timing starts.
 
 value = B_alg / step time (whole job), with the canonical algorithmic bytes
 of SURVEY.md §8d: B_alg = 8(N+1) + 12 nnz + 8 n_cols k + 8 N k.
@@ -47,6 +54,14 @@ CONFIGS = {
 }
 C1_P = 0.01
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# The L2-served gather ceiling of the tiled kernel's own inner loop (same
+# pipeline, 16-B/lane gathers, LDS read-add-write per chunk) on a static X
+# table that stays in each XCD's L2: scripts/perf/gather_ceiling.sh,
+# profiles/r03_gather_ceiling.log ("static 2 MiB table, LDS update" line).
+# It is the peak of roofline_gather: the C4 gathers (2.56 TB) cannot be served
+# faster than the L2 serves them.
+L2_GATHER_PEAK_GBS = 17_600.0
+L2_GATHER_PEAK_SRC = "profiles/r03_gather_ceiling.log"
 ROWLEN_CONST, ROWLEN_BINOMIAL = 0, 2  # bsm_synth.h row-length families
 SEED_A, SEED_X = 1000, 1001
 
@@ -76,43 +91,44 @@ def kernel_label(rows, nnz, k, panel_cols, tiled=False):
     return "spmm_rowwave<double>"
 
 
-def end_to_end(cfg_name, blks, x, comp, step, rows, k, iters=3):
-    """End-to-end figures next to the device-resident step:
-    device_ms = H2D of X from pinned host memory + the step + D2H of the
-    output Csr (row_ptr, col, vals) into pinned host memory, A resident (as the
-    host mirror caches it); public_api_ms (host-sized configs only) =
-    Csr.mul_dense(Dense) through the public API, host Dense in, host Csr out
-    (the library's own X upload/packing and int32 -> usize column widening)."""
-    out = {}
-    n_out = comp.nnz()
-    xh = x.cpu().pin_memory()
-    rp_h = torch.empty(rows + 1, dtype=torch.int64).pin_memory()
-    col_h = torch.empty(max(1, n_out), dtype=torch.int32).pin_memory()
-    val_h = torch.empty(max(1, n_out), dtype=torch.float64).pin_memory()
-    ts = []
-    for _ in range(iters):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        x.copy_(xh, non_blocking=True)
-        step(False)
-        rp_h.copy_(comp.row_ptr, non_blocking=True)
-        col_h[:n_out].copy_(comp.col[:n_out], non_blocking=True)
-        val_h[:n_out].copy_(comp.vals[:n_out], non_blocking=True)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    out["device_ms"] = round(float(np.median(ts)) * 1e3, 3)
-    out["h2d_bytes"] = int(xh.numel() * 8)
-    out["d2h_bytes"] = int((rows + 1) * 8 + n_out * 12)
-    if len(blks) == 1 and blks[0].nnz <= 200_000_000:
-        from basic_sparse_matrix_amd import Csr, Dense
+def end_to_end(cfg_name, m, x, dev, iters=3):
+    """What a caller of the public API pays (host buffers in and out, A
+    resident on the device as the mirrors cache it), next to the
+    device-resident step:
+      multi_api_ms = bsm_mcsr_mul_dense (host X columns uploaded to every
+        device, the step, the output Csr as a handle) + bsm_csr_download into
+        usize/T host arrays: the multi-GPU path a Rust mul_dense takes;
+      public_api_ms (host-sized configs) = Csr.mul_dense(Dense) of the Python
+        mirror on one GPU (bsm_csr_mul_dense + download), host Dense in, host
+        Csr out."""
+    from basic_sparse_matrix_amd import Csr, Dense
+    from basic_sparse_matrix_amd.device import DeviceCsrBlock
 
-        b = blks[0]
-        a = Csr.from_csr_arrays((b.rows, b.n_cols), b.row_ptr.cpu().numpy().astype(np.uint64),
+    out = {}
+    rows, n_cols, k = m.rows, m.cols, int(x.shape[1])
+    xh = x.cpu().numpy()
+    x_cols = [np.ascontiguousarray(xh[:, j]) for j in range(k)]
+    ts, n_out = [], 0
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        dc = m.mul_dense_cols(x_cols, n_cols)
+        rp, ci, v = dc.download()
+        ts.append(time.perf_counter() - t0)
+        n_out = int(rp[-1])
+        del dc, rp, ci, v
+    out["multi_api_ms"] = round(float(np.median(ts)) * 1e3, 3)
+    out["h2d_bytes"] = int(n_cols * k * 8)
+    out["d2h_bytes"] = int((rows + 1) * 8 + n_out * 16)
+    if m.nnz <= 200_000_000:
+        kind, ra, rb = rowlen_spec(cfg_name)
+        b = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, kind, ra, rb, 0, np.float64, device=dev)
+        a = Csr.from_csr_arrays((rows, n_cols), b.row_ptr.cpu().numpy().astype(np.uint64),
                                 b.col.cpu().numpy().astype(np.uint64), b.vals.cpu().numpy())
-        xd = Dense.from_columns([np.ascontiguousarray(xh[:, j].numpy()) for j in range(k)])
+        del b
+        xd = Dense.from_columns(x_cols)
         a.mul_dense(xd)  # first call uploads and caches A on the device (untimed, like the bench's setup)
         ts = []
-        for _ in range(max(iters, 20 if cfg_name == "c1" else iters)):
+        for _ in range(max(iters, 20 if cfg_name in ("c1", "c2", "c3") else iters)):
             t0 = time.perf_counter()
             a.mul_dense(xd)
             ts.append(time.perf_counter() - t0)
@@ -283,6 +299,46 @@ def ref_bench_suite(iters=20, which=("sd_mul", "ss_add", "ss_mul")):
             }), flush=True)
 
 
+def verify_rows(m, x, k, dev, kind, ra, rb, full):
+    """Rank 0: compare the assembled Y and row counts with a single-GPU
+    recomputation by the other schedule (column panels / one pass), bit for
+    bit. `full`: the whole matrix (needs a second copy of A); else blocks of
+    2048 rows around every piece bound plus the first and last rows (the
+    assembly's seams), so C4 fits beside its copy."""
+    from basic_sparse_matrix_amd.device import DeviceCsrBlock
+
+    rows, n_cols = m.rows, m.cols
+    y_all = torch.empty((rows, k), dtype=torch.float64, device=dev)
+    nnz_all = torch.empty(rows, dtype=torch.int32, device=dev)
+    m.copy_y(0, y_all.data_ptr(), nnz_all.data_ptr())
+    if full:
+        spans = [(0, rows)]
+    else:
+        pts = sorted(set(int(b) for b in m.bounds()) | {0, rows})
+        spans, last = [], -1
+        for p in pts:
+            a, b = max(0, p - 1024), min(rows, p + 1024)
+            if a < last:
+                a = last
+            if b > a:
+                spans.append((a, b))
+                last = b
+    checked = 0
+    for a, b in spans:
+        blk = DeviceCsrBlock.generate(SEED_A, a, b - a, n_cols, kind, ra, rb, 0, np.float64, device=dev)
+        blk.plan(k)
+        y_ref = torch.empty((b - a, k), dtype=torch.float64, device=dev)
+        nnz_ref = torch.empty(b - a, dtype=torch.int32, device=dev)
+        blk.spmm(x, y_ref, nnz_ref)
+        ok = torch.equal(y_ref.view(torch.int64), y_all[a:b].view(torch.int64)) and torch.equal(nnz_ref, nnz_all[a:b])
+        del blk, y_ref, nnz_ref
+        if not ok:
+            log(f"verify: rows [{a}, {b}) differ")
+            return False, checked
+        checked += b - a
+    return True, checked
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,195 +354,151 @@ def main():
                     help="SpMM schedule: auto = the library's choice (row-block x column-panel copy when "
                          "wanted, else column panels), tiled = the copy whenever possible, panel = never the copy")
     ap.add_argument("--chunks", type=int, default=0,
-                    help="rounds of the block-cyclic row partition (0: 1 at N=1, 4 at N>1)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+                    help="rounds of the row partition (pieces = chunks x N; 0: 1 at N=1 or with the tiled copy, "
+                         "4 otherwise)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend under a launcher (nccl = RCCL)")
     ap.add_argument("--verify", action="store_true",
-                    help="rank 0 recomputes the whole Y on its own GPU and checks the assembled Y bit for bit")
+                    help="rank 0 recomputes Y on its own GPU by another schedule and checks the assembled Y bit for "
+                         "bit (whole matrix up to 2e9 nnz, else the rows around every piece bound)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per SpMM launch (from profiles/), reported as roofline.traffic")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (H2D/D2H included) figures")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host buffers in/out) figures")
     ap.add_argument("--ref-benches", default=None,
                     help="comma list of the reference's own criterion benches to run instead "
                          "(sd_mul,ss_add,ss_mul; one JSON line per size)")
     args = ap.parse_args()
+    if args.panel_cols is not None:
+        os.environ["BSM_SPMM_PANEL_COLS"] = str(args.panel_cols)
     if args.ref_benches:
         ref_bench_suite(which=tuple(args.ref_benches.split(",")))
         return
 
+    launched = "WORLD_SIZE" in os.environ  # torch.distributed.run sets it, also at N = 1
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    # one GPU per rank; ranks beyond the visible GPUs share them (rehearsals)
     ordinal = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(ordinal)
     dev = torch.device("cuda", ordinal)
-    if world > 1:
-        if args.backend == "nccl":
+    backend = None
+    if launched:
+        backend = args.backend
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(backend)
 
     from basic_sparse_matrix_amd import _lib
-    from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
-
-    from basic_sparse_matrix_amd.distributed import partition_rows_cyclic
+    from basic_sparse_matrix_amd.device import gen_dense
+    from basic_sparse_matrix_amd.multi import MultiCsr, MultiGpu, unique_id
 
     rows, n_cols, nnz_r, k = CONFIGS[args.config]
     kind, ra, rb = rowlen_spec(args.config)
-    # block-cyclic row partition (equal rows = equal nnz: constant row length):
-    # `chunks` rounds, each finished by its own SpMM launch and all-gathered
-    # asynchronously while the next round computes (N > 1)
-    # one round per rank when the tiled copy serves the shape: its persistent
-    # grid wants every CU (an all-gather kernel beside it would hold some and
-    # defeat its batch pacing), so the all-gather follows the SpMM instead of
-    # overlapping a next round
     lib0 = _lib.load()
     tiled_shape = args.schedule != "panel" and k in (1, 32) and bool(lib0.bsm_dev_tiled_wanted(
         _lib.DTYPE_CODES[np.dtype(np.float64)], rows, n_cols, rows * (nnz_r or 1), k, nnz_r or 1))
+    # the tiled copy's persistent grid wants every CU, so by default its rank
+    # runs one round and the all-gather follows it (--chunks overrides)
     chunks = args.chunks if args.chunks else (1 if world == 1 or tiled_shape else 4)
-    cr, pieces = partition_rows_cyclic(rows, world, chunks)
-    mine = pieces[rank]
-    my_rows = sum(n for _, n in mine)
+
+    # the library's RCCL context: the id travels over torch.distributed
+    t0 = time.perf_counter()
+    if launched:
+        obj = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx = MultiGpu.for_rank(obj[0], world, rank, ordinal)
+    else:
+        ctx = MultiGpu(1, devices=[ordinal])
+    comm_init_ms = (time.perf_counter() - t0) * 1e3
 
     t0 = time.perf_counter()
-    blks = [DeviceCsrBlock.generate(SEED_A, r0, n, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64, device=dev)
-            for r0, n in mine]
-    my_nnz = sum(b.nnz for b in blks)
-    nnz_total = my_nnz
-    if world > 1:
-        t = torch.tensor([my_nnz], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        nnz_total = int(t.item())
-    x = gen_dense(SEED_X, 0, n_cols, k, device=dev)
-    y_local = torch.empty((chunks, cr, k), dtype=torch.float64, device=dev)
-    nnz_local = torch.zeros((chunks, cr), dtype=torch.int32, device=dev)
-    if world > 1:
-        y_full = torch.empty((chunks * world * cr, k), dtype=torch.float64, device=dev)
-        nnz_full = torch.zeros(chunks * world * cr, dtype=torch.int32, device=dev)
-    else:
-        y_full, nnz_full = y_local.view(chunks * cr, k), nnz_local.view(chunks * cr)
-    comp = Compactor(rows, k, np.float64, device=dev)
+    m = MultiCsr.generate(ctx, SEED_A, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64, chunks=chunks)
+    gen_ms = (time.perf_counter() - t0) * 1e3
+    nnz_total = m.nnz
+    bounds = m.bounds()
+    my_pieces = [(int(bounds[c * world + rank]), int(bounds[c * world + rank + 1])) for c in range(chunks)]
+    my_rows = sum(b - a for a, b in my_pieces)
+    # the rows' nnz (the generator's row lengths): constant-length configs by count
+    my_nnz = my_rows * nnz_r if nnz_r else None
+    x = torch.empty((n_cols, k), dtype=torch.float64, device=dev)
+    if rank == 0:
+        x.copy_(gen_dense(SEED_X, 0, n_cols, k, device=dev))
     torch.cuda.synchronize()
-    log(f"rank {rank}: {my_rows:,} rows in {chunks} round(s) of {cr:,}, nnz {my_nnz:,} generated in "
-        f"{time.perf_counter() - t0:.1f} s")
-    # the SpMM schedule's per-matrix preparation, built once per matrix like
-    # the matrix itself (outside the timed region; its cost is reported as
-    # plan_ms): the row-block x column-panel copy, or the column-panel plan
-    t0 = time.perf_counter()
-    panel_cols, tiled, tiled_info = 0, False, None
-    if args.schedule != "panel" and k in (1, 32):
-        plans = [b.plan_tiled(k, force=args.schedule == "tiled") for b in blks]
-        tiled = all(p is not None for p in plans)
-        if tiled:
-            infos = [p.info() for p in plans]
-            tiled_info = {"bytes": sum(i["bytes"] for i in infos), "slots": sum(i["slots"] for i in infos),
-                          "panel_cols": infos[0]["panel_cols"]}
-        else:
-            for b in blks:
-                b.tiled = None
-    if not tiled:
-        for b in blks:
-            panel_cols = b.plan(k, args.panel_cols)
-    torch.cuda.synchronize()
-    plan_ms = (time.perf_counter() - t0) * 1e3
+    ctx.broadcast([x.data_ptr()], x.numel() * 8, root=0)  # X replicated over RCCL (untimed setup)
+    log(f"rank {rank}: pieces {my_pieces} of {m.pieces} ({chunks} round(s)), nnz {nnz_total:,} in total, generated in "
+        f"{gen_ms:.0f} ms; RCCL context {comm_init_ms:.0f} ms")
+    # the schedule's per-matrix preparation (outside the timed region, like the
+    # matrix itself; reported per phase as plan_ms)
+    plan = m.prepare(k, args.schedule)
+    pinfo = m.plan_info()
+    tiled = pinfo["tiled_pieces"] == pinfo["local_pieces"] and pinfo["tiled_pieces"] > 0
+    panel_cols = 0 if tiled else pinfo["panel_cols"]
     n_passes = -(-n_cols // panel_cols) if panel_cols else 1
-    if tiled:
-        log(f"rank {rank}: row-block x column-panel copy {tiled_info}, built in {plan_ms:.1f} ms")
-    else:
-        log(f"rank {rank}: panel width {panel_cols} ({n_passes} passes), plan {plan_ms:.1f} ms")
+    log(f"rank {rank}: schedule {pinfo}, plan {plan}")
+    if my_nnz is None:  # variable row lengths (C1): count them on the device
+        from basic_sparse_matrix_amd.device import DeviceCsrBlock
 
-    # one set of events per timed step, read after the timed region: no host
-    # synchronisation between steps (small configs would time the bubble)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    kern_ms, comm_ms, comp_ms = [], [], []
-    round_rows = world * cr
+        my_nnz = sum(DeviceCsrBlock.generate(SEED_A, a, b - a, n_cols, kind, ra, rb, 0, np.float64, device=dev).nnz
+                     for a, b in my_pieces)
 
-    def step(timed):
-        if timed:
-            ev_k0, ev_k1, ev_c0, ev_c1 = evs[timed - 1]
-            ev_k0.record()
-        works = []
-        for c, b in enumerate(blks):
-            b.spmm(x, y_local[c, :b.rows], nnz_local[c, :b.rows])
-            if world > 1:  # RCCL all-gather of this round's Y rows (+ nnz counts), overlapped with the next
-                works.append(dist.all_gather_into_tensor(y_full[c * round_rows:(c + 1) * round_rows], y_local[c],
-                                                         async_op=True))
-                works.append(dist.all_gather_into_tensor(nnz_full[c * round_rows:(c + 1) * round_rows],
-                                                         nnz_local[c], async_op=True))
-        if timed:
-            ev_k1.record()
-        for w in works:
-            w.wait()
-        if timed:
-            ev_c0.record()
-        comp(y_full[:rows], nnz_full[:rows])
-        if timed:
-            ev_c1.record()
-
+    xp = [x.data_ptr()]
     for _ in range(args.warmup):
-        step(False)
+        m.step(xp)
     torch.cuda.synchronize()
-    if world > 1:
+    m.reset_times()
+    if launched:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(i + 1)
+    for _ in range(args.steps):
+        m.step(xp)
     torch.cuda.synchronize()
-    if world > 1:
+    if launched:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    for ev_k0, ev_k1, ev_c0, ev_c1 in evs:
-        kern_ms.append(ev_k0.elapsed_time(ev_k1))
-        comm_ms.append(ev_k1.elapsed_time(ev_c0))
-        comp_ms.append(ev_c0.elapsed_time(ev_c1))
-    log(f"rank {rank}: SpMM kernel ms per timed step: {[round(t, 2) for t in kern_ms]}")
-    if world > 1:
+    times = m.step_times(0)[:args.steps]
+    kern_ms = [t["spmm"] for t in times]
+    comm_ms = [t["allgather_tail"] for t in times]
+    comp_ms = [t["compaction"] for t in times]
+    log(f"rank {rank}: SpMM ms per timed step: {[round(t, 2) for t in kern_ms]}")
+    if launched:
         t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmax = float(t[0]), float(t[1])
     else:
         kmax = float(np.mean(kern_ms))
 
-    verified = None
+    verified, verified_rows = None, 0
     if args.verify:
-        if rank == 0:  # the whole product on one GPU, compared with the assembled one
-            full = DeviceCsrBlock.generate(SEED_A, 0, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64,
-                                           device=dev)
-            full.plan(k, args.panel_cols)  # the other schedule than the tiled ranks use: same bits
-            y_ref = torch.empty((rows, k), dtype=torch.float64, device=dev)
-            nnz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
-            full.spmm(x, y_ref, nnz_ref)
-            verified = bool(torch.equal(y_ref.view(torch.int64), y_full[:rows].reshape(rows, k).view(torch.int64))
-                            and torch.equal(nnz_ref, nnz_full[:rows]))
-            del full, y_ref, nnz_ref
-            log(f"verify: assembled Y {'==' if verified else '!='} single-GPU Y")
-        if world > 1:
+        if rank == 0:
+            verified, verified_rows = verify_rows(m, x, k, dev, kind, ra, rb, full=nnz_total <= 2_000_000_000)
+            log(f"verify: assembled Y {'==' if verified else '!='} single-GPU Y on {verified_rows:,} rows")
+        if launched:
             dist.barrier()
-    out_nnz = comp.nnz()
     e2e = None
     if world == 1 and not args.no_e2e:
-        e2e = end_to_end(args.config, blks, x, comp, step, rows, k)
+        e2e = end_to_end(args.config, m, x, dev)
         log(f"end to end: {e2e}")
     ms_per_step = elapsed / args.steps * 1e3
     value = b_alg(rows, n_cols, nnz_total, k) / (elapsed / args.steps) / 1e9
-    # roofline of the dominant kernel (the SpMM: n_passes launches of the
-    # panelled kernel, bracketed together by the HIP events): algorithmic
-    # bytes of THIS rank's SpMM over its measured average duration
+    # roofline of the dominant kernel (the SpMM rounds on the compute stream,
+    # bracketed by the library's HIP events): algorithmic bytes of THIS rank's
+    # SpMM over its measured average duration
     b_launch = b_alg(my_rows, n_cols, my_nnz, k)
-    achieved = b_launch / (float(np.mean(kern_ms)) / 1e3) / 1e9
-    achieved_gather = b_gather(my_rows, my_nnz, k) / (float(np.mean(kern_ms)) / 1e3) / 1e9
+    t_k = float(np.mean(kern_ms)) / 1e3
+    achieved = b_launch / t_k / 1e9
+    achieved_gather = b_gather(my_rows, my_nnz, k) / t_k / 1e9
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             log("timing cpu baseline ...")
             cpu = cpu_baseline(args.config, args.cpu_sample_rows)
-        traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
+        traffic, traffic_src, pmc = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None, None
         pmc_json = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
-        if traffic is None and world == 1 and os.path.exists(pmc_json):
+        if traffic is None and world == 1 and chunks == 1 and os.path.exists(pmc_json):
             # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this kernel on
             # this config (separate runs), corrected per MI355X_MICROARCH.md
             with open(pmc_json) as f:
@@ -495,6 +507,10 @@ def main():
                     "tiled" if tiled else "panel"):  # same schedule as this run
                 traffic = pmc["traffic_bytes_per_launch"] * pmc.get("launches_per_spmm", 1)
                 traffic_src = os.path.relpath(pmc_json, ROOT)
+            else:
+                pmc = None
+        comm = (f"library RCCL all-gather (bsm_mcsr_step; {world} rank(s)"
+                + (f", context id over torch.distributed {backend})" if launched else ", ncclCommInitAll)"))
         line = {
             "metric": "CSR x dense SpMM effective GB/s (B_alg / step time); nnz/s",
             "value": round(value, 2),
@@ -512,56 +528,64 @@ def main():
             "config": {
                 "workload": f"{args.config}: {rows:,} x {n_cols:,} CSR, "
                             + (f"{nnz_r} nnz/row" if nnz_r else f"Binomial({n_cols}, {C1_P:g}) nnz/row")
-                            + f" ({100.0 * nnz_total / rows / n_cols:.3g} % density, nnz {nnz_total:,}) x {k}-column dense RHS, "
-                            f"f64; step = SpMM + {'RCCL all-gather of Y + ' if world > 1 else ''}compaction "
-                            f"to Csr",
+                            + f" ({100.0 * nnz_total / rows / n_cols:.3g} % density, nnz {nnz_total:,}) x {k}-column "
+                              f"dense RHS, f64; step = SpMM rounds + RCCL all-gather of Y + compaction to Csr",
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
-                "parallelism": f"row-block x{world}" + (f" (block-cyclic, {chunks} rounds) + overlapped all-gather"
-                                                         if world > 1 else ""),
+                "parallelism": f"row-block x{world}, {chunks} round(s) of {world} nnz-balanced pieces",
+                "comm": comm,
                 "schedule": f"row-block x column-panel copy (spmm_tiled_k{k})" if tiled else
                             ("column panels" if panel_cols else "one pass"),
-                "panel_cols": tiled_info["panel_cols"] if tiled else panel_cols, "passes": n_passes,
-                "plan_ms": round(plan_ms, 1),
-                "tiled_copy": tiled_info,
+                "panel_cols": pinfo["panel_cols"], "passes": n_passes,
+                "plan_ms": plan,
+                "generate_ms": round(gen_ms, 1),
+                "comm_init_ms": round(comm_init_ms, 1),
+                "tiled_copy_bytes": pinfo["copy_bytes"] if tiled else None,
             },
             "nnz_per_s": round(nnz_total / (elapsed / args.steps), 1),
             "hbm_frac_of_peak": round(value / (world * HBM_PEAK_GBS), 5),
             "breakdown_ms": {
                 "spmm_kernel_mean": round(float(np.mean(kern_ms)), 3),
                 "spmm_kernel_max_over_ranks": round(kmax, 3),
-                "allgather_mean": round(float(np.mean(comm_ms)), 3),
+                "allgather_tail_mean": round(float(np.mean(comm_ms)), 3),
                 "compaction_mean": round(float(np.mean(comp_ms)), 3),
+                "spmm_kernel_per_step": [round(t, 3) for t in kern_ms],
             },
-            "output_nnz": out_nnz,
             "verified_vs_single_gpu": verified,
+            "verified_rows": verified_rows if args.verify else None,
             "roofline": {
                 "bound": "hbm",
                 "kernel": kernel_label(my_rows, my_nnz, k, panel_cols, tiled),
                 "model": "B_alg (SURVEY.md §8d canonical: X and Y counted once)",
-                "launches_per_spmm": n_passes,
+                "launches_per_spmm": n_passes * chunks,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "traffic_GBps": round(traffic / (float(np.mean(kern_ms)) / 1e3) / 1e9, 1) if traffic else None,
+                "traffic_GBps": round(traffic / t_k / 1e9, 1) if traffic else None,
+                "traffic_split": {key: pmc[key] for key in ("stream_bytes", "gather_bytes", "write_bytes")
+                                  if key in pmc} if pmc else None,
                 "bytes_per_launch_alg": b_launch,
             },
             "roofline_gather": {
-                "bound": "hbm",
-                "model": "B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row)",
+                "bound": "l2_gather",
+                "model": "B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row); peak = the "
+                         "measured L2-served gather rate of the same inner loop on a static L2-resident X table",
                 "achieved": round(achieved_gather, 2),
-                "peak": HBM_PEAK_GBS,
+                "peak": L2_GATHER_PEAK_GBS,
+                "peak_source": L2_GATHER_PEAK_SRC,
                 "unit": "GB/s",
-                "frac": round(achieved_gather / HBM_PEAK_GBS, 5),
+                "frac": round(achieved_gather / L2_GATHER_PEAK_GBS, 5),
                 "bytes_per_launch_gather": b_gather(my_rows, my_nnz, k),
             },
             "end_to_end_ms": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    del m
+    ctx.close()
+    if launched:
         dist.destroy_process_group()
 
 

@@ -61,7 +61,8 @@ typedef enum bsm_status {
     BSM_ERR_OOM = 6,         /* device allocation failed */
     BSM_ERR_UNSUPPORTED = 7, /* valid input outside what this build implements */
     BSM_ERR_NO_DEVICE = 8,   /* no usable gfx950 device */
-    BSM_ERR_OUT_OF_BOUNDS = 9 /* MatErr::OutOfBounds (util.rs:54; COO::insert, sparse.rs:45-53) */
+    BSM_ERR_OUT_OF_BOUNDS = 9, /* MatErr::OutOfBounds (util.rs:54; COO::insert, sparse.rs:45-53) */
+    BSM_ERR_COMM = 10          /* RCCL error (multi-GPU entry points) */
 } bsm_status;
 
 /* Opaque device-resident CSR matrix (a finalised Csr<T>, sparse.rs:68-78). */
@@ -71,9 +72,12 @@ typedef struct bsm_csr bsm_csr;
 int bsm_api_version(void);
 /* Thread-local description of the last failure on this thread. */
 const char* bsm_last_error(void);
-/* Device time of the stages of the last bsm_solve / bsm_solve_blocked on
- * this thread (HIP events on its stream): *n stages; the first min(max, *n)
- * names (32 chars each, NUL-terminated) and durations in ms. Diagnostic. */
+/* Device time of the stages of the last bsm_solve / bsm_solve_blocked /
+ * bsm_csr_cholesky on this thread (HIP events on its stream): *n stages; the
+ * first min(max, *n) names (32 chars each, NUL-terminated) and durations in
+ * ms. Diagnostic, recorded only while armed by bsm_stage_timing(1) (or env
+ * BSM_STAGE_TIMES=1). */
+int bsm_stage_timing(int on);
 int bsm_stage_times(int max, int* n, char* names, double* ms);
 int bsm_device_count(int* n);
 /* Select the device used by subsequent calls on this thread. */
@@ -246,6 +250,92 @@ void bsm_tiled_destroy(bsm_tiled* t);
 int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y,
                     const int32_t* row_nnz, int64_t* out_row_ptr, int32_t* out_col,
                     void* out_vals, void* workspace, uint64_t workspace_bytes, void* stream);
+
+/* ---- multi-GPU: row blocks + RCCL all-gather (north_star) ----
+ * Csr::mul_dense (sparse.rs:426-446) has independent rows (:431-444), so the
+ * CSR is cut into P = chunks x world contiguous row blocks of near-equal nnz
+ * ("pieces"; bound i is the first row whose start is >= i*nnz/P). Piece
+ * c*world + g belongs to global rank g and is computed in round c. Every
+ * device keeps a replica of X. The dense Y blocks are assembled on every
+ * device by RCCL all-gathers, one per round, in place and issued on a
+ * communication stream as soon as the round's SpMM is done, so they overlap
+ * the next round's SpMM. The output Csr is compacted on the first local
+ * device of each process. Per-row sums do not depend on the partition, so
+ * the result is bit-identical to bsm_csr_mul_dense.
+ *
+ * Two ways to build the context:
+ *  - one process drives n_gpus devices (the reference's single-threaded Rust
+ *    caller on an 8-GPU node): bsm_multi_create, i.e. SURVEY.md §8b's
+ *    bsm_init(int n_gpus) with ncclCommInitAll;
+ *  - one process per GPU (bench.py under torch.distributed.run): rank 0 calls
+ *    bsm_multi_unique_id, the caller ships the BSM_UNIQUE_ID_BYTES bytes to
+ *    every rank, and each rank calls bsm_multi_create_rank (ncclCommInitRank).
+ * Every rank of a communicator must make the same collective calls
+ * (bsm_mcsr_mul_dense, bsm_mcsr_step, bsm_multi_broadcast) in the same order. */
+typedef struct bsm_multi bsm_multi;
+typedef struct bsm_mcsr bsm_mcsr;
+#define BSM_UNIQUE_ID_BYTES 128
+int bsm_multi_create(int n_gpus, const int* devices, bsm_multi** out);
+int bsm_multi_unique_id(void* id);
+int bsm_multi_create_rank(const void* id, int world, int rank, int device, bsm_multi** out);
+/* world size, devices driven by this process, global rank of the first one */
+int bsm_multi_info(const bsm_multi* ctx, int* world, int* n_local, int* first_rank);
+/* Broadcast `bytes` from global rank `root` (its first local device's buffer)
+ * into bufs[i] on every local device i (ncclBroadcast; synchronous). */
+int bsm_multi_broadcast(bsm_multi* ctx, void* const* bufs, uint64_t bytes, int root);
+/* SURVEY.md §8b bsm_finalize: releases streams and communicators. Matrices
+ * made on the context must be freed first. */
+void bsm_multi_destroy(bsm_multi* ctx);
+
+/* Partitioned upload of a finalised Csr<T> (host arrays, as bsm_csr_upload):
+ * each process uploads only its own devices' pieces. chunks >= 1. */
+int bsm_mcsr_upload(bsm_multi* ctx, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz,
+                    const uint64_t* row_ptr, const uint64_t* col_idx, const void* vals, uint32_t chunks,
+                    bsm_mcsr** out);
+/* The synthetic matrix of bsm_dev_gen_row_ptr/bsm_dev_gen_entries (seed,
+ * row-length family, value family), every device generating only its own
+ * pieces (C4's 1e10 entries do not fit a host). */
+int bsm_mcsr_generate(bsm_multi* ctx, int dtype, uint64_t seed, uint64_t rows, uint32_t n_cols, int rowlen_kind,
+                      uint32_t a, uint32_t b, int value_kind, uint32_t chunks, bsm_mcsr** out);
+/* rows, cols, nnz, pieces P, padded piece rows; bounds (P+1 entries, may be NULL) */
+int bsm_mcsr_info(const bsm_mcsr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz, uint32_t* pieces,
+                  uint64_t* piece_rows, uint64_t* bounds);
+/* Build the per-piece SpMM schedules (schedule: 0 = the library's choice as
+ * in bsm_csr_mul_dense, 1 = the row-block x column-panel copy whenever
+ * possible, 2 = never the copy) and the gathered-Y and output buffers for k
+ * right-hand columns. Synchronous; bsm_mcsr_mul_dense calls it when needed.
+ * *plan_ms (may be NULL) receives per-phase host times of the slowest local
+ * device: {total, tiled count pass, tiled scan, tiled allocation, tiled
+ * write pass, panel plans, buffers}. */
+int bsm_mcsr_prepare(bsm_mcsr* m, uint64_t k, int schedule, double* plan_ms);
+/* The schedule prepare built, over this process's pieces: how many use the
+ * row-block x column-panel copy, its bytes in total, and the panel width in
+ * columns (the copy's, else the column-panel plan's; 0 = one pass). */
+int bsm_mcsr_plan_info(const bsm_mcsr* m, int* tiled_pieces, int* local_pieces, uint64_t* copy_bytes,
+                       uint64_t* panel_cols);
+/* Csr::mul_dense on all GPUs: X (k host columns of x_rows, Dense::get_col)
+ * uploaded to every local device, the step below, then the output Csr (dims
+ * rows x k, zero results dropped, sparse.rs:229) as a new handle on the
+ * first local device. x_rows != cols -> BSM_ERR_DIMENSIONS. */
+int bsm_mcsr_mul_dense(bsm_mcsr* m, uint64_t k, uint64_t x_rows, const void* const* x_cols, bsm_csr** out);
+/* Device level, asynchronous: x_dev[i] = X on local device i (ROW-major
+ * cols x k). Enqueues the rounds' SpMMs, the all-gathers of Y and of the
+ * per-row nonzero counts, and the compaction; bsm_mcsr_sync waits. */
+int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev);
+int bsm_mcsr_sync(bsm_mcsr* m);
+/* HIP-event times of the steps since the last reset on local device i, per
+ * step {SpMM rounds (first SpMM start .. last SpMM end on the compute
+ * stream), all-gather tail (last SpMM end .. last all-gather end), compaction,
+ * whole step}: *n steps, the first min(max, *n) written to ms[4*s ..]. */
+int bsm_mcsr_step_times(bsm_mcsr* m, int local, int max, int* n, double* ms);
+void bsm_mcsr_reset_times(bsm_mcsr* m);
+/* The assembled dense Y (rows x k ROW-major, global row order) and per-row
+ * nonzero counts on local device i, copied into caller device buffers
+ * (either may be NULL); synchronous. */
+int bsm_mcsr_copy_y(const bsm_mcsr* m, int local, void* y, int32_t* row_nnz);
+/* The last step's output Csr as a new handle on the first local device. */
+int bsm_mcsr_output(const bsm_mcsr* m, bsm_csr** out);
+void bsm_mcsr_free(bsm_mcsr* m);
 
 #ifdef __cplusplus
 }

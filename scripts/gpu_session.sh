@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-2 GPU session: scripts/gpu_r02.sh TAG STEP...
-# STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>
-#       | pmc:<config>:<COUNTER> | c5
+# GPU session: scripts/gpu_session.sh TAG STEP...
+# STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>[:extra]
+#       | pmc:<config>:<COUNTER>[:extra] | c5 | gather | torchrun:<config>[:extra]
 # Every step runs under its own time limit; the session stops at the first
 # failing step (no retries).
 set -u
@@ -29,13 +29,17 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench:*) IFS=: read -r _ cfg extra <<< "$step"
              run bench_$cfg 600 python bench.py --config $cfg $extra || exit $? ;;
-    prof:*) cfg=${step#prof:}
+    prof:*) IFS=: read -r _ cfg extra <<< "$step"
             run prof_$cfg 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${cfg}_$TAG -o run \
-                --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e || exit $? ;;
-    pmc:*) IFS=: read -r _ cfg ctr <<< "$step"
+                --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e $extra || exit $? ;;
+    pmc:*) IFS=: read -r _ cfg ctr extra <<< "$step"
            run pmc_${cfg}_${ctr} 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${cfg}_${ctr}_$TAG -o run \
                --output-format csv -- python bench.py --config $cfg --steps 2 --warmup 0 --no-cpu-baseline \
-               --no-e2e || exit $? ;;
+               --no-e2e $extra || exit $? ;;
+    gather) run gather 300 bash scripts/perf/gather_ceiling.sh || exit $? ;;
+    torchrun:*) IFS=: read -r _ cfg extra <<< "$step"
+                run torchrun_$cfg 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --config $cfg $extra || exit $? ;;
     c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

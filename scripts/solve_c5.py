@@ -91,6 +91,7 @@ def main():
     es = np.dtype(dt).itemsize
     flops = float(n) * g * g  # sum over rows of b^2 / 2 multiply-add pairs, x 2
     band_bytes = float(es) * n * (g + 1)
+    _lib.stage_timing(True)
     for order in args.orders.split(","):
         solve(A, B, order=order)  # warm-up (first call uploads A and builds nothing else)
         walls, stages = [], []
