@@ -192,10 +192,14 @@ __device__ __forceinline__ double bv(const Idx& c) {
     return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(c.vi), 0x150 + I, 0xf, 0xf, false),
                             __builtin_amdgcn_update_dpp(0, __double2loint(c.vi), 0x150 + I, 0xf, 0xf, false));
 }
-template <int... I>
+// PROBE (measurement only, wrong results): every gather reads X row
+// (col & xmask), e.g. xmask = 0 leaves the index/value stream alone on the
+// memory side (the PMC calibration of its 4-B / 8-B per-lane reads)
+template <bool PROBE, int... I>
 __device__ __forceinline__ void gather(double2 (&x)[16], const Idx& c, const double2* __restrict__ X, int q,
-                                       std::integer_sequence<int, I...>) {
-    ((x[I] = X[(int64_t)(bm<I>(c) >> 8) * 16 + q]), ...);
+                                       uint32_t xmask, std::integer_sequence<int, I...>) {
+    if (PROBE) ((x[I] = X[(int64_t)((bm<I>(c) >> 8) & xmask) * 16 + q]), ...);
+    else ((x[I] = X[(int64_t)(bm<I>(c) >> 8) * 16 + q]), ...);
 }
 template <int I>
 __device__ __forceinline__ double2* yaddr(const Idx& c, double2* yw, int q) {
@@ -245,10 +249,11 @@ __device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int l
     return false;  // not all resident: stop pacing
 }
 
+template <bool PROBE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const uint32_t* __restrict__ meta, const double* __restrict__ val, const double2* __restrict__ X,
-    double2* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar) {
+    double2* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask) {
     extern __shared__ double2 ylds[];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = threadIdx.x / WAVE;
@@ -274,13 +279,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             double2 XS[3][16];
 #pragma unroll
             for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
-            gather(XS[0], M[0], X, q, SEQ);
-            gather(XS[1], M[1], X, q, SEQ);
+            gather<PROBE>(XS[0], M[0], X, q, xmask, SEQ);
+            gather<PROBE>(XS[1], M[1], X, q, xmask, SEQ);
             for (int64_t i = c0; i < c1; i += PHASES) {
 #pragma unroll
                 for (int k = 0; k < PHASES; ++k) {
                     load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
-                    gather(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, SEQ);
+                    gather<PROBE>(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
                     sum_chunk(XS[k % 3], M[k], yw, q, SEQ);
                     __builtin_amdgcn_sched_barrier(0);
@@ -564,9 +569,12 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
                                               neg_init, xmask);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
-        spmm_tiled_k32<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
-                                                        static_cast<const double2*>(x), static_cast<double2*>(y),
-                                                        row_nnz, bar);
+        // BSM_TILED_PROBE_MASK=<mask> (measurement only, wrong results): see gather()
+        static const uint32_t xmask = env_u32("BSM_TILED_PROBE_MASK", 0xffffffffu);
+        auto kern = xmask == 0xffffffffu ? spmm_tiled_k32<false> : spmm_tiled_k32<true>;
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
+                                              static_cast<const double2*>(x), static_cast<double2*>(y), row_nnz, bar,
+                                              xmask);
     }
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;

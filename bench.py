@@ -60,7 +60,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # profiles/r03_gather_ceiling.log ("static 2 MiB table, LDS update" line).
 # It is the peak of roofline_gather: the C4 gathers (2.56 TB) cannot be served
 # faster than the L2 serves them.
-L2_GATHER_PEAK_GBS = 17_600.0
+L2_GATHER_PEAK_GBS = 17_030.0  # 17.03 TB/s: "mode 2 ... 8191" line (0.987 ms for 6.57e7 entries)
 L2_GATHER_PEAK_SRC = "profiles/r03_gather_ceiling.log"
 ROWLEN_CONST, ROWLEN_BINOMIAL = 0, 2  # bsm_synth.h row-length families
 SEED_A, SEED_X = 1000, 1001

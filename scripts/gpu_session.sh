@@ -2,6 +2,7 @@
 # GPU session: scripts/gpu_session.sh TAG STEP...
 # STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>[:extra]
 #       | pmc:<config>:<COUNTER>[:extra] | c5 | gather | torchrun:<config>[:extra]
+#       | py:<script args> | env:VAR=VALUE (for the later steps) | unenv:VAR
 # Every step runs under its own time limit; the session stops at the first
 # failing step (no retries).
 set -u
@@ -20,6 +21,7 @@ run() {
   tail -3 "$OUT/${name}_$TAG.log" | cut -c1-600 | tee -a $OUT/session_$TAG.log
   return $rc
 }
+n=0
 for step in "$@"; do
   case $step in
     tests) run gpu_tests 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
@@ -41,6 +43,9 @@ for step in "$@"; do
                 run torchrun_$cfg 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --config $cfg $extra || exit $? ;;
     c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
+    py:*) n=$((n + 1)); run py${n} 600 python ${step#py:} || exit $? ;;
+    env:*) export "${step#env:}"; echo "=== export ${step#env:}" | tee -a $OUT/session_$TAG.log ;;
+    unenv:*) unset "${step#unenv:}" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
