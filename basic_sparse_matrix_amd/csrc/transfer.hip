@@ -5,13 +5,19 @@
 // (dense.rs:8), and takes back a fresh Csr with usize indices. Moving those
 // through the driver's own pageable path, with the 8 B <-> 4 B index
 // conversion as a scalar host loop, cost 7x the device time at C3 (round 2:
-// 102 ms against 13.8 ms). Here every large transfer is a pipeline over two
-// pinned chunk buffers: a few host threads copy chunk i+1 into one while the
-// DMA engine moves chunk i out of the other, and index conversions run on the
-// device (a narrowing / widening kernel per chunk), so the host only copies.
+// 102 ms against 13.8 ms). Here index conversions run on the device (a
+// narrowing / widening kernel per chunk); uploads go by the runtime's pageable
+// DMA at the link rate, downloads through two pinned chunk buffers (host
+// threads copy chunk i out while the DMA fills chunk i+1), with the caller's
+// fresh result pages faulted in ahead by host threads, as huge pages.
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
+
+#include <sys/mman.h>
 #include <vector>
 
 #include "bsm_internal.hpp"
@@ -79,6 +85,25 @@ Stage& stage() {
     return st;
 }
 
+// Host -> device: the runtime's own pageable copies (BSM_XFER_H2D=direct,
+// the default) reach the link rate (56 GB/s, profiles/r03_b_marshal.log);
+// BSM_XFER_H2D=staged selects the pinned two-buffer pipeline. Device ->
+// host: staged by default. A direct pageable DMA into the caller's fresh
+// result arrays is as fast, but the runtime then holds those pages, and the
+// caller's later free of the 520 MB of a C3 result took 25-30 ms
+// (profiles/r03_g_xfer_dbg.log) against ~0 after a staged copy.
+bool direct_mode(bool h2d) {
+    static const bool d_h2d = [] {
+        const char* e = getenv("BSM_XFER_H2D");
+        return !(e && std::strcmp(e, "staged") == 0);
+    }();
+    static const bool d_d2h = [] {
+        const char* e = getenv("BSM_XFER_D2H");
+        return e && std::strcmp(e, "direct") == 0;
+    }();
+    return h2d ? d_h2d : d_d2h;
+}
+
 size_t chunk_bytes() {
     static const size_t c = std::max<size_t>(env_size("BSM_STAGE_CHUNK", STAGE_CHUNK), 1 << 16) & ~size_t(255);
     return c;
@@ -110,6 +135,57 @@ __global__ __launch_bounds__(256) void widen_i32_u64(const int32_t* __restrict__
 
 inline unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
+// Fault in [p, p + bytes) chunk by chunk from BSM_TOUCH_THREADS threads
+// (default 8): a write per 4 KiB page; wait(i) returns once chunk i is in.
+class Prefault {
+public:
+    Prefault(char* p, size_t bytes, size_t chunk) : p_(p), bytes_(bytes), chunk_(chunk) {
+        static const int threads = (int)std::clamp<size_t>(env_size("BSM_TOUCH_THREADS", 8), 0, 32);
+        n_ = (bytes + chunk - 1) / chunk;
+        if (threads == 0 || bytes < (8ull << 20)) {
+            n_ = 0;  // small: the DMA takes its own faults
+            return;
+        }
+        // transparent huge pages for the 2 MiB-aligned interior (advice only;
+        // the box runs THP in madvise mode): 520 MB faults in 3.8 ms on 8
+        // threads with it, 30-40 ms without (profiles/r03_e_first_touch.log)
+        const uintptr_t a0 = ((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+        const uintptr_t a1 = ((uintptr_t)p + bytes) & ~(uintptr_t)((2u << 20) - 1);
+        if (a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
+        ready_.reset(new std::atomic<int>[n_]);
+        for (size_t i = 0; i < n_; ++i) ready_[i].store(0, std::memory_order_relaxed);
+        for (int t = 0; t < threads; ++t)
+            th_.emplace_back([this] {
+                for (;;) {
+                    const size_t i = next_.fetch_add(1, std::memory_order_relaxed);
+                    if (i >= n_ || stop_.load(std::memory_order_relaxed)) return;
+                    char* q = p_ + i * chunk_;
+                    const size_t len = std::min(chunk_, bytes_ - i * chunk_);
+                    for (size_t o = 0; o < len; o += 4096) reinterpret_cast<volatile char*>(q)[o] = 0;
+                    ready_[i].store(1, std::memory_order_release);
+                }
+            });
+    }
+    void wait(size_t i) {
+        if (i >= n_) return;
+        while (!ready_[i].load(std::memory_order_acquire)) std::this_thread::yield();
+    }
+    void finish() {
+        stop_.store(true, std::memory_order_relaxed);
+        for (auto& t : th_) t.join();
+        th_.clear();
+    }
+    ~Prefault() { finish(); }
+
+private:
+    char* p_;
+    size_t bytes_, chunk_, n_ = 0;
+    std::unique_ptr<std::atomic<int>[]> ready_;
+    std::atomic<size_t> next_{0};
+    std::atomic<bool> stop_{false};
+    std::vector<std::thread> th_;
+};
+
 }  // namespace
 
 // Host -> device, synchronous (src may be released when it returns). The
@@ -121,6 +197,17 @@ template <typename Post>
 static int h2d_pipeline(void* dst, const void* src, size_t bytes, hipStream_t s, void* dev_stage, Post&& post) {
     if (bytes == 0) return BSM_OK;
     const size_t C = chunk_bytes();
+    if (direct_mode(true)) {  // pageable DMA per chunk, the device work behind it
+        const size_t n = (bytes + C - 1) / C;
+        for (size_t i = 0; i < n; ++i) {
+            const size_t off = i * C, len = std::min(C, bytes - off);
+            void* d = dev_stage ? static_cast<char*>(dev_stage) + (i & 1) * C : static_cast<char*>(dst) + off;
+            BSM_HIP_TRY(hipMemcpyAsync(d, static_cast<const char*>(src) + off, len, hipMemcpyHostToDevice, s));
+            if (dev_stage) BSM_TRY(post(off, len, d));
+        }
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        return BSM_OK;
+    }
     Stage& st = stage();
     BSM_TRY(st.get(std::min(C, bytes)));
     const size_t n = (bytes + C - 1) / C;
@@ -149,12 +236,53 @@ template <typename Pre>
 static int d2h_pipeline(void* dst, const void* src, size_t bytes, hipStream_t s, void* dev_stage, Pre&& pre) {
     if (bytes == 0) return BSM_OK;
     const size_t C = chunk_bytes();
+    if (direct_mode(false)) {
+        // The caller's result arrays are fresh (Rust Vec::with_capacity, numpy
+        // empty): their first touch is a zero-fill page fault per 4 KiB, 43 ms
+        // for C3's 520 MB against 10 ms for the DMA itself
+        // (profiles/r03_c_marshal.log). Host threads fault the chunks in (huge
+        // pages where the mapping allows), in order, ahead of the DMA.
+        const size_t n = (bytes + C - 1) / C;
+        static const bool dbg = getenv("BSM_XFER_DEBUG") != nullptr;
+        const auto t0 = host_now();
+        Prefault pf(static_cast<char*>(dst), bytes, C);
+        double t_wait = 0, t_dma = 0;
+        int rc = BSM_OK;
+        for (size_t i = 0; i < n && rc == BSM_OK; ++i) {
+            const size_t off = i * C, len = std::min(C, bytes - off);
+            const void* from = static_cast<const char*>(src) + off;
+            if (dev_stage) {
+                void* d = static_cast<char*>(dev_stage) + (i & 1) * C;
+                rc = pre(off, len, d);
+                from = d;
+            }
+            auto tw = host_now();
+            pf.wait(i);
+            t_wait += ms_since(tw);
+            tw = host_now();
+            if (rc == BSM_OK && hipMemcpyAsync(static_cast<char*>(dst) + off, from, len, hipMemcpyDeviceToHost, s) !=
+                                    hipSuccess) {
+                set_error("d2h: %s", hipGetErrorString(hipGetLastError()));
+                rc = BSM_ERR_HIP;
+            }
+            t_dma += ms_since(tw);
+        }
+        pf.finish();
+        BSM_TRY(rc);
+        BSM_HIP_TRY(hipStreamSynchronize(s));
+        if (dbg)
+            fprintf(stderr, "[bsm xfer] d2h %zu B in %zu chunks: %.2f ms (prefault waits %.2f, DMA calls %.2f)\n",
+                    bytes, n, ms_since(t0), t_wait, t_dma);
+        return BSM_OK;
+    }
     Stage& st = stage();
     BSM_TRY(st.get(std::min(C, bytes)));
     const size_t n = (bytes + C - 1) / C;
+    Prefault pf(static_cast<char*>(dst), bytes, C);  // fresh result pages, faulted in ahead of the copies
     auto drain = [&](size_t i) -> int {  // chunk i's DMA done -> copy out of its pinned buffer
         const size_t off = i * C, len = std::min(C, bytes - off);
         BSM_HIP_TRY(hipEventSynchronize(st.ev[i & 1]));
+        pf.wait(i);
         par_memcpy(static_cast<char*>(dst) + off, st.buf[i & 1], len);
         return BSM_OK;
     };

@@ -134,7 +134,55 @@ def end_to_end(cfg_name, m, x, dev, iters=3):
             ts.append(time.perf_counter() - t0)
         out["public_api_ms"] = round(float(np.median(ts)) * 1e3, 4)
         out["public_api_calls"] = len(ts)
+        # the same call split: time inside the C-ABI (bsm_csr_mul_dense: X
+        # upload + SpMM + compaction; bsm_csr_download into fresh usize / f64
+        # arrays) and the caller freeing the previous result (its host pages)
+        import ctypes
+
+        lib = _lib_load()
+        dev_a = a._device()
+        ptrs = _ptr_array(x_cols)
+        lib_ts, free_ts, prev = [], [], None
+        for _ in range(len(ts)):
+            t0 = time.perf_counter()
+            h = ctypes.c_void_p()
+            _check(lib.bsm_csr_mul_dense(dev_a.handle, k, n_cols, ptrs, ctypes.byref(h)))
+            dc = _DeviceCsr(h.value)
+            res = dc.download()
+            t1 = time.perf_counter()
+            prev, old = res, prev
+            del old
+            t2 = time.perf_counter()
+            lib_ts.append(t1 - t0)
+            free_ts.append(t2 - t1)
+            del dc
+        out["public_api_split_ms"] = {"in_library": round(float(np.median(lib_ts)) * 1e3, 4),
+                                      "caller_frees_previous_result": round(float(np.median(free_ts)) * 1e3, 4)}
     return out
+
+
+def _lib_load():
+    from basic_sparse_matrix_amd import _lib
+
+    return _lib.load()
+
+
+def _ptr_array(arrs):
+    from basic_sparse_matrix_amd import _lib
+
+    return _lib.ptr_array(arrs)
+
+
+def _check(rc):
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.check(rc)
+
+
+def _DeviceCsr(h):
+    from basic_sparse_matrix_amd import _lib
+
+    return _lib.DeviceCsr(h)
 
 
 def log(msg):

@@ -22,10 +22,13 @@
 #ifndef BSM_HPP
 #define BSM_HPP
 
+#include <algorithm>
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <span>
 #include <stdexcept>
@@ -164,7 +167,62 @@ inline std::optional<MatErr> status(int rc) {
 inline void check(int rc) {
     if (auto e = status(rc)) throw Panic(std::string("unexpected ") + to_string(*e) + ": " + bsm_last_error());
 }
+
+// The process-wide multi-GPU context of mul_dense (the Rust binding's
+// OnceLock): gpus = 0 is the single-GPU path.
+struct MultiState {
+    std::mutex mu;
+    bool init = false;
+    int gpus = 0;
+    uint32_t chunks = 1;
+    std::shared_ptr<bsm_multi> ctx;
+};
+inline MultiState& multi_state() {
+    static MultiState st;
+    return st;
+}
+inline void multi_env(MultiState& st) {  // BSM_N_GPUS / BSM_CHUNKS, read once
+    if (st.init) return;
+    st.init = true;
+    if (const char* e = std::getenv("BSM_N_GPUS")) st.gpus = std::atoi(e);
+    if (const char* e = std::getenv("BSM_CHUNKS")) st.chunks = (uint32_t)std::max(1, std::atoi(e));
+}
+/// The context (created on first use) and its chunks, or nullptr for one GPU.
+inline std::shared_ptr<bsm_multi> multi_context(uint32_t* chunks) {
+    MultiState& st = multi_state();
+    std::lock_guard<std::mutex> lk(st.mu);
+    multi_env(st);
+    if (st.gpus <= 0) return nullptr;
+    if (!st.ctx) {
+        bsm_multi* c = nullptr;
+        if (auto e = status(bsm_multi_create(st.gpus, nullptr, &c)))
+            throw Panic(std::string("bsm_multi_create: ") + to_string(*e));
+        st.ctx = std::shared_ptr<bsm_multi>(c, [](bsm_multi* p) { bsm_multi_destroy(p); });
+    }
+    *chunks = st.chunks;
+    return st.ctx;
+}
+/// A matrix partitioned over a context; keeps the context alive.
+struct MultiCopy {
+    std::shared_ptr<bsm_multi> ctx;
+    uint32_t chunks = 1;
+    std::shared_ptr<bsm_mcsr> m;
+};
 }  // namespace detail
+
+/// Route every Csr::mul_dense of this process over n GPUs (row blocks of the
+/// CSR on each, RCCL all-gather of the dense result; bit-identical to one
+/// GPU); n = 0 returns to the single-GPU path, n = 1 runs the RCCL path on one
+/// GPU. chunks: rounds per GPU (an all-gather per round overlaps the next
+/// round's SpMM). Env BSM_N_GPUS / BSM_CHUNKS give the default.
+inline void set_gpus(int n, uint32_t chunks = 1) {
+    detail::MultiState& st = detail::multi_state();
+    std::lock_guard<std::mutex> lk(st.mu);
+    st.init = true;
+    if (n != st.gpus) st.ctx.reset();
+    st.gpus = n > 0 ? n : 0;
+    st.chunks = chunks ? chunks : 1;
+}
 
 // --------------------------------------------------------------- dense.rs
 /// dense.rs:4-62: column-major, one vector per column.
@@ -481,6 +539,19 @@ public:
     /// reference's row loop sees them; panics where it panics.
     detail::Handle device() const {
         if (dev_) return dev_;
+        auto [rp, used] = device_row_ptr();
+        bsm_csr* h = nullptr;
+        static_assert(sizeof(size_t) == sizeof(uint64_t), "usize is 8 bytes (x86_64)");
+        detail::check(bsm_csr_upload(detail::dtype_of<T>::value, dims_.rows, dims_.cols, used, rp.data(),
+                                     reinterpret_cast<const uint64_t*>(col_index_.data()), v_.data(), &h));
+        detail::Handle hd(h, detail::HandleFree{});
+        if (is_finalised_) dev_ = hd;
+        return hd;
+    }
+
+    /// row_ptr (rows + 1) as the reference's row loop sees the matrix, and
+    /// the entries it uses; panics where it panics.
+    std::pair<std::vector<uint64_t>, size_t> device_row_ptr() const {
         const size_t rows = dims_.rows, nnz = v_.size();
         std::vector<uint64_t> rp(rows + 1);
         if (row_index_.size() >= rows + 1) {
@@ -501,13 +572,7 @@ public:
             if (col_index_[i] >= dims_.cols)
                 throw Panic("index out of bounds: column " + std::to_string(col_index_[i]) + " >= " +
                             std::to_string(dims_.cols));
-        std::vector<uint64_t> ci(col_index_.begin(), col_index_.begin() + used);
-        bsm_csr* h = nullptr;
-        detail::check(bsm_csr_upload(detail::dtype_of<T>::value, rows, dims_.cols, used, rp.data(), ci.data(),
-                                     v_.data(), &h));
-        detail::Handle hd(h, detail::HandleFree{});
-        if (is_finalised_) dev_ = hd;
-        return hd;
+        return {std::move(rp), used};
     }
 
 private:
@@ -518,6 +583,7 @@ private:
     /// maximum; an entry for an earlier row is appended to the current last row.
     void insert_unchecked(T value, size_t row, size_t col) {
         dev_.reset();
+        mdev_ = {};
         v_.push_back(value);
         col_index_.push_back(col);
         if (row + 1 > row_index_.size()) {
@@ -537,10 +603,31 @@ private:
     }
 
     Result<Csr> mul_cols(const std::vector<const void*>& cols, size_t x_rows) const {
+        uint32_t chunks = 1;
+        if (auto ctx = detail::multi_context(&chunks)) {  // row blocks on every GPU + RCCL all-gather
+            auto m = multi_device(ctx, chunks);
+            bsm_csr* out = nullptr;
+            if (auto e = detail::status(bsm_mcsr_mul_dense(m.get(), cols.size(), x_rows, cols.data(), &out)))
+                return *e;
+            return from_device(detail::Handle(out, detail::HandleFree{}));
+        }
         auto h = device();
         bsm_csr* out = nullptr;
         if (auto e = detail::status(bsm_csr_mul_dense(h.get(), cols.size(), x_rows, cols.data(), &out))) return *e;
         return from_device(detail::Handle(out, detail::HandleFree{}));
+    }
+
+    /// The matrix partitioned over the multi-GPU context, cached like the
+    /// single-GPU copy for a finalised matrix.
+    std::shared_ptr<bsm_mcsr> multi_device(const std::shared_ptr<bsm_multi>& ctx, uint32_t chunks) const {
+        if (mdev_.m && mdev_.ctx == ctx && mdev_.chunks == chunks) return mdev_.m;
+        auto [rp, used] = device_row_ptr();
+        bsm_mcsr* m = nullptr;
+        detail::check(bsm_mcsr_upload(ctx.get(), detail::dtype_of<T>::value, dims_.rows, dims_.cols, used, rp.data(),
+                                      reinterpret_cast<const uint64_t*>(col_index_.data()), v_.data(), chunks, &m));
+        std::shared_ptr<bsm_mcsr> sp(m, [](bsm_mcsr* p) { bsm_mcsr_free(p); });
+        if (is_finalised_) mdev_ = {ctx, chunks, sp};
+        return sp;
     }
 
     Result<Csr> binary(const Csr& rhs, int (*fn)(const bsm_csr*, const bsm_csr*, bsm_csr**)) const {
@@ -556,13 +643,14 @@ public:
         uint64_t rows = 0, cols = 0, nnz = 0;
         int dt = 0;
         detail::check(bsm_csr_shape(h.get(), &rows, &cols, &nnz, &dt));
-        std::vector<uint64_t> rp(rows + 1), ci(nnz);
         Csr m;
         m.dims_ = {rows, cols};
         m.v_.resize(nnz);
-        detail::check(bsm_csr_download(h.get(), rp.data(), ci.data(), m.v_.data()));
-        m.row_index_.assign(rp.begin(), rp.end());
-        m.col_index_.assign(ci.begin(), ci.end());
+        m.row_index_.resize(rows + 1);
+        m.col_index_.resize(nnz);
+        // usize Vecs filled in place (the library widens int32 columns on the device)
+        detail::check(bsm_csr_download(h.get(), reinterpret_cast<uint64_t*>(m.row_index_.data()),
+                                       reinterpret_cast<uint64_t*>(m.col_index_.data()), m.v_.data()));
         m.is_finalised_ = true;  // what finalise() leaves (sparse.rs:206-219)
         m.dev_ = std::move(h);
         return m;
@@ -576,6 +664,7 @@ private:
     bool is_finalised_ = false;
     size_t iter_v_index_ = 0, iter_row_index_ = 0;
     mutable detail::Handle dev_;
+    mutable detail::MultiCopy mdev_;
 };
 
 template <class T>

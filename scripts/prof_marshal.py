@@ -36,7 +36,8 @@ def med(fn, n=10):
 
 
 def emit(name, ms, **kw):
-    print(json.dumps({"what": name, "ms": ms, "copy_threads": os.environ.get("BSM_COPY_THREADS", "4"),
+    print(json.dumps({"what": name, "ms": ms, "xfer_d2h": os.environ.get("BSM_XFER_D2H", "staged"),
+                      "copy_threads": os.environ.get("BSM_COPY_THREADS", "4"),
                       "stage_chunk": os.environ.get("BSM_STAGE_CHUNK", str(16 << 20)), **kw}), flush=True)
 
 
@@ -93,6 +94,16 @@ def main():
     emit("mul_dense_handle", med(mul))
     o = outs[-1]
     emit("download", med(lambda: o.download()), out_nnz=o.nnz)
+    # the same into destination arrays whose pages are already touched: the
+    # difference is the first-touch page-fault cost of fresh host arrays
+    rp_t = np.ones(o.rows + 1, np.uint64)
+    ci_t = np.ones(o.nnz, np.uint64)
+    v_t = np.ones(o.nnz, np.float64)
+    emit("download_touched", med(lambda: _lib.check(lib.bsm_csr_download(o.handle, _lib.ptr(rp_t), _lib.ptr(ci_t),
+                                                                         _lib.ptr(v_t)))))
+    fresh = lambda: (np.empty(o.rows + 1, np.uint64).fill(1), np.empty(o.nnz, np.uint64).fill(1),  # noqa: E731
+                     np.empty(o.nnz, np.float64).fill(1))
+    emit("host_first_touch_520MB", med(fresh))
     emit("public_api", med(lambda: a.mul_dense(xd), 20))
 
 

@@ -299,6 +299,60 @@ GPU_TEST(mul_dense_u32_wrapping_vs_oracle) {  // bench type, overflow-checks=fal
     CHECK((y.row_index() == std::vector<size_t>(er.begin(), er.end())));
 }
 
+// north_star's multi-GPU path through the C-ABI (bsm_multi_*, bsm_mcsr_*):
+// RCCL on the visible GPU(s), bit-identical to the oracle and to one GPU
+GPU_TEST(mul_dense_multi_gpu_rccl_vs_oracle) {
+    const uint64_t rows = 2500, cols = 900, k = 32;
+    std::vector<uint64_t> rp(rows + 1);
+    orc_gen_row_ptr(21, rows, cols, /*UNIFORM*/ 1, 0, 60, rp.data());
+    const uint64_t nnz = rp[rows];
+    std::vector<uint64_t> ci(nnz);
+    std::vector<double> v(nnz);
+    orc_gen_entries(21, 0, rows, cols, rp.data(), 0, ci.data(), v.data());
+    std::vector<double> x(cols * k);
+    orc_gen_x_colmajor(22, cols, k, 0, x.data());
+    std::vector<uint64_t> er(rows + 1), ec(rows * k);
+    std::vector<double> ev(rows * k);
+    uint64_t enz = 0;
+    CHECK(orc_mul_dense_f64(rows, cols, rp.data(), rows + 1, ci.data(), v.data(), nnz, k, cols, x.data(), cols,
+                            er.data(), ec.data(), ev.data(), &enz) == ORC_OK);
+    ev.resize(enz);
+    ec.resize(enz);
+    // the raw C-ABI, as a Rust binding calls it
+    bsm_multi* ctx = nullptr;
+    CHECK(bsm_multi_create(1, nullptr, &ctx) == BSM_OK);
+    bsm_mcsr* m = nullptr;
+    CHECK(bsm_mcsr_upload(ctx, BSM_F64, rows, cols, nnz, rp.data(), ci.data(), v.data(), 3, &m) == BSM_OK);
+    std::vector<const void*> xc(k);
+    for (uint64_t j = 0; j < k; ++j) xc[j] = x.data() + j * cols;
+    bsm_csr* out = nullptr;
+    CHECK(bsm_mcsr_mul_dense(m, k, cols, xc.data(), &out) == BSM_OK);
+    uint64_t orows = 0, ocols = 0, onnz = 0;
+    int dt = -1;
+    CHECK(bsm_csr_shape(out, &orows, &ocols, &onnz, &dt) == BSM_OK);
+    CHECK(orows == rows && ocols == k && onnz == enz && dt == BSM_F64);
+    std::vector<uint64_t> gr(rows + 1), gc(onnz);
+    std::vector<double> gv(onnz);
+    CHECK(bsm_csr_download(out, gr.data(), gc.data(), gv.data()) == BSM_OK);
+    CHECK(gr == er && gc == ec && same_bits(gv, ev));
+    CHECK(bsm_mcsr_mul_dense(m, k, cols - 1, xc.data(), &out) == BSM_ERR_DIMENSIONS);
+    bsm_csr_free(out);
+    bsm_mcsr_free(m);
+    bsm_multi_destroy(ctx);
+    // the mirror's mul_dense routed over the context (bsm::set_gpus)
+    auto a = Csr<double>::from_csr_arrays({rows, cols}, {rp.begin(), rp.end()}, {ci.begin(), ci.end()}, v);
+    std::vector<std::vector<double>> xcols(k);
+    for (uint64_t j = 0; j < k; ++j) xcols[j].assign(x.begin() + j * cols, x.begin() + (j + 1) * cols);
+    bsm::set_gpus(1, 4);
+    auto y = a.mul_dense(Dense<double>::from_data(xcols)).unwrap();
+    auto y2 = a.mul_dense(Dense<double>::from_data(xcols)).unwrap();  // the cached partition
+    bsm::set_gpus(0);
+    CHECK((y.row_index() == std::vector<size_t>(er.begin(), er.end())));
+    CHECK((y.col_index() == std::vector<size_t>(ec.begin(), ec.end())));
+    CHECK(same_bits(y.v(), ev) && same_bits(y2.v(), ev));
+    CHECK(a.mul_dense(Dense<double>::new_default_with_dims(k, cols - 1)) == MatErr::IncorrectDimensions);
+}
+
 GPU_TEST(solve_poisson_f64_vs_band_oracle) {
     const uint64_t g = 24, n = g * g;
     std::vector<uint64_t> rp(n + 1), ci(5 * n);
