@@ -57,7 +57,15 @@ bool stage_on() {
 // Every public entry point that marks stages starts its own list.
 void stage_reset(hipStream_t s) {
     stage_clear();
-    if (stage_on()) stage_mark("start", s);
+    if (!stage_on()) return;
+    Stage st;
+    st.name = "start";
+    if (hipEventCreate(&st.ev) != hipSuccess) return;
+    if (hipEventRecord(st.ev, s) != hipSuccess) {
+        (void)hipEventDestroy(st.ev);
+        return;
+    }
+    g_stages.push_back(st);
 }
 void stage_mark(const char* name, hipStream_t s) {
     if (!stage_on() || g_stages.empty() || g_stages.size() >= 64) return;

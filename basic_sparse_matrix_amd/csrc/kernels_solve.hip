@@ -2424,7 +2424,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                                 T* __restrict__ Dinv, int* __restrict__ flags,
                                                 int* __restrict__ ticket, int* __restrict__ status,
                                                 unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
-                                                int panels) {
+                                                int panels, T* __restrict__ pend, int* __restrict__ pendf) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
     __shared__ T rd[64];
@@ -2488,28 +2488,135 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             X[e >> 6][e & 63] = v[u];
         }
     };
+    // this thread's 16 elements of a 64 x 64 tile, in the f64 MFMA accumulator
+    // layout: X[cb][q] = element (row rb + 4q, column 16cb + cm)
+    const int rb = 16 * w + (lane >> 4), cm = lane & 15;
+    lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
+    lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
+    const bool chain = pend != nullptr;
     for (;;) {
         if (tid == 0) tk = atomicAdd(ticket, 1);
         __syncthreads();
-        const int64_t t = tk;
-        if (dbg && tid == 0) __hip_atomic_fetch_max(&dbg[0], (unsigned long long)t, __ATOMIC_RELAXED,
+        const int64_t t0 = tk;
+        if (dbg && tid == 0) __hip_atomic_fetch_max(&dbg[0], (unsigned long long)t0, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        if (chain && t0 == 0) {
+            // THE CHAIN (ticket 0, one workgroup for the whole factor): for each
+            // block column K, the sub-diagonal tile L_{K,K-1} = S_{K,K-1}
+            // Linv_{K-1}^T with Linv_{K-1} still in LDS from the previous
+            // factor, the diagonal update by it, the factor of the diagonal
+            // tile, Dinv[K] and L_{K,K} out. S_{K,K} and S_{K,K-1} with every
+            // block column J <= K-2 applied come from the pending tile K
+            // (ticketed below, publishing to pend), which has the chain's whole
+            // factor of K-1 to finish its last update. Against one workgroup per
+            // diagonal tile this removes the hand-off of Dinv between
+            // workgroups (flag wait + staging of Linv) on the chain.
+            T acc[4][4], acc2[4][4];
+            long long ck[6] = {0, 0, 0, 0, 0, 0};
+            auto load_pend = [&](int64_t Kp) {
+                const long long cw = tdbg ? clock64() : 0;
+                wait_flag(&pendf[Kp]);
+                if (tdbg && tid == 0)
+                    __hip_atomic_fetch_add(&tdbg[0], (unsigned long long)(clock64() - cw), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                const T* pp = pend + Kp * 8192 + tid;  // element (cb, q) of thread tid at (4 cb + q) * 256 + tid
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc[cb][q] = ld_sc1(pp + (4 * cb + q) * 256);
+                        acc2[cb][q] = ld_sc1(pp + 4096 + (4 * cb + q) * 256);
+                    }
+            };
+            load_pend(0);
+            for (int64_t K = 0; K < nb64; ++K) {
+                if (tdbg) ck[0] = clock64();
+                if (K > 0) {
+                    // L_{K,K-1} = S_{K,K-1} Linv_{K-1}^T; QT holds Linv_{K-1}^T
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
+                    __syncthreads();
+                    T o[4][4] = {};
+                    mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int r = rb + 4 * q, c = 16 * cb + cm;
+                            if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
+                        }
+                    __syncthreads();  // every wave has read PT
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = o[cb][q];
+                    __syncthreads();
+                    mfma_tile<T, true>(PTl, PTl, acc, w, lane);  // S_{K,K} -= L_{K,K-1} L_{K,K-1}^T
+                    // L_{K,K-1} drained: its flag (pending tile K+1's last update waits on it)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (tid == 0 && DM > 1)
+                        __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (tdbg) ck[1] = clock64();
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
+                __syncthreads();
+                blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
+                                         (lds_t<T>*)rd, status, tid, tdbg);
+                if (tdbg) ck[2] = clock64();
+                // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]; L_{K,K} to the band
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int e = tid + 256 * u;
+                    st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int e = tid + 256 * u, r = e & 63, c = e >> 6;
+                    if (r >= c && in_band(K, K, r, c)) st_sc1(&CB[band_idx(K, K, r, c)], PT[r][c]);
+                }
+                // Dinv[K] at once (drained, then its flag): tile (K+2, K) needs it for
+                // pending tile K+2, whose last update the chain waits for after
+                // the NEXT factor (a flag deferred to the next round stalled the
+                // chain: 36 us per block column against 21)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) __hip_atomic_store(&flags[K * DM], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (K + 1 < nb64) load_pend(K + 1);
+                if (tdbg && tid == 0) {  // BSM_BLK_DEBUG: the chain's three steps per block column
+                    ck[3] = clock64();
+                    __hip_atomic_fetch_add(&tdbg[20], (unsigned long long)(ck[1] - ck[0]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[21], (unsigned long long)(ck[2] - ck[1]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[22], (unsigned long long)(ck[3] - ck[2]), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&tdbg[23], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long wc = wall_clock64();
+                    if (K == 0) __hip_atomic_store(&tdbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (K == nb64 - 1) __hip_atomic_store(&tdbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        const int64_t t = chain ? t0 - 1 : t0;
         if (t >= nb64 * DM) break;
         const int64_t K = t / DM, d = t % DM, I = K + d;
         int* fl = flags + K * DM;
         // no such tile (past the matrix or the band), or the sub-diagonal tile
-        // (K + 1, K), which diagonal tile K + 1's workgroup forms (one hand-off
-        // on the chain per block column instead of two)
+        // (K + 1, K), which diagonal tile K + 1's workgroup (or the chain) forms
+        // (one hand-off on the chain per block column instead of two)
         if (I >= nb64 || 64 * d - 63 > b || d == 1) {
             __syncthreads();
             continue;
         }
         const bool sub = d == 0 && K > 0 && DM > 1;  // this workgroup also forms tile (K, K - 1)
-        // this thread's 16 elements of a 64 x 64 tile, in the f64 MFMA accumulator
-        // layout: X[cb][q] = element (row rb + 4q, column 16cb + cm)
-        const int rb = 16 * w + (lane >> 4), cm = lane & 15;
-        lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
-        lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
         T acc[4][4];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
@@ -2532,10 +2639,13 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
         // left-looking updates from block columns J in the band of both I and K
         // (with sub, J = K - 1 comes after tile (K, K - 1) is formed, below)
         const int64_t Jlo = I - (DM - 1) > 0 ? I - (DM - 1) : 0;
+        long long cp0 = 0, cp1 = 0;  // BSM_BLK_DEBUG (pending tiles): the last J's flag wait and the rest
         for (int64_t J = Jlo; J < (sub ? K - 1 : K); ++J) {
+            if (tdbg && chain && d == 0 && J + 2 == K) cp0 = clock64();
             wait_flag(&flags[J * DM + (I - J)]);
             if (d > 0) wait_flag(&flags[J * DM + (K - J)]);
             if (sub) wait_flag(&flags[J * DM + (K - 1 - J)]);
+            if (tdbg && chain && d == 0 && J + 2 == K) cp1 = clock64();
             stage(PT, I, J);
             if (d > 0) stage(QT, K, J);
             if (sub) stage(QT, K - 1, J);
@@ -2543,6 +2653,33 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             mfma_tile<T, true>(PTl, d > 0 ? QTl : PTl, acc, w, lane);
             if (sub) mfma_tile<T, true>(PTl, QTl, acc2, w, lane);
             __syncthreads();
+        }
+        if (chain && d == 0) {
+            // pending tile K for the chain: S_{K,K} and S_{K,K-1} with block
+            // columns J <= K-2 applied, in the accumulator layout, element
+            // (cb, q) of every thread contiguous (2 KiB per store instruction;
+            // thread-contiguous rows made each 8-B store touch its own line:
+            // 48.6k cycles from the last update to the publication)
+            T* pp = pend + K * 8192 + tid;
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    st_sc1(pp + (4 * cb + q) * 256, acc[cb][q]);
+                    st_sc1(pp + 4096 + (4 * cb + q) * 256, acc2[cb][q]);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&pendf[K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tdbg && tid == 0 && cp0) {
+                __hip_atomic_fetch_add(&tdbg[1], (unsigned long long)(cp1 - cp0), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&tdbg[2], (unsigned long long)(clock64() - cp1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&tdbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
         }
         long long cw0 = 0, cw1 = 0, cs1 = 0, cs2 = 0, cs3 = 0;  // BSM_BLK_DEBUG: the chain's steps
         if (sub) {
@@ -3150,7 +3287,20 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
                         "product + stores %.0f, update + drain + flag %.0f, the rest)",
                         (double)t[8] / t[10], (double)t[9] / t[10], (double)t[14] / t[10], (double)t[15] / t[10],
                         (double)t[16] / t[10]);
-            if (t[7] && t[17])
+            if (t[23])
+                fprintf(stderr, "; chain workgroup per block column: L_{K,K-1} + update + flags %.0f cycles, factor "
+                        "%.0f, publish + next pending %.0f; %.3f ms over %llu block columns (%.2f us each, 100 MHz "
+                        "clock)",
+                        (double)t[20] / t[23], (double)t[21] / t[23], (double)t[22] / t[23], (t[13] - t[12]) * 1e-5,
+                        t[23], (t[13] - t[12]) * 1e-2 / (double)t[23]);
+            if (t[23] && t[3])
+                fprintf(stderr, "; chain waits for the next pending tile %.0f cycles; pending tiles: last block "
+                        "column's flags waited %.0f, its update to the publication %.0f",
+                        (double)t[0] / t[23], (double)t[1] / t[3], (double)t[2] / t[3]);
+            if (t[23] && t[17])
+                fprintf(stderr, "; panel factor: wave 0's blocks %.0f, rows below %.0f, trailing %.0f",
+                        (double)t[17] / t[23], (double)t[18] / t[23], (double)t[19] / t[23]);
+            else if (t[7] && t[17])
                 fprintf(stderr, "; panel factor: wave 0's blocks %.0f, rows below %.0f, trailing %.0f",
                         (double)t[17] / t[7], (double)t[18] / t[7], (double)t[19] / t[7]);
             fprintf(stderr, "\n");
@@ -3174,20 +3324,27 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const int64_t n = bd.n, nb64 = (n + 63) / 64, DM = (63 + bd.b) / 64 + 1;
     BSM_TRY(dinv.alloc((size_t)(nb64 > 0 ? nb64 : 1) * 4096 * sizeof(T)));
     if (n == 0) return BSM_OK;
-    DBuf fl;
-    const size_t nfl = (size_t)(nb64 * DM + 2);
+    // BSM_BLK_CHAIN (default 1): one workgroup runs the diagonal chain with
+    // Linv in LDS, fed by pending tiles (pend: S_{K,K}, S_{K,K-1} per block
+    // column, 64 KiB each); 0: one workgroup per diagonal tile (round 2, A/B)
+    const char* ce = getenv("BSM_BLK_CHAIN");
+    const bool chain = !ce || atoi(ce) != 0;
+    DBuf fl, pend;
+    const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0));
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* flags = fl.as<int>();
     int* tix = flags + nb64 * DM;
     int* st = tix + 1;
+    int* pendf = chain ? st + 1 : nullptr;
+    if (chain) BSM_TRY(pend.alloc((size_t)nb64 * 8192 * sizeof(T)));
     int dev = 0, cus = 0, per_cu = 0;
     BSM_HIP_TRY(hipGetDevice(&dev));
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, blk_chol<T>, 256, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_chol does not fit a CU");
     int64_t grid = (int64_t)cus * per_cu;
-    if (grid > nb64 * DM) grid = nb64 * DM;
+    if (grid > nb64 * DM + (chain ? 1 : 0)) grid = nb64 * DM + (chain ? 1 : 0);
     // BSM_BLK_DEBUG=1: watchdog counters in host memory and chain timers;
     // =2: the chain timers alone (device memory: no PCIe atomics on the chain)
     unsigned long long* hdbg = nullptr;
@@ -3212,7 +3369,8 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const char* pe = getenv("BSM_BLK_PANELS");
     const int panels = pe ? atoi(pe) : 1;
     blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
-                                               tdb.as<unsigned long long>(), panels);
+                                               tdb.as<unsigned long long>(), panels, chain ? pend.as<T>() : nullptr,
+                                               pendf);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());

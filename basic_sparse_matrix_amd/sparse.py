@@ -380,6 +380,28 @@ class Csr(GetDims):
             self._dev = dev
         return dev
 
+    def _panic_on_short_columns(self, cols, short) -> None:
+        """rhs.get_col(c)[e.col_index] (sparse.rs:437) panics at the FIRST
+        out-of-range read in the reference's loop order: rows ascending, then
+        RHS columns c ascending (:432), then the row's entries in storage order
+        (:435). The message names that entry's index (not the
+        largest index)."""
+        rp, ci, _ = self._csr_arrays()
+        if not ci.size:
+            return
+        rows_of = np.repeat(np.arange(len(rp) - 1), np.diff(rp.astype(np.int64)))
+        best = None  # (row, c, entry)
+        for j in short:
+            bad = np.nonzero(ci >= len(cols[j]))[0]
+            if bad.size:
+                e = int(bad[0])  # storage order = row order: the first bad entry has the lowest row
+                key = (int(rows_of[e]), j, e)
+                if best is None or key[:2] < best[:2]:
+                    best = key
+        if best is not None:
+            _, j, e = best
+            raise Panic(f"index out of bounds: the len is {len(cols[j])} but the index is {int(ci[e])}")
+
     def _multi_device(self):
         """The matrix partitioned over the multi-GPU context (set_gpus), cached
         like the single-GPU copy for a finalised (immutable) matrix."""
@@ -428,17 +450,15 @@ class Csr(GetDims):
         for c in cols:
             if c.dtype != self.dtype:
                 raise TypeError(f"mul_dense: Csr<{self.dtype}> x Dense<{c.dtype}>")
+        short = [j for j, c in enumerate(cols) if len(c) < x_rows]
+        if short:  # host logic: the reference panics here whatever runs the sums
+            self._panic_on_short_columns(cols, short)
         dev = self._device()
         lib = _lib.require_device()
         arrs = []
         for c in cols:
             a = np.ascontiguousarray(c)
-            if a.shape[0] < x_rows:
-                # rhs.get_col(col)[e.col_index] (sparse.rs:437): a short column panics
-                # only when an entry reaches past its end; the rest is never read
-                ci = self._csr_arrays()[1]
-                if ci.size and int(ci.max()) >= a.shape[0]:
-                    raise Panic(f"index out of bounds: the len is {a.shape[0]} but the index is {int(ci.max())}")
+            if a.shape[0] < x_rows:  # never read past its end (checked above)
                 a = np.concatenate([a, np.zeros(x_rows - a.shape[0], dtype=a.dtype)])
             arrs.append(np.ascontiguousarray(a[:x_rows]))
         if _multi.gpus() is not None:  # row blocks on n GPUs + RCCL all-gather (csrc/multi.hip)
