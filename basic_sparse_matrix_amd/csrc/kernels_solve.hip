@@ -2419,14 +2419,176 @@ __device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B,
         for (int q = 0; q < 4; ++q) X[cb][q] = (T)c[cb][q];
 }
 
+// ---------------------------------------------------------------------------
+// The chain workgroup's dataflow (BSM_BLK_CHAIN=2, an A/B variant). One block
+// column K of the blocked factor, as tasks over 16 x 16 blocks of the diagonal
+// tile (P, row-major) and of L_{K,K-1}^T (A):
+//   PR(w)        wave w: its 16 rows of S_{K,K} to P and of S_{K,K-1}^T to A,
+//                then its row block of L_{K,K-1} = S_{K,K-1} Linv_{K-1}^T (Q
+//                still holds Linv_{K-1}^T), in place in A;
+//   U1(pi, pj)   P[pi][pj] -= L_{K,K-1}[pi] L_{K,K-1}[pj]^T (block column K-1);
+//   F(p)         the 16 x 16 diagonal block p: factor, inverse Di[p], 1/pivots;
+//   R(pb, p)     L[pb][p] = S[pb][p] Di[p]^T;
+//   U(pi, pj, p) P[pi][pj] -= L[pi][p] L[pj][p]^T;
+//   LD(p), LB(p2, p1)  Linv's diagonal and off-diagonal blocks into Q.
+// Each task is the same MFMA / DPP sequence per element as blk_diag_panels and
+// the update of the one-workgroup-per-tile form, so the factor is bit-identical
+// to both; only the order of independent blocks changes. Wave 0 runs the
+// pivot chain's tasks, F(p) -> R(p+1, p) -> U(p+1, p+1, p) -> F(p+1), with no
+// workgroup barrier between them; waves 1-3 take the other tasks from an LDS
+// queue in priority order. A task waits on the done flags (LDS) of the tasks
+// it reads from; every dependency is earlier in the queue or on wave 0's list,
+// which only waits on earlier queue tasks, so the order cannot deadlock
+// (checked by simulation when the table was made).
+enum { TK_U1 = 1, TK_F, TK_R, TK_U, TK_LD, TK_LB };
+struct ChainTask {
+    uint8_t type, a, b, c;
+    int8_t dep[4];
+};
+constexpr int CH_ALLPR = 44;  // pseudo-task: every PR done (Q may be overwritten)
+__constant__ ChainTask kChainTasks[44] = {
+    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 0 PR(0)
+    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 1 PR(1)
+    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 2 PR(2)
+    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 3 PR(3)
+    {TK_U1, 0, 0, 0, {0, -1, -1, -1}},  // 4
+    {TK_U1, 1, 0, 0, {0, 1, -1, -1}},  // 5
+    {TK_U1, 1, 1, 0, {1, -1, -1, -1}},  // 6
+    {TK_U1, 2, 0, 0, {0, 2, -1, -1}},  // 7
+    {TK_U1, 2, 1, 0, {1, 2, -1, -1}},  // 8
+    {TK_U1, 2, 2, 0, {2, -1, -1, -1}},  // 9
+    {TK_U1, 3, 0, 0, {0, 3, -1, -1}},  // 10
+    {TK_U1, 3, 1, 0, {1, 3, -1, -1}},  // 11
+    {TK_U1, 3, 2, 0, {2, 3, -1, -1}},  // 12
+    {TK_U1, 3, 3, 0, {3, -1, -1, -1}},  // 13
+    {TK_F, 0, 0, 0, {4, -1, -1, -1}},  // 14
+    {TK_F, 1, 0, 0, {24, -1, -1, -1}},  // 15
+    {TK_F, 2, 0, 0, {30, -1, -1, -1}},  // 16
+    {TK_F, 3, 0, 0, {33, -1, -1, -1}},  // 17
+    {TK_R, 1, 0, 0, {14, 5, -1, -1}},  // 18
+    {TK_R, 2, 0, 0, {14, 7, -1, -1}},  // 19
+    {TK_R, 3, 0, 0, {14, 10, -1, -1}},  // 20
+    {TK_R, 2, 1, 0, {15, 25, -1, -1}},  // 21
+    {TK_R, 3, 1, 0, {15, 27, -1, -1}},  // 22
+    {TK_R, 3, 2, 0, {16, 31, -1, -1}},  // 23
+    {TK_U, 1, 1, 0, {18, 6, -1, -1}},  // 24
+    {TK_U, 2, 1, 0, {19, 18, 8, -1}},  // 25
+    {TK_U, 2, 2, 0, {19, 9, -1, -1}},  // 26
+    {TK_U, 3, 1, 0, {20, 18, 11, -1}},  // 27
+    {TK_U, 3, 2, 0, {20, 19, 12, -1}},  // 28
+    {TK_U, 3, 3, 0, {20, 13, -1, -1}},  // 29
+    {TK_U, 2, 2, 1, {21, 26, -1, -1}},  // 30
+    {TK_U, 3, 2, 1, {22, 21, 28, -1}},  // 31
+    {TK_U, 3, 3, 1, {22, 29, -1, -1}},  // 32
+    {TK_U, 3, 3, 2, {23, 32, -1, -1}},  // 33
+    {TK_LD, 0, 0, 0, {14, 44, -1, -1}},  // 34
+    {TK_LD, 1, 0, 0, {15, 44, -1, -1}},  // 35
+    {TK_LD, 2, 0, 0, {16, 44, -1, -1}},  // 36
+    {TK_LD, 3, 0, 0, {17, 44, -1, -1}},  // 37
+    {TK_LB, 1, 0, 0, {15, 34, -1, -1}},  // 38
+    {TK_LB, 2, 0, 0, {16, 34, 38, -1}},  // 39
+    {TK_LB, 2, 1, 0, {16, 35, -1, -1}},  // 40
+    {TK_LB, 3, 0, 0, {17, 34, 38, 39}},  // 41
+    {TK_LB, 3, 1, 0, {17, 35, 40, -1}},  // 42
+    {TK_LB, 3, 2, 0, {17, 36, -1, -1}},  // 43
+};
+constexpr int CH_W0 = 11, CH_NQ = 29;
+__constant__ uint8_t kChainWave0[CH_W0] = {4, 14, 18, 24, 15, 21, 30, 16, 23, 33, 17};
+__constant__ uint8_t kChainQueue[CH_NQ] = {5,  6,  7,  8,  9,  10, 11, 12, 13, 19, 20, 25, 26, 27, 28,
+                                           29, 34, 22, 31, 32, 38, 35, 39, 40, 36, 41, 42, 43, 37};
+
+// F(p): wave 0's 16 x 16 block factor and inverse of blk_diag_panels
+template <typename T, bool NR1>
+__device__ __forceinline__ void blk_block_factor(lds_t<T>* P, lds_t<T>* Di, lds_t<T>* rd, int p, int tid, bool& pd) {
+    const int c0 = 16 * p, r = tid & 15;
+    T dv[16], rps[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dv[j] = P[(c0 + r) * TLD + c0 + j];
+    auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
+        const T piv = rowbcast<t>(dv[t]);
+        pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
+        const T rp = NR1 ? rsqrt_nr1(piv) : rsqrt_nr(piv);
+        rps[t] = rp;
+        const T l = dv[t] * rp;
+        dv[t] = l;
+        [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+            ((dv[t + 1 + js] = fma_t(-l, rowbcast<t + 1 + js>(l), dv[t + 1 + js])), ...);
+        }(std::make_integer_sequence<int, 15 - t>{});
+    };
+    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+        (step(std::integral_constant<int, ts>{}), ...);
+    }(std::make_integer_sequence<int, 16>{});
+#pragma unroll
+    for (int j = 0; j < 16; ++j) P[(c0 + r) * TLD + c0 + j] = j <= r ? dv[j] : (T)0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(dv[j]));
+    T x[16];
+    auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
+        T sm = (T)0;
+        [&]<int... qs>(std::integer_sequence<int, qs...>) __attribute__((always_inline)) {
+            ((sm = fma_t(rowbcast<q2>(dv[qs]), x[qs], sm)), ...);
+        }(std::make_integer_sequence<int, q2>{});
+        x[q2] = ((q2 == r ? (T)1 : (T)0) - sm) * rps[q2];
+    };
+    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+        (irow(std::integral_constant<int, ts>{}), ...);
+    }(std::make_integer_sequence<int, 16>{});
+#pragma unroll
+    for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
+}
+
+// R(pb, p): L[pb][p] = S[pb][p] Di[p]^T (one wave, f64 MFMA 16x16x4)
+template <typename T>
+__device__ __forceinline__ void blk_rows_below(lds_t<T>* P, const lds_t<T>* Di, int pb, int p, int l) {
+    const int m = l & 15, kq = l >> 4, r0 = 16 * pb, c0 = 16 * p;
+    bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+        const int k = 4 * k4 + kq;
+        o = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(r0 + m) * TLD + c0 + k], (double)Di[p * 256 + m * 16 + k],
+                                                 o, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[(r0 + kq + 4 * q) * TLD + c0 + m] = (T)o[q];
+}
+
+// U(pi, pj, p): P[pi][pj] -= L[pi][p] L[pj][p]^T (K4 k-steps of 4: 4 within
+// the tile's panel p, from P); U1: the same with the 64 columns of L_{K,K-1}^T
+// in A (16 k-steps)
+template <typename T, int K4>
+__device__ __forceinline__ void blk_block_update(lds_t<T>* P, const lds_t<T>* X, int pi, int pj, int p, int l) {
+    const int m = l & 15, kq = l >> 4, i0 = 16 * pi, j0 = 16 * pj;
+    bsm_d4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (double)P[(i0 + kq + 4 * q) * TLD + j0 + m];
+#pragma unroll
+    for (int k4 = 0; k4 < K4; ++k4) {
+        const int k = 4 * k4 + kq;
+        if (K4 == 4)  // L columns of panel p, rows i0.. / j0.. (P row-major)
+            o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)P[(i0 + m) * TLD + 16 * p + k],
+                                                     (double)P[(j0 + m) * TLD + 16 * p + k], o, 0, 0, 0);
+        else  // X = L_{K,K-1}^T: X[k][r] = L[r][k]
+            o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)X[k * TLD + i0 + m], (double)X[k * TLD + j0 + m], o, 0,
+                                                     0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                 T* __restrict__ Dinv, int* __restrict__ flags,
                                                 int* __restrict__ ticket, int* __restrict__ status,
                                                 unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
-                                                int panels, T* __restrict__ pend, int* __restrict__ pendf) {
+                                                int panels, T* __restrict__ pend, int* __restrict__ pendf,
+                                                int chain_mode) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
+    __shared__ T AT[64][TLD];  // the dataflow chain: S_{K,K-1}^T, then L_{K,K-1}^T in place
+    __shared__ int tdone[48];  // the dataflow chain's task flags (CH_ALLPR included)
+    __shared__ int qhead, prcnt, subcnt;
     __shared__ T rd[64];
     __shared__ T Di[4 * 256];  // blk_diag_panels: the 16 x 16 diagonal blocks' inverses
     __shared__ T Tb[3 * 256];  //                  and its block products
@@ -2513,6 +2675,170 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             // workgroups (flag wait + staging of Linv) on the chain.
             T acc[4][4], acc2[4][4];
             long long ck[6] = {0, 0, 0, 0, 0, 0};
+            if (chain_mode == 2) {
+                // the dataflow form (see kChainTasks)
+                lds_t<T>* const ATl = (lds_t<T>*)&AT[0][0];
+                bool pd = true;
+                auto wait_done = [&](int id) {
+                    long long spins = 0;
+                    while (__hip_atomic_load(&tdone[id], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > SPIN_LIMIT) {
+                            if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                            return;
+                        }
+                    }
+                };
+                auto set_done = [&](int id) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_store(&tdone[id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                };
+                auto run = [&](int id, int slot) {
+                    const ChainTask tk = kChainTasks[id];
+                    const long long cw = (tdbg && slot >= 0) ? clock64() : 0;
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        if (tk.dep[d] >= 0) wait_done(tk.dep[d]);
+                    const long long cr = (tdbg && slot >= 0) ? clock64() : 0;
+                    switch (tk.type) {
+                        case TK_U1: blk_block_update<T, 16>(PTl, ATl, tk.a, tk.b, 0, lane); break;
+                        case TK_F:
+                            blk_block_factor<T, true>(PTl, (lds_t<T>*)Di, (lds_t<T>*)rd, tk.a, tid, pd);
+                            break;
+                        case TK_R: blk_rows_below<T>(PTl, (lds_t<T>*)Di, tk.a, tk.b, lane); break;
+                        case TK_U: blk_block_update<T, 4>(PTl, PTl, tk.a, tk.b, tk.c, lane); break;
+                        case TK_LD: blk_linv_diag<T>(QTl, (lds_t<T>*)Di, tk.a, lane); break;
+                        case TK_LB: blk_linv_block<T>(PTl, QTl, (lds_t<T>*)Di, tk.a, tk.b, lane); break;
+                        default: break;
+                    }
+                    set_done(id);
+                    if (tdbg && slot >= 0 && lane == 0) {  // BSM_BLK_DEBUG: wave 0's task `slot`: wait, run
+                        const long long ce = clock64();
+                        __hip_atomic_fetch_add(&tdbg[24 + slot], (unsigned long long)(cr - cw), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(&tdbg[36 + slot], (unsigned long long)(ce - cr), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                };
+                auto load_pend2 = [&](int64_t Kp) {
+                    const long long cw = tdbg ? clock64() : 0;
+                    wait_flag(&pendf[Kp]);
+                    if (tdbg && tid == 0)
+                        __hip_atomic_fetch_add(&tdbg[0], (unsigned long long)(clock64() - cw), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    const T* pp = pend + Kp * 8192 + tid;
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            acc[cb][q] = ld_sc1(pp + (4 * cb + q) * 256);
+                            acc2[cb][q] = ld_sc1(pp + 4096 + (4 * cb + q) * 256);
+                        }
+                };
+                load_pend2(0);
+                // Linv's strictly upper blocks stay zero for the whole factor:
+                // LD / LB only ever write the lower ones
+#pragma unroll
+                for (int u = 0; u < 16; ++u) QT[tid >> 2][16 * (tid & 3) + u] = (T)0;
+                for (int64_t K = 0; K < nb64; ++K) {
+                    if (tid < 48) tdone[tid] = 0;
+                    if (tid == 0) {
+                        qhead = 0;
+                        prcnt = 0;
+                        subcnt = 0;
+                    }
+                    __syncthreads();
+                    if (tdbg) ck[0] = clock64();
+                    // PR(w): this wave's rows of S_{K,K} to P, its strip of S_{K,K-1}^T
+                    // to A, its row block of L_{K,K-1} (A and Q), back into its strip
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
+                            AT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
+                        }
+                    T o[4][4] = {};
+                    mfma_tile<T, false, true>(ATl, QTl, o, w, lane);
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) AT[16 * cb + cm][rb + 4 * q] = o[cb][q];
+                    set_done(w);
+                    if (lane == 0 && __hip_atomic_fetch_add(&prcnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3)
+                        __hip_atomic_store(&tdone[CH_ALLPR], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    // L_{K,K-1} to the band; the tile's flag once all four waves'
+                    // stores have drained (pending tile K+1's last update waits on it)
+                    if (K > 0) {
+#pragma unroll
+                        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int r = rb + 4 * q, c = 16 * cb + cm;
+                                if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
+                            }
+                    }
+                    auto sub_done = [&] {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0 &&
+                            __hip_atomic_fetch_add(&subcnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3 &&
+                            K > 0 && DM > 1)
+                            __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    };
+                    if (tdbg) ck[1] = clock64();
+                    if (w == 0) {  // the pivot chain; its own stores drain behind F(0)
+                        for (int i = 0; i < CH_W0; ++i) {
+                            run(kChainWave0[i], i);
+                            if (i == 1) sub_done();
+                        }
+                    } else {
+                        sub_done();
+                        for (;;) {
+                            int qi = 0;
+                            if (lane == 0) qi = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            qi = __builtin_amdgcn_readfirstlane(qi);
+                            if (qi >= CH_NQ) break;
+                            run(kChainQueue[qi], -1);
+                        }
+                    }
+                    if (tdbg) ck[2] = clock64();
+                    __syncthreads();
+                    // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]; L_{K,K} to the band
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const int e = tid + 256 * u;
+                        st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (tid == 0) __hip_atomic_store(&flags[K * DM], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {  // no tile of this kernel reads L_{K,K}: drains later
+                        const int e = tid + 256 * u, r = e & 63, c = e >> 6;
+                        if (r >= c && in_band(K, K, r, c)) st_sc1(&CB[band_idx(K, K, r, c)], PT[r][c]);
+                    }
+                    if (K + 1 < nb64) load_pend2(K + 1);
+                    if (tdbg && tid == 0) {
+                        ck[3] = clock64();
+                        __hip_atomic_fetch_add(&tdbg[20], (unsigned long long)(ck[1] - ck[0]), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(&tdbg[21], (unsigned long long)(ck[2] - ck[1]), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(&tdbg[22], (unsigned long long)(ck[3] - ck[2]), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_add(&tdbg[23], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long wc = wall_clock64();
+                        if (K == 0) __hip_atomic_store(&tdbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (K == nb64 - 1)
+                            __hip_atomic_store(&tdbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                if (w == 0 && lane == 0 && !pd) atomicOr(status, ST_NOT_PD);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                continue;
+            }
             auto load_pend = [&](int64_t Kp) {
                 const long long cw = tdbg ? clock64() : 0;
                 wait_flag(&pendf[Kp]);
@@ -3275,7 +3601,7 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
     for (int i = 0; i < 200; ++i) {
         if (hipStreamQuery(s) == hipSuccess) {
             fprintf(stderr, "[blk debug] %s done: tickets %lld grid %lld", what, tickets, grid);
-            unsigned long long t[24] = {};
+            unsigned long long t[48] = {};
             if (tdev && hipMemcpy(t, tdev, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) t[7] = t[10] = 0;
             if (t[7])
                 fprintf(stderr, "; per diagonal tile: factor %.0f cycles, inverse %.0f, factor..drained %.0f; "
@@ -3303,6 +3629,11 @@ static void blk_watchdog(hipStream_t s, const char* what, unsigned long long* hd
             else if (t[7] && t[17])
                 fprintf(stderr, "; panel factor: wave 0's blocks %.0f, rows below %.0f, trailing %.0f",
                         (double)t[17] / t[7], (double)t[18] / t[7], (double)t[19] / t[7]);
+            if (t[23] && t[36]) {
+                fprintf(stderr, "; wave 0's tasks (wait/run cycles):");
+                for (int i = 0; i < 11; ++i)
+                    fprintf(stderr, " %.0f/%.0f", (double)t[24 + i] / t[23], (double)t[36 + i] / t[23]);
+            }
             fprintf(stderr, "\n");
             return;
         }
@@ -3326,9 +3657,15 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     if (n == 0) return BSM_OK;
     // BSM_BLK_CHAIN (default 1): one workgroup runs the diagonal chain with
     // Linv in LDS, fed by pending tiles (pend: S_{K,K}, S_{K,K-1} per block
-    // column, 64 KiB each); 0: one workgroup per diagonal tile (round 2, A/B)
+    // column, 64 KiB each), barriers between its steps; 2: the same workgroup
+    // as a dataflow of 16 x 16 block tasks over its four waves (measured
+    // slower: 24.4 against 21.7 us per block column, profiles/r03_j_*: each
+    // task pays ~400 cycles of flag polling and ~900 of dispatch, and the four
+    // serial 16 x 16 factors stay on the chain); 0: one workgroup per diagonal
+    // tile (round 2). All three give the same bits.
     const char* ce = getenv("BSM_BLK_CHAIN");
-    const bool chain = !ce || atoi(ce) != 0;
+    const int chain_mode = ce ? atoi(ce) : 1;  // 1: the chain workgroup, 2: its dataflow form, 0: per-tile
+    const bool chain = chain_mode != 0;
     DBuf fl, pend;
     const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0));
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
@@ -3355,8 +3692,8 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
         memset(hdbg, 0, 24 * sizeof(unsigned long long));
     }
     if (dbe) {
-        BSM_TRY(tdb.alloc(24 * sizeof(unsigned long long)));
-        BSM_HIP_TRY(hipMemsetAsync(tdb.p, 0, 24 * sizeof(unsigned long long), s));
+        BSM_TRY(tdb.alloc(48 * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(tdb.p, 0, 48 * sizeof(unsigned long long), s));
     }
     g_blk_phase = "blk_chol launch";
     // BSM_BLK_PANELS: 1 (default) the diagonal tile by 16-column panels on four
@@ -3370,7 +3707,7 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const int panels = pe ? atoi(pe) : 1;
     blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
                                                tdb.as<unsigned long long>(), panels, chain ? pend.as<T>() : nullptr,
-                                               pendf);
+                                               pendf, chain_mode);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());

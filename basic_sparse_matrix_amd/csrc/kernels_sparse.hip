@@ -275,8 +275,10 @@ template <typename T, bool SUB>
 __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ pieces, const int32_t* __restrict__ acol,
                                                   const T* __restrict__ av, const int32_t* __restrict__ bcol,
                                                   const T* __restrict__ bv, int32_t* __restrict__ tcol,
-                                                  T* __restrict__ tval, int32_t* __restrict__ pcnt) {
+                                                  T* __restrict__ tval, int32_t* __restrict__ pcnt,
+                                                  unsigned long long* __restrict__ pdbg) {
     using A = Arith<T>;
+    const long long c_start = pdbg ? clock64() : 0;  // BSM_SS_DEBUG=2: s_memtime stamps per piece
     extern __shared__ __attribute__((aligned(16))) unsigned char piece_sm[];
     int32_t* sac = reinterpret_cast<int32_t*>(piece_sm);
     int32_t* sbc = sac + PIECE_CAP;
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
     T vaw = A::zero(), vbw = A::zero();
     if (ea > pc.a0) load(false, wa, caw, vaw);
     if (eb > pc.b0) load(true, wb, cbw, vbw);
+    const long long c_staged = pdbg ? clock64() : 0;
+    long long c_win = 0;  // cycles spent refilling the windows
     int64_t o = pc.a0 + pc.b0;
     int nbuf = 0;
     int32_t cnt = 0, oc = 0;
@@ -340,12 +344,22 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
     };
     while (ia < ea && ib < eb) {
         if (ia - wa == 64) {
+            const long long c0 = pdbg ? clock64() : 0;
             wa += 64;
             load(false, wa, caw, vaw);
+            if (pdbg) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                c_win += clock64() - c0;
+            }
         }
         if (ib - wb == 64) {
+            const long long c0 = pdbg ? clock64() : 0;
             wb += 64;
             load(true, wb, cbw, vbw);
+            if (pdbg) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                c_win += clock64() - c0;
+            }
         }
         const int32_t ca = rl(caw, (int)(ia - wa)), cb = rl(cbw, (int)(ib - wb));
         if (ca > cb) {
@@ -362,6 +376,8 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
             ++ib;
         }
     }
+    const long long c_merged = pdbg ? clock64() : 0;
+    const int64_t steps = (ia - pc.a0) + (ib - pc.b0);
     // one side is exhausted: the rest of the other side goes out in order,
     // 64 entries per step (ballot compaction of the kept ones)
     if (ia < ea || ib < eb) {
@@ -400,6 +416,15 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
         tval[o + lane] = ov;
     }
     if (lane == 0) pcnt[blockIdx.x] = cnt;
+    if (pdbg && lane == 0) {
+        unsigned long long* d = pdbg + 6 * (int64_t)blockIdx.x;
+        d[0] = (unsigned long long)(c_staged - c_start);   // piece descriptor + LDS staging + first windows
+        d[1] = (unsigned long long)(c_merged - c_staged);  // the two-sided merge loop
+        d[2] = (unsigned long long)c_win;                  //   of which window refills (waited)
+        d[3] = (unsigned long long)steps;                  //   its steps
+        d[4] = (unsigned long long)(clock64() - c_merged); // the one-sided tail
+        d[5] = (unsigned long long)((ea - pc.a0) + (eb - pc.b0));
+    }
 }
 
 // one wave per piece: scratch slot -> the output rows
@@ -659,9 +684,36 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             BSM_TRY(tcol.alloc((a->nnz + b->nnz + 1) * sizeof(int32_t)));
             BSM_TRY(tval.alloc((a->nnz + b->nnz + 1) * sizeof(T)));
             BSM_REQUIRE(n_pieces < (1ll << 31), BSM_ERR_UNSUPPORTED, "too many pieces");
-            piece_merge<T, SUB><<<(unsigned)n_pieces, 64, 2 * PIECE_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(pieces.as<Piece>(), a->col, av, b->col, bv,
-                                                                  tcol.as<int32_t>(), tval.as<T>(), pcnt.as<int32_t>());
+            const char* ssd = getenv("BSM_SS_DEBUG");
+            DBuf pdbg;
+            if (ssd && atoi(ssd) >= 2) {
+                BSM_TRY(pdbg.alloc(6 * n_pieces * sizeof(unsigned long long)));
+                BSM_HIP_TRY(hipMemsetAsync(pdbg.p, 0, 6 * n_pieces * sizeof(unsigned long long), s));
+            }
+            piece_merge<T, SUB><<<(unsigned)n_pieces, 64, 2 * PIECE_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(
+                pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(), pcnt.as<int32_t>(),
+                pdbg.as<unsigned long long>());
             BSM_HIP_TRY(hipGetLastError());
+            if (pdbg.p) {  // per-piece s_memtime stamps: where a merge step's cycles go
+                std::vector<unsigned long long> h(6 * n_pieces);
+                BSM_HIP_TRY(hipMemcpyAsync(h.data(), pdbg.p, h.size() * sizeof(unsigned long long),
+                                           hipMemcpyDeviceToHost, s));
+                BSM_HIP_TRY(hipStreamSynchronize(s));
+                double sum[6] = {}, mx_len = 0, mx_cyc = 0;
+                for (int64_t p = 0; p < n_pieces; ++p) {
+                    for (int k = 0; k < 6; ++k) sum[k] += (double)h[6 * p + k];
+                    const double cyc = (double)(h[6 * p] + h[6 * p + 1] + h[6 * p + 4]);
+                    if (cyc > mx_cyc) {
+                        mx_cyc = cyc;
+                        mx_len = (double)h[6 * p + 5];
+                    }
+                }
+                fprintf(stderr, "[bsm ss debug] piece_merge over %lld pieces: per piece staging %.0f cycles, merge loop "
+                        "%.0f (window refills %.0f) for %.0f steps = %.1f cycles/step, tail %.0f; longest piece %.0f "
+                        "cycles over %.0f entries\n", (long long)n_pieces, sum[0] / n_pieces, sum[1] / n_pieces,
+                        sum[2] / n_pieces, sum[3] / n_pieces, sum[3] > 0 ? sum[1] / sum[3] : 0.0, sum[4] / n_pieces,
+                        mx_cyc, mx_len);
+            }
             BSM_TRY(exclusive_scan_i32_to_i64(pcnt.as<int32_t>(), poff.as<int64_t>(), n_pieces, ws2.p, ws2.bytes, s));
             long_row_totals<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), pstart.as<int64_t>(),
                                                              poff.as<int64_t>(), cnt.as<int32_t>());

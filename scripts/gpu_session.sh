@@ -2,7 +2,8 @@
 # GPU session: scripts/gpu_session.sh TAG STEP...
 # STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>[:extra]
 #       | pmc:<config>:<COUNTER>[:extra] | c5 | gather | torchrun:<config>[:extra]
-#       | py:<script args> | env:VAR=VALUE (for the later steps) | unenv:VAR
+#       | py:<script args> | profpy:<name>:<script args> (the script under rocprofv3 --kernel-trace --stats)
+#       | env:VAR=VALUE (for the later steps) | unenv:VAR
 # Every step runs under its own time limit; the session stops at the first
 # failing step (no retries).
 set -u
@@ -44,6 +45,9 @@ for step in "$@"; do
                     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --config $cfg $extra || exit $? ;;
     c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
     py:*) n=$((n + 1)); run py${n} 600 python ${step#py:} || exit $? ;;
+    profpy:*) IFS=: read -r _ nm args <<< "$step"
+              run profpy_$nm 600 rocprofv3 --kernel-trace --stats -d $OUT/profpy_${nm}_$TAG -o run \
+                  --output-format csv -- python $args || exit $? ;;
     env:*) export "${step#env:}"; echo "=== export ${step#env:}" | tee -a $OUT/session_$TAG.log ;;
     unenv:*) unset "${step#unenv:}" ;;
     *) echo "unknown step $step"; exit 2 ;;
