@@ -160,6 +160,7 @@ struct bsm_tiled {
     uint32_t stage = 4;          // k = 1: chunks per pipeline stage
     uint64_t rows = 0, n_cols = 0, nnz = 0;
     uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
+    uint32_t half = 0;           // k = 32: 1 = two half-width passes, 8 waves per CU (spmm_tiled_k32h)
     uint64_t chunks = 0;         // total, without the over-read padding
     int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
     uint32_t* meta = nullptr;    // (chunks + overread) * 64

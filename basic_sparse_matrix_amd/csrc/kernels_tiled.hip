@@ -222,6 +222,21 @@ __device__ __forceinline__ void sum_chunk(const double2 (&x)[16], const Idx& c, 
     ((*yaddr<I>(c, yw, q) = y[I]), ...);
 }
 
+// BSM_TILED_LDSADD=1 (A/B): the chunk's Y update as LDS atomic adds of the
+// rounded products (ds_add_f64: y + RN(v*x), the same two roundings), no
+// read-back of the rows into registers
+template <int I>
+__device__ __forceinline__ void madd_lds(double2* yp, const double2& x, const Idx& c) {
+    const double v = bv<I>(c);
+    __hip_atomic_fetch_add(&yp->x, __dmul_rn(v, x.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(&yp->y, __dmul_rn(v, x.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int... I>
+__device__ __forceinline__ void sum_chunk_lds(const double2 (&x)[16], const Idx& c, double2* yw, int q,
+                                              std::integer_sequence<int, I...>) {
+    (madd_lds<I>(yaddr<I>(c, yw, q), x[I], c), ...);
+}
+
 // Batch pacing. Within a batch the layout keeps the waves on the same
 // panels (equal chunks per panel), but time noise accumulates from batch to
 // batch; once the waves are spread over the batch cycle, every XCD gathers
@@ -249,7 +264,7 @@ __device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int l
     return false;  // not all resident: stop pacing
 }
 
-template <bool PROBE>
+template <bool PROBE, bool ATOM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const uint32_t* __restrict__ meta, const double* __restrict__ val, const double2* __restrict__ X,
@@ -287,7 +302,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
                     gather<PROBE>(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
-                    sum_chunk(XS[k % 3], M[k], yw, q, SEQ);
+                    if (ATOM) sum_chunk_lds(XS[k % 3], M[k], yw, q, SEQ);
+                    else sum_chunk(XS[k % 3], M[k], yw, q, SEQ);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -300,6 +316,98 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const uint64_t m0 = __ballot(y.x != 0.0), m1 = __ballot(y.y != 0.0);
             if (live && q == 0 && row_nnz)
                 row_nnz[r0 + r] = __popcll((m0 >> (16 * g)) & 0xffffull) + __popcll((m1 >> (16 * g)) & 0xffffull);
+        }
+        if (sync) batch_arrive(bar, 1, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k = 32 in two half-width passes (BSM_TILED_HALF=1, round 3 A/B). The L2
+// misses of spmm_tiled_k32 are one X sweep per batch and XCD (1.3 TB at C4):
+// an XCD holds only the ~20k Y rows that fit its LDS. Here a Y row in LDS is
+// half a row (16 doubles, 128 B), so eight waves per CU hold twice the rows
+// and every X panel fetched into L2 serves twice the gathers; each batch is
+// swept twice (columns 0-15, then 16-31), so the stream is read twice and
+// each gather moves one 128-B line. Same copy, same chunks, same per-element
+// order: bit-identical to spmm_tiled_k32. Lane 16g+q gathers X[col][16h+q]
+// (8 B) for entry (u, g) of the chunk.
+// ---------------------------------------------------------------------------
+constexpr uint32_t HALF_WAVES_PER_CU = 8;
+constexpr uint32_t HALF_RW_MAX = 155;  // 8 waves x (RW+1) rows x 128 B <= 160 KiB of LDS
+
+template <int... I>
+__device__ __forceinline__ void gather_h(double (&x)[16], const Idx& c, const double* __restrict__ Xh, int q,
+                                         std::integer_sequence<int, I...>) {
+    ((x[I] = Xh[(int64_t)(bm<I>(c) >> 8) * 32 + q]), ...);
+}
+template <int I>
+__device__ __forceinline__ void madd_h(double& y, double x, const Idx& c) {
+    y = __dadd_rn(y, __dmul_rn(bv<I>(c), x));
+}
+template <int... I>
+__device__ __forceinline__ void sum_chunk_h(const double (&x)[16], const Idx& c, double* yw, int q,
+                                            std::integer_sequence<int, I...>) {
+    double y[16];
+    ((y[I] = yw[(bm<I>(c) & 255u) * 16 + q]), ...);
+    (madd_h<I>(y[I], x[I], c), ...);
+    ((yw[(bm<I>(c) & 255u) * 16 + q] = y[I]), ...);
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void spmm_tiled_k32h(
+    uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
+    const uint32_t* __restrict__ meta, const double* __restrict__ val, const double* __restrict__ X,
+    double* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar) {
+    extern __shared__ double yhlds[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = threadIdx.x / WAVE;
+    const int g = lane >> 4, q = lane & 15;
+    double* yw = yhlds + (size_t)wave * (rw + 1) * 16;
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+    const uint64_t w0 = gw * rpw;
+    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
+    const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
+    constexpr auto SEQ = std::make_integer_sequence<int, 16>{};
+    bool sync = bar != nullptr;
+    for (uint32_t st = 0; st < 2 * nb; ++st) {  // step = (batch, half)
+        const uint32_t b = st >> 1, h = st & 1;
+        const uint64_t r0 = w0 + (uint64_t)b * rw;
+        if (r0 >= wend) {
+            if (sync) batch_arrive(bar, 2 * nb - st, lane);
+            break;
+        }
+        if (sync && st > 0) sync = batch_wait(bar, waves * st, lane);
+        const int nr = (int)min<uint64_t>(rw, wend - r0);
+        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = 0.0;
+        const double* Xh = X + 16 * h;
+        const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
+        if (c1 > c0) {  // (c1 - c0) % PHASES == 0
+            Idx M[6];
+            double XS[3][16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
+            gather_h(XS[0], M[0], Xh, q, SEQ);
+            gather_h(XS[1], M[1], Xh, q, SEQ);
+            for (int64_t i = c0; i < c1; i += PHASES) {
+#pragma unroll
+                for (int k = 0; k < PHASES; ++k) {
+                    load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
+                    gather_h(XS[(k + 2) % 3], M[(k + 2) % 6], Xh, q, SEQ);
+                    __builtin_amdgcn_sched_barrier(0);
+                    sum_chunk_h(XS[k % 3], M[k], yw, q, SEQ);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        for (int rb = 0; rb < nr; rb += 4) {  // Y half rows; nonzero counts over both halves
+            const int r = rb + g;
+            const bool live = r < nr;
+            const double y = live ? yw[r * 16 + q] : 0.0;
+            if (live) Y[(r0 + r) * 32 + 16 * h + q] = y;
+            const uint64_t m = __ballot(y != 0.0);
+            if (live && q == 0 && row_nnz) {
+                const int n = __popcll((m >> (16 * g)) & 0xffffull);
+                row_nnz[r0 + r] = h ? row_nnz[r0 + r] + n : n;  // the same lane wrote the first half
+            }
         }
         if (sync) batch_arrive(bar, 1, lane);
     }
@@ -455,16 +563,20 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     BSM_TRY(current_device(&dev));
     int cus = 0;
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const uint32_t nw = env_u32("BSM_TILED_WAVES", (k == 1 ? K1_WAVES_PER_CU : 4u) * (uint32_t)cus);
+    // k = 32: BSM_TILED_HALF=1 selects the two half-width passes (8 waves per CU)
+    const uint32_t half = k == 32 && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
+    const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : (half ? HALF_WAVES_PER_CU : 4u);
+    const uint32_t nw_env = env_u32("BSM_TILED_WAVES", wpc * (uint32_t)cus);
+    const uint32_t nw = half ? (nw_env + wpc - 1) / wpc * wpc : nw_env;  // whole workgroups
     const uint32_t k1_stage = env_u32("BSM_TILED_K1_STAGE", K1_STAGE_DEFAULT) == 8 ? 8u : 4u;
-    const uint32_t rw_cap = k == 1 ? K1_RW_MAX : RW_MAX;
+    const uint32_t rw_cap = k == 1 ? K1_RW_MAX : (half ? HALF_RW_MAX : RW_MAX);
     uint32_t rw_max = env_u32("BSM_TILED_RW", rw_cap);
     rw_max = rw_max < 8u ? 8u : (rw_max > rw_cap ? rw_cap : rw_max);
     const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", k == 1 ? K1_PSHIFT : PSHIFT);
     const double pace = 1.0 + env_u32("BSM_TILED_PACE_PCT", PACE_PCT) / 100.0;
     const uint32_t pad = k == 1 ? 1u : PHASES;  // k = 1 runs a task's tail chunks unpipelined
     const uint32_t overread = k == 1 ? 2 * k1_stage : OVERREAD;
-    BSM_REQUIRE(nw >= 4 && nw % 4 == 0 && pshift < 32, BSM_ERR_INVALID, "tiled: bad geometry");
+    BSM_REQUIRE(nw >= wpc && nw % wpc == 0 && pshift < 32, BSM_ERR_INVALID, "tiled: bad geometry");
     const uint64_t rpw64 = (rows + nw - 1) / nw;
     BSM_REQUIRE(rpw64 < (1ull << 31), BSM_ERR_UNSUPPORTED, "tiled: too many rows per wave");
     const uint32_t rpw = rpw64 ? (uint32_t)rpw64 : 1u;
@@ -538,6 +650,7 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     t->nb = nb;
     t->rw = rw;
     t->pshift = pshift;
+    t->half = half;
     t->chunks = (uint64_t)total;
     t->overread = overread;
     t->stage = k1_stage;
@@ -554,7 +667,7 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
     BSM_REQUIRE(!neg_init || t->k == 1, BSM_ERR_INVALID, "tiled: -0 init only for k = 1");
     if (t->rows == 0) return BSM_OK;
     unsigned* bar = nullptr;
-    if (t->bar && t->nb > 1 && env_u32("BSM_TILED_SYNC", 1)) {
+    if (t->bar && (t->nb > 1 || t->half) && env_u32("BSM_TILED_SYNC", 1)) {
         BSM_HIP_TRY(hipMemsetAsync(t->bar, 0, 8 * BAR_STRIDE * sizeof(unsigned), s));
         bar = t->bar;
     }
@@ -567,11 +680,18 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
                                               static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar,
                                               neg_init, xmask);
+    } else if (t->half) {
+        const size_t lds = (size_t)HALF_WAVES_PER_CU * (t->rw + 1) * 128;
+        spmm_tiled_k32h<<<dim3(t->nw / HALF_WAVES_PER_CU), 64 * HALF_WAVES_PER_CU, lds, s>>>(
+            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val, static_cast<const double*>(x),
+            static_cast<double*>(y), row_nnz, bar);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
         // BSM_TILED_PROBE_MASK=<mask> (measurement only, wrong results): see gather()
         static const uint32_t xmask = env_u32("BSM_TILED_PROBE_MASK", 0xffffffffu);
-        auto kern = xmask == 0xffffffffu ? spmm_tiled_k32<false> : spmm_tiled_k32<true>;
+        static const bool atom = env_u32("BSM_TILED_LDSADD", 0) == 1;
+        auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true, false>
+                                         : (atom ? spmm_tiled_k32<false, true> : spmm_tiled_k32<false, false>);
         kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
                                               static_cast<const double2*>(x), static_cast<double2*>(y), row_nnz, bar,
                                               xmask);
