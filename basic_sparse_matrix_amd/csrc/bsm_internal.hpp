@@ -116,18 +116,47 @@ int ctx_stream(hipStream_t* s);  // stream of the calling thread's device
 // (a pageable hipMemcpyAsync costs ~19 us; this is a few).
 hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s);
 
-// RAII device buffer for host-path temporaries.
+// Per-thread cache of device temporaries (tmp_get / tmp_put): a hipFree
+// waits for the whole device, and a call such as add_sparse makes ~25 of
+// them (1.3-2 ms per call at the reference bench's e = 300k,
+// profiles/r03_u_*). A cached block is only handed out again to the same
+// thread for the same stream, so stream order separates its uses.
+void* tmp_get(size_t n, hipStream_t s, size_t* cap);
+void tmp_put(void* p, size_t cap, hipStream_t s);
+
+// RAII device buffer for host-path temporaries. alloc(n) is hipMalloc /
+// hipFree; alloc(n, s) takes the block from the calling thread's cache for
+// stream s and gives it back there, for the many small temporaries of a call.
 struct DBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    hipStream_t st = nullptr;
+    size_t cap = 0;  // > 0: a cached temporary of this capacity
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (cap) tmp_put(p, cap, st);
+            else (void)hipFree(p);
+        }
         p = nullptr;
         bytes = 0;
+        cap = 0;
+    }
+    int alloc(size_t n, hipStream_t s) {
+        reset();
+        if (n == 0) n = 16;
+        p = tmp_get(n, s, &cap);
+        if (!p) {
+            cap = 0;
+            set_error("device temporary of %zu bytes: out of memory", n);
+            return BSM_ERR_OOM;
+        }
+        bytes = n;
+        st = s;
+        return BSM_OK;
     }
     int alloc(size_t n) {
         reset();
@@ -141,7 +170,8 @@ struct DBuf {
         bytes = n;
         return BSM_OK;
     }
-    void* release() {
+    void* release() {  // a cached temporary is never released (it goes back to the cache)
+        if (cap) return nullptr;
         void* q = p;
         p = nullptr;
         bytes = 0;
@@ -177,9 +207,12 @@ struct bsm_csr {
     int32_t* col = nullptr;      // nnz
     void* vals = nullptr;        // nnz * sizeof(T)
     // lazily computed analysis (see bsm_analyse)
-    bool analysed = false;
-    bool rows_sorted = true;  // col non-decreasing inside every row
-    uint64_t max_row_len = 0;
+    // analysis (csr_analyse) is cached on the handle: computed when the handle
+    // is made from host data, lazily for device-built results (add / sub /
+    // mul_sparse) the first time a kernel choice needs it
+    mutable bool analysed = false;
+    mutable bool rows_sorted = true;  // col non-decreasing inside every row
+    mutable uint64_t max_row_len = 0;
     // cached column-panel plan of mul_dense (spmm_plan), keyed by panel width;
     // plan_mu serialises its (re)build and use across threads sharing the handle
     mutable std::mutex plan_mu;
@@ -203,7 +236,7 @@ inline double ms_since(std::chrono::steady_clock::time_point t0) {
 }
 
 int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz);
-int csr_analyse(bsm_csr* m, hipStream_t s);
+int csr_analyse(const bsm_csr* m, hipStream_t s);
 // mul_dense's schedule (capi.hip): build once per handle and k (synchronous;
 // schedule 0 auto, 1 the tiled copy whenever possible, 2 never), then launch.
 // The caller holds a->plan_mu for both.

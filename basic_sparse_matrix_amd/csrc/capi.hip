@@ -127,10 +127,62 @@ int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t n
     return BSM_OK;
 }
 
-int csr_analyse(bsm_csr* m, hipStream_t s) {
+namespace {
+struct TmpCache {
+    struct Ent {
+        void* p;
+        size_t cap;
+        hipStream_t s;
+    };
+    std::vector<Ent> free_list;
+    size_t held = 0;
+    ~TmpCache() {
+        for (auto& e : free_list) (void)hipFree(e.p);
+    }
+};
+TmpCache& tmp_cache() {
+    static thread_local TmpCache c;
+    return c;
+}
+constexpr size_t TMP_CACHE_MAX = 512ull << 20;   // bytes kept per thread
+constexpr size_t TMP_BLOCK_MAX = 256ull << 20;   // larger temporaries are not cached
+}  // namespace
+
+void* tmp_get(size_t n, hipStream_t s, size_t* cap) {
+    size_t c = 4096;
+    while (c < n) c <<= 1;  // power-of-two classes
+    TmpCache& tc = tmp_cache();
+    for (size_t i = 0; i < tc.free_list.size(); ++i) {
+        if (tc.free_list[i].cap == c && tc.free_list[i].s == s) {
+            void* p = tc.free_list[i].p;
+            tc.held -= c;
+            tc.free_list[i] = tc.free_list.back();
+            tc.free_list.pop_back();
+            *cap = c;
+            return p;
+        }
+    }
+    const size_t want = c <= TMP_BLOCK_MAX ? c : n;
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    *cap = want;
+    return p;
+}
+
+void tmp_put(void* p, size_t cap, hipStream_t s) {
+    TmpCache& tc = tmp_cache();
+    if (cap > TMP_BLOCK_MAX || (cap & (cap - 1)) || tc.held + cap > TMP_CACHE_MAX) {
+        (void)hipFree(p);
+        return;
+    }
+    tc.free_list.push_back({p, cap, s});
+    tc.held += cap;
+}
+
+int csr_analyse(const bsm_csr* m, hipStream_t s) {
     if (m->analysed) return BSM_OK;
     DBuf out;
-    BSM_TRY(out.alloc(3 * sizeof(uint64_t)));
+    BSM_TRY(out.alloc(3 * sizeof(uint64_t), s));
     BSM_TRY(analyse_dispatch(m->row_ptr, m->col, m->rows, m->cols, out.as<uint64_t>(), s));
     uint64_t h[3] = {0, 0, 0};
     BSM_HIP_TRY(hipMemcpyAsync(h, out.p, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -337,6 +389,7 @@ int csr_upload_rows(int dtype, uint64_t r0, uint64_t r1, uint64_t cols, const ui
 int spmm_prepare_locked(const bsm_csr* a, uint64_t k, int schedule, uint64_t reserve, hipStream_t s,
                         PlanTimes* pt) {
     if (k == 0) return BSM_OK;
+    BSM_TRY(csr_analyse(a, s));  // cached; device-built results are analysed here, lazily
     const auto t_start = host_now();
     if (schedule != 2 && !a->tiled_tried && !spmm_wants_split(a->dtype, k, a->max_row_len) &&
         (schedule == 1 ? a->dtype == BSM_F64 && (k == 1 || k == 32) && a->nnz > 0
@@ -379,6 +432,7 @@ int spmm_launch_locked(const bsm_csr* a, uint64_t k, bool allow_tiled, const voi
         if (nz && a->rows) BSM_HIP_TRY(hipMemsetAsync(nz, 0, a->rows * sizeof(int32_t), s));
         return BSM_OK;
     }
+    BSM_TRY(csr_analyse(a, s));  // cached (a no-op once done)
     const uint64_t w = spmm_panel_cols(a->dtype, a->cols, k);
     if (allow_tiled && a->tiled && a->tiled->k == k) return tiled_spmm(a->tiled, x, y, nz, false, s);
     if (spmm_wants_split(a->dtype, k, a->max_row_len))
@@ -664,6 +718,7 @@ int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void
     // storage order; otherwise sort each row stably first: (A^T)^T.
     const bsm_csr* src = a;
     bsm_csr* sorted = nullptr;
+    BSM_TRY(csr_analyse(a, s));  // rows_sorted (cached)
     if (!a->rows_sorted) {
         bsm_csr* t = nullptr;
         BSM_TRY(transpose_dispatch(a, &t, s));

@@ -2293,15 +2293,35 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             T dv[16], rps[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) dv[j] = P[(c0 + r) * TLD + c0 + j];
+            // The factor and the block's inverse in one pass. Step t: the pivot,
+            // column t of L (l, lane j: L[j][t]), the trailing update of the
+            // rows below by L[j][t] broadcast from lane j; and, with the same
+            // broadcasts, x[t] = Linv[t][r] of lane r's inverse column and its
+            // terms in the later rows' sums (acc[j] += L[j][t] x[t]): the FMAs
+            // of the row-by-row inverse, in the same order per row, so the
+            // same bits, with no second pass and no second set of broadcasts.
+            // The next pivot is lane t+1's own update fma(-l, l, dv[t+1]) (its
+            // broadcast of l is its own l): the pivot chain skips that broadcast.
+            T x[16], acc[16];
+#pragma unroll
+            for (int q2 = 0; q2 < 16; ++q2) acc[q2] = (T)0;
+            T nxt = dv[0];
             auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
-                const T piv = rowbcast<t>(dv[t]);
+                const T piv = rowbcast<t>(nxt);
                 pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
                 const T rp = NR1 ? rsqrt_nr1(piv) : rsqrt_nr(piv);
                 rps[t] = rp;
                 const T l = dv[t] * rp;  // lane t: the pivot's square root
                 dv[t] = l;
+                x[t] = ((t == r ? (T)1 : (T)0) - acc[t]) * rp;
+                if constexpr (t < 15) nxt = fma_t(-l, l, dv[t + 1]);
                 [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
-                    ((dv[t + 1 + js] = fma_t(-l, rowbcast<t + 1 + js>(l), dv[t + 1 + js])), ...);
+                    (([&] {
+                         const T bl = rowbcast<t + 1 + js>(l);
+                         dv[t + 1 + js] = fma_t(-l, bl, dv[t + 1 + js]);
+                         acc[t + 1 + js] = fma_t(bl, x[t], acc[t + 1 + js]);
+                     }()),
+                     ...);
                 }(std::make_integer_sequence<int, 15 - t>{});
             };
             [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
@@ -2309,21 +2329,6 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             }(std::make_integer_sequence<int, 16>{});
 #pragma unroll
             for (int j = 0; j < 16; ++j) P[(c0 + r) * TLD + c0 + j] = j <= r ? dv[j] : (T)0;
-            // inverse of the block: lane r forms column r; L[q2][q] of row q2 by row broadcast
-            // (re-broadcast: opaque rows keep the factor's 120 broadcasts from living on in AGPRs)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(dv[j]));
-            T x[16];
-            auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
-                T s = (T)0;
-                [&]<int... qs>(std::integer_sequence<int, qs...>) __attribute__((always_inline)) {
-                    ((s = fma_t(rowbcast<q2>(dv[qs]), x[qs], s)), ...);
-                }(std::make_integer_sequence<int, q2>{});
-                x[q2] = ((q2 == r ? (T)1 : (T)0) - s) * rps[q2];
-            };
-            [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-                (irow(std::integral_constant<int, ts>{}), ...);
-            }(std::make_integer_sequence<int, 16>{});
 #pragma unroll
             for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];  // Di[p][row][col]
 #pragma unroll
@@ -3655,16 +3660,17 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const int64_t n = bd.n, nb64 = (n + 63) / 64, DM = (63 + bd.b) / 64 + 1;
     BSM_TRY(dinv.alloc((size_t)(nb64 > 0 ? nb64 : 1) * 4096 * sizeof(T)));
     if (n == 0) return BSM_OK;
-    // BSM_BLK_CHAIN (default 1): one workgroup runs the diagonal chain with
-    // Linv in LDS, fed by pending tiles (pend: S_{K,K}, S_{K,K-1} per block
-    // column, 64 KiB each), barriers between its steps; 2: the same workgroup
-    // as a dataflow of 16 x 16 block tasks over its four waves (measured
-    // slower: 24.4 against 21.7 us per block column, profiles/r03_j_*: each
+    // BSM_BLK_CHAIN (default 0): one workgroup per diagonal tile (round 2);
+    // 1: one workgroup runs the diagonal chain with Linv in LDS, fed by
+    // pending tiles (pend: S_{K,K}, S_{K,K-1} per block column, 64 KiB each),
+    // barriers between its steps; 2: the same workgroup as a dataflow of
+    // 16 x 16 block tasks over its four waves. Measured on one box
+    // (profiles/r03_o_blk_chain_ab.log): 0 318.6 ms, 1 336.2 ms; 2 is slower
+    // still (24.4 against 21.7 us per block column, profiles/r03_j_*: each
     // task pays ~400 cycles of flag polling and ~900 of dispatch, and the four
-    // serial 16 x 16 factors stay on the chain); 0: one workgroup per diagonal
-    // tile (round 2). All three give the same bits.
+    // serial 16 x 16 factors stay on the chain). All three give the same bits.
     const char* ce = getenv("BSM_BLK_CHAIN");
-    const int chain_mode = ce ? atoi(ce) : 1;  // 1: the chain workgroup, 2: its dataflow form, 0: per-tile
+    const int chain_mode = ce ? atoi(ce) : 0;  // 0: per-tile, 1: the chain workgroup, 2: its dataflow form
     const bool chain = chain_mode != 0;
     DBuf fl, pend;
     const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0));

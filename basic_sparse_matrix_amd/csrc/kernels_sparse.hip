@@ -88,7 +88,9 @@ __device__ __forceinline__ void merge_range(int64_t ia, int64_t ea, int64_t ib, 
 }
 
 constexpr int64_t PIECE_CAP = 2048;  // entries per side staged in LDS by piece_merge
-constexpr int64_t LONG_ROW = 2048;  // la + lb above this: cut the row into pieces (wave merges)
+constexpr int64_t LONG_ROW = 64;  // la + lb above this: cut the row into pieces (one thread's merge costs
+                                  // ~350 ns per step, dependent global loads: a 2,000-entry row took 55 + 108
+                                  // us of count + fill at e = 100k)
 
 __device__ __forceinline__ bool is_long(const int64_t* arp, const int64_t* brp, int64_t r) {
     return (arp[r + 1] - arp[r]) + (brp[r + 1] - brp[r]) > LONG_ROW;
@@ -138,7 +140,7 @@ struct Piece {
 
 // Long-row setup, chunk-parallel: a long row's two sides are cut into
 // chunks of LR_CHUNK entries (listed on the host from the rows' extents).
-constexpr int64_t LR_CHUNK = 16384;
+constexpr int64_t LR_CHUNK = 2048;
 
 struct LrChunk {
     int64_t l;     // long-row index
@@ -427,6 +429,378 @@ __global__ __launch_bounds__(64) void piece_merge(const Piece* __restrict__ piec
     }
 }
 
+// ---- long rows, round 3: recursive cut + one lane per leaf ------------------
+// piece_merge above walks a piece with one wave, ~450 cycles per merge step
+// (BSM_SS_DEBUG=2 stamps, profiles/r03_j_ss_add_piece_stamps.log), and the
+// longest piece (up to ~20k steps at e = 100k) sets the kernel's time. The cut
+// that made the pieces applies again inside each one, with m = the largest
+// column of the PIECE:
+//   * both sides hold an m: the first m of each pair up (every smaller value
+//     goes out first), so (a0..qa, b0..qb) + that pair, then the rest;
+//   * only one side holds an m, say self at qa: the rhs side is all smaller,
+//     so once the self pointer reaches qa the rhs drains and self continues
+//     alone: merge(a0..qa, all of rhs) then a plain copy of self from qa on
+//     (the piece's closing pair, if any, after it).
+// Sub-pieces of at most LEAF entries become leaves; leaf l is merged by lane l
+// of the wave (the reference's two-pointer loop, merge_range), one-sided
+// pieces are copied by the whole wave. Every sub-piece writes its kept outputs
+// from scratch position a0 + b0 on: the ranges of a piece's parts are disjoint
+// and in output order (a part emits at most its two lengths plus its pair),
+// so a scan of the used-position flags places every output (pos_copy). The
+// work stack and the leaf list live in registers, entry i in lane i.
+struct SubPiece {
+    int64_t a0, a1, b0, b1, pa, pb;  // pa < 0: no closing pair
+};
+// A leaf costs its length in serial steps on one lane (~650 cycles per step
+// from LDS, branch-free); a cut costs ~700 cycles of wave-wide work plus its
+// scan. Measured per 1,900-entry piece at e = 300k (BSM_SS_DEBUG=4,
+// profiles/r03_x_ss_split_stamps.log, r03_za_*): LEAF 64: 182k cycles, the
+// longest piece 632k; LEAF 128: 186k / 786k; LEAF 192: 255k / 909k.
+constexpr int64_t LEAF = 64;
+constexpr int64_t SPLIT_CAP = 2048;  // entries per side staged in LDS by piece_split
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) { return rl(v, l); }
+__device__ __forceinline__ SubPiece sp_read(const SubPiece& x, int l) {
+    return {rl64(x.a0, l), rl64(x.a1, l), rl64(x.b0, l), rl64(x.b1, l), rl64(x.pa, l), rl64(x.pb, l)};
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = max(v, __shfl_xor(v, off, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+// One side of a piece: its entries in global memory, or staged in LDS
+// (entry e at offset e - base). LDS is indexed by offset, never through a
+// generic pointer moved below the LDS aperture.
+template <typename T>
+struct SideView {
+    const int32_t* __restrict__ gc;
+    const T* __restrict__ gv;
+    const __attribute__((address_space(3))) int32_t* lc;
+    const __attribute__((address_space(3))) T* lv;
+    int64_t base;
+    bool staged;
+    __device__ __forceinline__ int32_t col(int64_t e) const { return staged ? lc[e - base] : gc[e]; }
+    __device__ __forceinline__ T val(int64_t e) const { return staged ? lv[e - base] : gv[e]; }
+};
+
+// first e in [e0, e1) with col(e) == m, else e1 (uniform)
+template <typename S>
+__device__ __forceinline__ int64_t first_eq(const S& sd, int64_t e0, int64_t e1, int32_t m, int lane) {
+    for (int64_t base = e0; base < e1; base += 4 * 64) {  // four windows' loads in flight
+        bool h[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t e = base + 64 * u + lane;
+            h[u] = e < e1 && sd.col(e) == m;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t bal = __ballot(h[u]);
+            if (bal) return base + 64 * u + __builtin_ctzll(bal);
+        }
+    }
+    return e1;
+}
+
+// first e in [e0, e1) with col(e) >= v, else e1; col non-decreasing on
+// [e0, e1) (uniform): 64 samples per round narrow the range 64-fold
+template <typename S>
+__device__ __forceinline__ int64_t lower_bound_wave(const S& sd, int64_t e0, int64_t e1, int32_t v, int lane) {
+    int64_t lo = e0, hi = e1;  // the answer is in [lo, hi]
+    while (hi - lo > 64) {
+        const int64_t step = (hi - lo + 63) / 64, p = lo + lane * step;
+        const uint64_t bal = __ballot(p >= hi || sd.col(p) >= v);  // monotone in the lane
+        const int k = bal ? __builtin_ctzll(bal) : 64;
+        if (k == 0) return lo;
+        const int64_t nlo = lo + (int64_t)(k - 1) * step + 1, nhi = lo + (int64_t)k * step;
+        lo = nlo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const int64_t e = lo + lane;
+    const uint64_t bal = __ballot(e < hi && sd.col(e) >= v);
+    return bal ? lo + __builtin_ctzll(bal) : hi;
+}
+
+template <typename T, bool SUB>
+__global__ __launch_bounds__(64) void piece_split(const Piece* __restrict__ pieces, const int32_t* __restrict__ acol,
+                                                  const T* __restrict__ av, const int32_t* __restrict__ bcol,
+                                                  const T* __restrict__ bv, int32_t* __restrict__ tcol,
+                                                  T* __restrict__ tval, unsigned long long* __restrict__ sdbg) {
+    using A = Arith<T>;
+    // BSM_SS_DEBUG=4: cycles per piece (total, cut scans, leaf merges, one-sided
+    // copies, staging), entries scanned, flushes, leaves, the piece's size
+    long long k_cut = 0, k_flush = 0, k_bulk = 0, k_stage = 0, n_scan = 0, n_flush = 0, n_leaf = 0;
+    const long long k_start = sdbg ? clock64() : 0;
+    using lds_i = __attribute__((address_space(3))) int32_t;
+    using lds_v = __attribute__((address_space(3))) T;
+    const int lane = threadIdx.x;
+    const Piece pc = pieces[blockIdx.x];
+    // A sub-piece that still needs cutting and fits in LDS (both sides, and
+    // its closing pair, which always sits at a1 / b1) is staged there with
+    // its whole subtree: every cut scan and leaf step of it then reads LDS
+    // (~100 cycles) instead of global memory (~1 us per dependent step). The
+    // top piece is staged at once when it fits; a piece too long for LDS (a
+    // row's tail) is cut from global memory until its parts fit.
+    extern __shared__ __attribute__((aligned(16))) unsigned char split_sm[];
+    lds_i* sac = (lds_i*)split_sm;
+    lds_i* sbc = sac + SPLIT_CAP;
+    lds_v* sav = (lds_v*)(sbc + SPLIT_CAP);
+    lds_v* sbv = sav + SPLIT_CAP;
+    SideView<T> SA{acol, av, sac, sav, 0, false}, SB{bcol, bv, sbc, sbv, 0, false};
+    bool staged = false;
+    int sp_base = 0;  // staged: the stack level below the staged subtree
+    auto stage_piece = [&](const SubPiece& x) {
+        const int64_t la = (x.a1 - x.a0) + (x.pa >= 0 ? 1 : 0), lb = (x.b1 - x.b0) + (x.pb >= 0 ? 1 : 0);
+        for (int64_t i = lane; i < la; i += 64) {
+            sac[i] = acol[x.a0 + i];
+            sav[i] = av[x.a0 + i];
+        }
+        for (int64_t i = lane; i < lb; i += 64) {
+            sbc[i] = bcol[x.b0 + i];
+            sbv[i] = bv[x.b0 + i];
+        }
+        __syncthreads();
+        SA.base = x.a0;
+        SB.base = x.b0;
+        SA.staged = SB.staged = staged = true;
+    };
+    auto unstage = [&] {
+        SA.staged = SB.staged = staged = false;
+        __syncthreads();  // every lane's LDS reads are done before the next staging
+    };
+    SubPiece stk{}, lf{};  // lane i: stack entry i / leaf i
+    int sp = 0, nl = 0;    // uniform
+    auto pair_val = [&](int64_t pa, int64_t pb) -> T {
+        return SUB ? A::sub(SA.val(pa), SB.val(pb)) : A::add(SA.val(pa), SB.val(pb));
+    };
+    auto emit = [&](int64_t o, int32_t c, T v) {
+        tcol[o] = c;
+        tval[o] = v;
+    };
+    auto flush = [&] {  // lane l < nl merges leaf l from position a0 + b0 on (sparse.rs:493-531)
+        const long long k0 = sdbg ? clock64() : 0;
+        n_leaf += nl;
+        n_flush += nl > 0;
+        if (lane < nl) {
+            // one reference merge step per iteration, without branches (the
+            // 64 leaves of a wave differ in every comparison): an exhausted
+            // side reads as column INT32_MAX (device columns are < 2^31 - 1),
+            // so the other side goes out; an equal pair goes out as one entry
+            int64_t o = lf.a0 + lf.b0, ia = lf.a0, ib = lf.b0;
+            while (ia < lf.a1 || ib < lf.b1) {
+                const bool ha = ia < lf.a1, hb = ib < lf.b1;
+                const int32_t ca = ha ? SA.col(ia) : 0x7fffffff, cb = hb ? SB.col(ib) : 0x7fffffff;
+                const T va = ha ? SA.val(ia) : A::zero(), vb = hb ? SB.val(ib) : A::zero();
+                const bool ta = ca <= cb, tb = cb <= ca;  // both: the pair
+                const T v = ta && tb ? (SUB ? A::sub(va, vb) : A::add(va, vb))
+                                     : (ta ? va : (SUB ? A::sub(A::zero(), vb) : vb));
+                if (A::nz(v)) {
+                    tcol[o] = ta ? ca : cb;
+                    tval[o] = v;
+                    ++o;
+                }
+                ia += ta ? 1 : 0;
+                ib += tb ? 1 : 0;
+            }
+            if (lf.pa >= 0) {
+                const T v = pair_val(lf.pa, lf.pb);
+                if (A::nz(v)) {
+                    tcol[o] = SA.col(lf.pa);
+                    tval[o] = v;
+                }
+            }
+        }
+        nl = 0;
+        if (sdbg) k_flush += clock64() - k0;
+    };
+    auto push = [&](const SubPiece& x) {
+        if (sp == 64) {  // stack full (deeply nested columns): merge it on one lane, serially
+            if (nl == 64) flush();
+            if (lane == nl) lf = x;
+            ++nl;
+            return;
+        }
+        if (lane == sp) stk = x;
+        ++sp;
+    };
+    push({pc.a0, pc.a1, pc.b0, pc.b1, pc.pa, pc.pb});
+    // scan budget: inputs that make every cut peel off O(1) entries (e.g. equal
+    // descending rows) stop being cut after ~32 passes over the piece and
+    // merge as they stand, one lane per piece
+    int64_t budget = 32 * ((pc.a1 - pc.a0) + (pc.b1 - pc.b0)) + 4096;
+    while (sp > 0) {
+        if (staged && sp == sp_base) {  // the staged subtree is done: its leaves first
+            flush();
+            unstage();
+        }
+        const SubPiece x = sp_read(stk, --sp);
+        const int64_t na = x.a1 - x.a0, nb = x.b1 - x.b0;
+        if (!staged && na > 0 && nb > 0 && na + nb > LEAF && budget >= 0 &&
+            na + (x.pa >= 0 ? 1 : 0) <= SPLIT_CAP && nb + (x.pb >= 0 ? 1 : 0) <= SPLIT_CAP) {
+            flush();  // leaves so far read global memory; the rest reads LDS
+            const long long k0 = sdbg ? clock64() : 0;
+            stage_piece(x);
+            if (sdbg) k_stage += clock64() - k0;
+            sp_base = sp;
+        }
+        if (na + nb <= LEAF || na == 0 || nb == 0 || budget < 0) {
+            if (na + nb == 0 && x.pa < 0) continue;
+            if (na > 0 && nb > 0) {  // a leaf (a one-sided piece is cheaper as a wave copy)
+                if (nl == 64) flush();
+                if (lane == nl) lf = x;
+                ++nl;
+                continue;
+            }
+            // one side: copied by the wave, entry e to position a0 + b0 + (e -
+            // s0) (scratch positions need not be dense: pos_copy ranks the
+            // used ones), sixteen windows' loads in flight (a row's tail can
+            // leave tens of thousands of entries here, read from global memory)
+            const long long kb0 = sdbg ? clock64() : 0;
+            const bool side_b = nb > 0;
+            const SideView<T> sd = side_b ? SB : SA;
+            const int64_t s0 = side_b ? x.b0 : x.a0, s1 = side_b ? x.b1 : x.a1, o0 = x.a0 + x.b0 - s0;
+            for (int64_t base = s0; base < s1; base += 16 * 64) {
+                T v[16];
+                int32_t c[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int64_t e = base + 64 * u + lane;
+                    v[u] = e < s1 ? sd.val(e) : A::zero();
+                    c[u] = e < s1 ? sd.col(e) : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int64_t e = base + 64 * u + lane;
+                    if (SUB && side_b) v[u] = A::sub(A::zero(), v[u]);
+                    if (e < s1 && A::nz(v[u])) emit(o0 + e, c[u], v[u]);
+                }
+            }
+            if (x.pa >= 0) {
+                const T v = pair_val(x.pa, x.pb);
+                if (A::nz(v) && lane == 0) emit(o0 + s1, SA.col(x.pa), v);
+            }
+            if (sdbg) k_bulk += clock64() - kb0;
+            continue;
+        }
+        budget -= na + nb;
+        const long long kc0 = sdbg ? clock64() : 0;
+        n_scan += na + nb;
+        // the piece's largest column, and whether both sides are sorted
+        int mx = -1;
+        bool srt = true;
+        auto scan_side = [&](const SideView<T>& sd, int64_t e0, int64_t e1) {
+            for (int64_t base = e0; base < e1; base += 8 * 64) {  // eight windows' loads in flight
+                int32_t c[8], n[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t e = base + 64 * u + lane;
+                    c[u] = e < e1 ? sd.col(e) : -1;
+                    n[u] = e + 1 < e1 ? sd.col(e + 1) : 0x7fffffff;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    mx = max(mx, c[u]);
+                    srt = srt && c[u] <= n[u];
+                }
+            }
+        };
+        scan_side(SA, x.a0, x.a1);
+        scan_side(SB, x.b0, x.b1);
+        mx = wave_max_i32(mx);
+        if (__ballot(!srt) == 0) {
+            // sorted sides (the cut at the maximum would peel one pair off the
+            // end): cut by value at the longer side's median v. Everything
+            // below v merges first, on both sides, then the rest.
+            const int32_t v = na >= nb ? SA.col(x.a0 + na / 2) : SB.col(x.b0 + nb / 2);
+            int64_t qa = lower_bound_wave(SA, x.a0, x.a1, v, lane), qb = lower_bound_wave(SB, x.b0, x.b1, v, lane);
+            if (qa == x.a0 && qb == x.b0 && v < 0x7fffffff) {  // nothing below v: cut above it
+                qa = lower_bound_wave(SA, x.a0, x.a1, v + 1, lane);
+                qb = lower_bound_wave(SB, x.b0, x.b1, v + 1, lane);
+            }
+            if (!(qa == x.a0 && qb == x.b0) && !(qa == x.a1 && qb == x.b1)) {
+                if (sdbg) k_cut += clock64() - kc0;
+                push({qa, x.a1, qb, x.b1, x.pa, x.pb});
+                push({x.a0, qa, x.b0, qb, -1, -1});
+                continue;
+            }
+        }
+        // the first occurrence of the maximum on each side
+        const int64_t qa = first_eq(SA, x.a0, x.a1, mx, lane), qb = first_eq(SB, x.b0, x.b1, mx, lane);
+        if (sdbg) k_cut += clock64() - kc0;
+        if (qa < x.a1 && qb < x.b1) {  // the first pair of m splits the piece
+            push({qa + 1, x.a1, qb + 1, x.b1, x.pa, x.pb});
+            push({x.a0, qa, x.b0, qb, qa, qb});
+        } else if (qa < x.a1) {  // only self holds m: merge up to it, then self alone
+            push({qa, x.a1, x.b1, x.b1, x.pa, x.pb});
+            push({x.a0, qa, x.b0, x.b1, -1, -1});
+        } else {  // only rhs holds m
+            push({x.a1, x.a1, qb, x.b1, x.pa, x.pb});
+            push({x.a0, x.a1, x.b0, qb, -1, -1});
+        }
+    }
+    if (nl) flush();
+    if (sdbg && lane == 0) {
+        unsigned long long* d = sdbg + 9 * (int64_t)blockIdx.x;
+        d[0] = (unsigned long long)(clock64() - k_start);
+        d[1] = (unsigned long long)k_cut;
+        d[2] = (unsigned long long)k_flush;
+        d[3] = (unsigned long long)k_bulk;
+        d[4] = (unsigned long long)k_stage;
+        d[5] = (unsigned long long)n_scan;
+        d[6] = (unsigned long long)n_flush;
+        d[7] = (unsigned long long)n_leaf;
+        d[8] = (unsigned long long)((pc.a1 - pc.a0) + (pc.b1 - pc.b0));
+    }
+}
+
+// output count of each long row from the position offsets: its positions are
+// [arp[r] + brp[r], arp[r+1] + brp[r+1])
+__global__ __launch_bounds__(256) void long_row_totals_slots(int64_t n_long, const int64_t* __restrict__ long_rows,
+                                                             const int64_t* __restrict__ arp,
+                                                             const int64_t* __restrict__ brp,
+                                                             const int64_t* __restrict__ soff, int32_t* __restrict__ cnt,
+                                                             int64_t* __restrict__ lstart) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n_long) return;
+    const int64_t r = long_rows[l];
+    lstart[l] = arp[r] + brp[r];
+    cnt[r] = (int32_t)(soff[arp[r + 1] + brp[r + 1]] - soff[arp[r] + brp[r]]);
+}
+
+// Scratch columns start as -1 (memset): a used position holds its column.
+__global__ __launch_bounds__(256) void pos_flags(int64_t n_pos, const int32_t* __restrict__ tcol,
+                                                 int32_t* __restrict__ pvalid) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_pos) pvalid[j] = tcol[j] >= 0 ? 1 : 0;
+}
+
+// every used scratch position to its place in the output row (the scan of
+// the used-position flags gives its rank inside the row); its row is the last
+// long row starting at or before it (lstart: the long rows' first positions,
+// ascending)
+template <typename T>
+__global__ __launch_bounds__(256) void pos_copy(int64_t n_pos, const int32_t* __restrict__ tcol,
+                                                const int64_t* __restrict__ poff, int64_t n_long,
+                                                const int64_t* __restrict__ long_rows,
+                                                const int64_t* __restrict__ lstart, const int64_t* __restrict__ orp,
+                                                const T* __restrict__ tval, int32_t* __restrict__ ocol,
+                                                T* __restrict__ ov) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pos) return;
+    const int32_t c = tcol[j];
+    if (c < 0) return;
+    int64_t lo = 0, hi = n_long - 1;  // last l with lstart[l] <= j
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (lstart[mid] <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t r = long_rows[lo];
+    const int64_t dst = orp[r] + (poff[j] - poff[lstart[lo]]);
+    ocol[dst] = c;
+    ov[dst] = tval[j];
+}
+
 // one wave per piece: scratch slot -> the output rows
 template <typename T>
 __global__ __launch_bounds__(64) void piece_copy(const Piece* __restrict__ pieces, const int32_t* __restrict__ pcnt,
@@ -595,12 +969,21 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
     const uint64_t rows = a->rows;
     DBuf cnt, lflag, lpos, ws;
     CsrGuard g;
-    BSM_TRY(cnt.alloc(rows * sizeof(int32_t)));
-    BSM_TRY(lflag.alloc(rows * sizeof(int32_t)));
-    BSM_TRY(lpos.alloc((rows + 1) * sizeof(int64_t)));
-    BSM_TRY(ws.alloc(scan_workspace_bytes(rows)));
+    BSM_TRY(cnt.alloc(rows * sizeof(int32_t), s));
+    BSM_TRY(lflag.alloc(rows * sizeof(int32_t), s));
+    BSM_TRY(lpos.alloc((rows + 1) * sizeof(int64_t), s));
+    BSM_TRY(ws.alloc(scan_workspace_bytes(rows), s));
     DBuf orp;
-    BSM_TRY(orp.alloc((rows + 1) * sizeof(int64_t)));
+    BSM_TRY(orp.alloc((rows + 1) * sizeof(int64_t), s));
+    // BSM_SS_DEBUG=3: host time per phase (each mark synchronises the stream)
+    static const bool tdbg = getenv("BSM_SS_DEBUG") && atoi(getenv("BSM_SS_DEBUG")) == 3;
+    auto t_last = host_now();
+    auto tmark = [&](const char* what) {
+        if (!tdbg) return;
+        (void)hipStreamSynchronize(s);
+        fprintf(stderr, "[bsm ss time] %-28s %8.3f ms\n", what, ms_since(t_last));
+        t_last = host_now();
+    };
     auto run = [&]<typename T, bool SUB>() -> int {
         const T* av = static_cast<const T*>(a->vals);
         const T* bv = static_cast<const T*>(b->vals);
@@ -612,14 +995,19 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
         int64_t n_long = 0;
         BSM_HIP_TRY(read_dev(&n_long, lpos.as<int64_t>() + rows, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
+        tmark("count + long-row scan");
         DBuf long_rows, mval, pstart, pieces, pcnt, poff, first, ws2, tcol, tval;
+        DBuf scnt, srow, soff, ws3;  // the split path's used-position flags, long-row starts, offsets
+        // BSM_SS_SPLIT=0: the round-2 wave-per-piece merge (piece_merge), for A/B
+        static const bool split = !getenv("BSM_SS_SPLIT") || atoi(getenv("BSM_SS_SPLIT")) != 0;
+        const int64_t n_slots = (int64_t)(a->nnz + b->nnz + 1);
         int64_t n_pieces = 0;
         if (n_long) {
-            BSM_TRY(long_rows.alloc(n_long * sizeof(int64_t)));
-            BSM_TRY(mval.alloc(n_long * sizeof(int32_t)));
-            BSM_TRY(pstart.alloc((n_long + 1) * sizeof(int64_t)));
+            BSM_TRY(long_rows.alloc(n_long * sizeof(int64_t), s));
+            BSM_TRY(mval.alloc(n_long * sizeof(int32_t), s));
+            BSM_TRY(pstart.alloc((n_long + 1) * sizeof(int64_t), s));
             DBuf ext;
-            BSM_TRY(ext.alloc(4 * n_long * sizeof(int64_t)));
+            BSM_TRY(ext.alloc(4 * n_long * sizeof(int64_t), s));
             compact_flags<<<grid_of(rows), 256, 0, s>>>((int64_t)rows, lflag.as<int32_t>(), lpos.as<int64_t>(),
                                                         long_rows.as<int64_t>());
             long_extents<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), a->row_ptr, b->row_ptr,
@@ -628,6 +1016,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             std::vector<int64_t> hx(4 * n_long);
             BSM_HIP_TRY(hipMemcpyAsync(hx.data(), ext.p, hx.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
             BSM_HIP_TRY(hipStreamSynchronize(s));
+        tmark("long rows + extents");
             std::vector<LrChunk> hc;
             for (int64_t l = 0; l < n_long; ++l)
                 for (int64_t side = 0; side < 2; ++side)
@@ -635,8 +1024,8 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                         hc.push_back({l, side, b0, std::min(b0 + LR_CHUNK, hx[4 * l + 2 * side + 1]), 0});
             const int64_t n_chunks = (int64_t)hc.size();
             DBuf chunks, ccnt;
-            BSM_TRY(chunks.alloc((n_chunks ? n_chunks : 1) * sizeof(LrChunk)));
-            BSM_TRY(ccnt.alloc((n_chunks ? n_chunks : 1) * sizeof(int64_t)));
+            BSM_TRY(chunks.alloc((n_chunks ? n_chunks : 1) * sizeof(LrChunk), s));
+            BSM_TRY(ccnt.alloc((n_chunks ? n_chunks : 1) * sizeof(int64_t), s));
             BSM_HIP_TRY(hipMemsetAsync(mval.p, 0xff, n_long * sizeof(int32_t), s));  // -1
             std::vector<int64_t> hcnt(n_chunks);
             if (n_chunks) {
@@ -649,6 +1038,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                 BSM_HIP_TRY(hipMemcpyAsync(hcnt.data(), ccnt.p, n_chunks * sizeof(int64_t), hipMemcpyDeviceToHost, s));
                 BSM_HIP_TRY(hipStreamSynchronize(s));  // hc (host) is read by the copy above
             }
+        tmark("row maxima + counts");
             // M pairs per row: min of the two sides' counts; chunk offsets
             std::vector<int64_t> cnt_side(2 * n_long, 0), ps(n_long + 1, 0);
             for (int64_t i = 0; i < n_chunks; ++i) {
@@ -666,11 +1056,11 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                         (long long)n_chunks, (long long)n_pieces);
             }
             BSM_HIP_TRY(hipMemcpyAsync(pstart.p, ps.data(), (n_long + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-            BSM_TRY(pieces.alloc(n_pieces * sizeof(Piece)));
-            BSM_TRY(pcnt.alloc(n_pieces * sizeof(int32_t)));
-            BSM_TRY(poff.alloc((n_pieces + 1) * sizeof(int64_t)));
-            BSM_TRY(first.alloc(n_pieces * sizeof(int64_t)));
-            BSM_TRY(ws2.alloc(scan_workspace_bytes(n_pieces)));
+            BSM_TRY(pieces.alloc(n_pieces * sizeof(Piece), s));
+            BSM_TRY(pcnt.alloc(n_pieces * sizeof(int32_t), s));
+            BSM_TRY(poff.alloc((n_pieces + 1) * sizeof(int64_t), s));
+            BSM_TRY(first.alloc(n_pieces * sizeof(int64_t), s));
+            BSM_TRY(ws2.alloc(scan_workspace_bytes(n_pieces), s));
             long_piece_init<<<(unsigned)n_long, 256, 0, s>>>(n_long, long_rows.as<int64_t>(), ext.as<int64_t>(),
                                                              pstart.as<int64_t>(), pieces.as<Piece>(),
                                                              first.as<int64_t>());
@@ -681,13 +1071,59 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             }
             BSM_HIP_TRY(hipGetLastError());
             BSM_HIP_TRY(hipStreamSynchronize(s));  // ps / hc (host) are read by the copies above
-            BSM_TRY(tcol.alloc((a->nnz + b->nnz + 1) * sizeof(int32_t)));
-            BSM_TRY(tval.alloc((a->nnz + b->nnz + 1) * sizeof(T)));
+        tmark("pieces");
+            BSM_TRY(tcol.alloc((a->nnz + b->nnz + 1) * sizeof(int32_t), s));
+            BSM_TRY(tval.alloc((a->nnz + b->nnz + 1) * sizeof(T), s));
             BSM_REQUIRE(n_pieces < (1ll << 31), BSM_ERR_UNSUPPORTED, "too many pieces");
+            if (split) {  // recursive cut, one lane per leaf; outputs placed by a scan of the slot counts
+                BSM_TRY(scnt.alloc(n_slots * sizeof(int32_t), s));
+                BSM_TRY(srow.alloc(n_long * sizeof(int64_t), s));  // the long rows' first positions
+                BSM_TRY(soff.alloc((n_slots + 1) * sizeof(int64_t), s));
+                BSM_TRY(ws3.alloc(scan_workspace_bytes((uint64_t)n_slots), s));
+                BSM_HIP_TRY(hipMemsetAsync(tcol.p, 0xff, n_slots * sizeof(int32_t), s));  // -1: unused
+                const char* ssd4 = getenv("BSM_SS_DEBUG");
+                DBuf sdbg;
+                if (ssd4 && atoi(ssd4) == 4) {
+                    BSM_TRY(sdbg.alloc(9 * n_pieces * sizeof(unsigned long long), s));
+                    BSM_HIP_TRY(hipMemsetAsync(sdbg.p, 0, 9 * n_pieces * sizeof(unsigned long long), s));
+                }
+                piece_split<T, SUB><<<(unsigned)n_pieces, 64, 2 * SPLIT_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(
+                    pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(),
+                    sdbg.as<unsigned long long>());
+                pos_flags<<<grid_of((uint64_t)n_slots), 256, 0, s>>>(n_slots, tcol.as<int32_t>(), scnt.as<int32_t>());
+                if (sdbg.p) {
+                    std::vector<unsigned long long> h(9 * n_pieces);
+                    BSM_HIP_TRY(hipMemcpyAsync(h.data(), sdbg.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+                    BSM_HIP_TRY(hipStreamSynchronize(s));
+                    int64_t worst = 0;
+                    double sum[9] = {};
+                    for (int64_t q = 0; q < n_pieces; ++q) {
+                        for (int k = 0; k < 9; ++k) sum[k] += (double)h[9 * q + k];
+                        if (h[9 * q] > h[9 * worst]) worst = q;
+                    }
+                    const unsigned long long* w = &h[9 * worst];
+                    fprintf(stderr, "[bsm ss split] %lld pieces, mean %.0f cycles (cut %.0f, leaves %.0f, one-sided %.0f, "
+                            "staging %.0f; scanned %.0f, flushes %.1f, leaves %.0f, size %.0f); longest: %llu cycles "
+                            "(cut %llu, leaves %llu, one-sided %llu, staging %llu; scanned %llu, flushes %llu, leaves "
+                            "%llu, size %llu)\n", (long long)n_pieces, sum[0] / n_pieces, sum[1] / n_pieces,
+                            sum[2] / n_pieces, sum[3] / n_pieces, sum[4] / n_pieces, sum[5] / n_pieces,
+                            sum[6] / n_pieces, sum[7] / n_pieces, sum[8] / n_pieces, w[0], w[1], w[2], w[3], w[4], w[5],
+                            w[6], w[7], w[8]);
+                }
+                // (scnt: 1 at every used scratch position, srow: its row)
+                BSM_HIP_TRY(hipGetLastError());
+                BSM_TRY(exclusive_scan_i32_to_i64(scnt.as<int32_t>(), soff.as<int64_t>(), (uint64_t)n_slots, ws3.p,
+                                                  ws3.bytes, s));
+                long_row_totals_slots<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), a->row_ptr,
+                                                                       b->row_ptr, soff.as<int64_t>(), cnt.as<int32_t>(),
+                                                                       srow.as<int64_t>());
+                BSM_HIP_TRY(hipGetLastError());
+        tmark("piece_split + scan");
+            } else {
             const char* ssd = getenv("BSM_SS_DEBUG");
             DBuf pdbg;
             if (ssd && atoi(ssd) >= 2) {
-                BSM_TRY(pdbg.alloc(6 * n_pieces * sizeof(unsigned long long)));
+                BSM_TRY(pdbg.alloc(6 * n_pieces * sizeof(unsigned long long), s));
                 BSM_HIP_TRY(hipMemsetAsync(pdbg.p, 0, 6 * n_pieces * sizeof(unsigned long long), s));
             }
             piece_merge<T, SUB><<<(unsigned)n_pieces, 64, 2 * PIECE_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(
@@ -718,29 +1154,40 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             long_row_totals<<<grid_of(n_long), 256, 0, s>>>(n_long, long_rows.as<int64_t>(), pstart.as<int64_t>(),
                                                              poff.as<int64_t>(), cnt.as<int32_t>());
             BSM_HIP_TRY(hipGetLastError());
+            }
         }
         BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), orp.as<int64_t>(), rows, ws.p, ws.bytes, s));
         int64_t nnz = 0;
         BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
+        tmark("row scan + nnz");
         BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, (uint64_t)nnz));
+        tmark("output alloc");
         BSM_HIP_TRY(hipMemcpyAsync(g.m->row_ptr, orp.p, (rows + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         addsub_fill<T, SUB><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr, b->col,
                                                           bv, orp.as<int64_t>(), g.m->col, static_cast<T*>(g.m->vals));
         BSM_HIP_TRY(hipGetLastError());
-        if (n_pieces) {
+        if (n_pieces && split) {
+            pos_copy<T><<<grid_of((uint64_t)n_slots), 256, 0, s>>>(
+                n_slots, tcol.as<int32_t>(), soff.as<int64_t>(), n_long, long_rows.as<int64_t>(), srow.as<int64_t>(),
+                orp.as<int64_t>(), tval.as<T>(), g.m->col, static_cast<T*>(g.m->vals));
+            BSM_HIP_TRY(hipGetLastError());
+        } else if (n_pieces) {
             piece_copy<T><<<(unsigned)n_pieces, 64, 0, s>>>(pieces.as<Piece>(), pcnt.as<int32_t>(), poff.as<int64_t>(),
                                                             first.as<int64_t>(), orp.as<int64_t>(), tcol.as<int32_t>(),
                                                             tval.as<T>(), g.m->col, static_cast<T*>(g.m->vals));
             BSM_HIP_TRY(hipGetLastError());
         }
         BSM_HIP_TRY(hipStreamSynchronize(s));  // the piece buffers die with this scope
+        tmark("fill + copy");
         return BSM_OK;
     };
     BSM_TRY(dispatch_dtype(a->dtype, [&]<typename T>() -> int {
         return sub ? run.template operator()<T, true>() : run.template operator()<T, false>();
     }));
-    BSM_TRY(csr_analyse(g.m, s));  // synchronises
+    tmark("scope exit (frees)");
+    // no eager csr_analyse: the result's columns come from the operands (in
+    // bounds); its row order and longest row are found when first needed
     *out = g.release();
     return BSM_OK;
 }
@@ -760,9 +1207,9 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
     // 2. candidates
     const uint64_t nnz_a = a->nnz;
     DBuf cnt, off, ws;
-    BSM_TRY(cnt.alloc((nnz_a ? nnz_a : 1) * sizeof(int32_t)));
-    BSM_TRY(off.alloc((nnz_a + 1) * sizeof(int64_t)));
-    BSM_TRY(ws.alloc(scan_workspace_bytes(nnz_a ? nnz_a : 1)));
+    BSM_TRY(cnt.alloc((nnz_a ? nnz_a : 1) * sizeof(int32_t), s));
+    BSM_TRY(off.alloc((nnz_a + 1) * sizeof(int64_t), s));
+    BSM_TRY(ws.alloc(scan_workspace_bytes(nnz_a ? nnz_a : 1), s));
     if (nnz_a) {
         spgemm_count<<<grid_of(nnz_a), 256, 0, s>>>(nnz_a, a->col, b->rows, b->row_ptr, cnt.as<int32_t>());
         BSM_HIP_TRY(hipGetLastError());
@@ -776,8 +1223,8 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
     uint64_t n_cand = 0;
     DBuf keys, keys_s, tmp, cand, n_dev;
     if (total > 0) {
-        BSM_TRY(keys.alloc(total * sizeof(uint64_t)));
-        BSM_TRY(keys_s.alloc(total * sizeof(uint64_t)));
+        BSM_TRY(keys.alloc(total * sizeof(uint64_t), s));
+        BSM_TRY(keys_s.alloc(total * sizeof(uint64_t), s));
         spgemm_expand<<<grid_of(total), 256, 0, s>>>((uint64_t)total, nnz_a, off.as<int64_t>(), a->row_ptr, rows,
                                                      a->col, b->row_ptr, b->col, cb, keys.as<uint64_t>());
         BSM_HIP_TRY(hipGetLastError());
@@ -785,16 +1232,16 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
         size_t tb = 0;
         BSM_HIP_TRY(rocprim::radix_sort_keys(nullptr, tb, keys.as<uint64_t>(), keys_s.as<uint64_t>(), (size_t)total,
                                              0u, end_bit, s));
-        BSM_TRY(tmp.alloc(tb ? tb : 1));
+        BSM_TRY(tmp.alloc(tb ? tb : 1, s));
         BSM_HIP_TRY(rocprim::radix_sort_keys(tmp.p, tb, keys.as<uint64_t>(), keys_s.as<uint64_t>(), (size_t)total,
                                              0u, end_bit, s));
-        BSM_TRY(n_dev.alloc(sizeof(uint64_t)));
+        BSM_TRY(n_dev.alloc(sizeof(uint64_t), s));
         // unique into `keys` (free after the sort)
         size_t ub = 0;
         BSM_HIP_TRY(rocprim::unique(nullptr, ub, keys_s.as<uint64_t>(), keys.as<uint64_t>(), n_dev.as<uint64_t>(),
                                     (size_t)total, rocprim::equal_to<uint64_t>(), s));
         DBuf tmp2;
-        BSM_TRY(tmp2.alloc(ub ? ub : 1));
+        BSM_TRY(tmp2.alloc(ub ? ub : 1, s));
         BSM_HIP_TRY(rocprim::unique(tmp2.p, ub, keys_s.as<uint64_t>(), keys.as<uint64_t>(), n_dev.as<uint64_t>(),
                                     (size_t)total, rocprim::equal_to<uint64_t>(), s));
         BSM_HIP_TRY(read_dev(&n_cand, n_dev.p, sizeof(uint64_t), s));
@@ -803,11 +1250,11 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
     // 3. the merge per candidate, 4. keep the nonzero ones
     const size_t es = dtype_size(a->dtype);
     DBuf val, keep, pos, orow;
-    BSM_TRY(val.alloc((n_cand ? n_cand : 1) * es));
-    BSM_TRY(keep.alloc((n_cand ? n_cand : 1) * sizeof(int32_t)));
-    BSM_TRY(pos.alloc((n_cand + 1) * sizeof(int64_t)));
+    BSM_TRY(val.alloc((n_cand ? n_cand : 1) * es, s));
+    BSM_TRY(keep.alloc((n_cand ? n_cand : 1) * sizeof(int32_t), s));
+    BSM_TRY(pos.alloc((n_cand + 1) * sizeof(int64_t), s));
     DBuf ws2;
-    BSM_TRY(ws2.alloc(scan_workspace_bytes(n_cand ? n_cand : 1)));
+    BSM_TRY(ws2.alloc(scan_workspace_bytes(n_cand ? n_cand : 1), s));
     int64_t nnz = 0;
     auto run = [&]<typename T>() -> int {
         if (n_cand) {
@@ -821,7 +1268,7 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
         BSM_HIP_TRY(read_dev(&nnz, pos.as<int64_t>() + n_cand, sizeof(int64_t), s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         BSM_TRY(csr_alloc(&g.m, a->dtype, rows, cols, (uint64_t)nnz));
-        BSM_TRY(orow.alloc((nnz ? nnz : 1) * sizeof(int64_t)));
+        BSM_TRY(orow.alloc((nnz ? nnz : 1) * sizeof(int64_t), s));
         if (n_cand) {
             spgemm_scatter<T><<<grid_of(n_cand), 256, 0, s>>>(n_cand, keys.as<uint64_t>(), cb, val.as<T>(),
                                                               pos.as<int64_t>(), orow.as<int64_t>(), g.m->col,
@@ -833,7 +1280,8 @@ int sparse_mul_dispatch(const bsm_csr* a, const bsm_csr* b, bsm_csr** out, hipSt
         return BSM_OK;
     };
     BSM_TRY(dispatch_dtype(a->dtype, run));
-    BSM_TRY(csr_analyse(g.m, s));  // synchronises: every temporary above is idle
+    BSM_HIP_TRY(hipStreamSynchronize(s));  // the result is complete when the call returns
+    // (no eager csr_analyse: see sparse_addsub_dispatch)
     *out = g.release();
     return BSM_OK;
 }

@@ -333,7 +333,7 @@ def ref_bench_suite(iters=20, which=("sd_mul", "ss_add", "ss_mul")):
                 cpu = lambda: cpu_fn(ra, rb)  # noqa: E731
                 extra = {"b_nnz": int(b.get_nnz())}
             cts = []
-            for _ in range(3 if name != "ss_mul" or e <= 100_000 else 1):
+            for _ in range(7 if name != "ss_mul" else (3 if e <= 100_000 else 1)):  # median: host noise
                 t0 = time.perf_counter()
                 ref = cpu()
                 cts.append(time.perf_counter() - t0)

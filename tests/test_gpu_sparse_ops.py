@@ -125,10 +125,14 @@ def test_mul_sparse_rectangular_mismatch(orc):
 
 
 @pytest.mark.parametrize("case", ["both_have_max", "rhs_lacks_max", "unequal_max_counts", "one_side_empty",
-                                  "sorted_long"])
+                                  "sorted_long", "sorted_duplicates", "one_sorted", "all_equal",
+                                  "descending_equal", "descending", "three_columns", "wide_columns"])
 def test_add_sub_long_rows_vs_oracle(orc, case):
-    """Rows above the piece threshold (8192 entries) are cut at the pairs of
-    the row maximum; every way the maximum can be distributed stays exact."""
+    """Rows above the piece threshold (64 entries) are cut at the pairs of
+    the row maximum, then again inside each piece (at the piece's maximum, or
+    by value when both sides are sorted); every way the maxima can be
+    distributed stays exact, including inputs that defeat the cut (equal
+    descending rows: the scan budget)."""
     rng = np.random.default_rng(len(case))
     n, cols = 30_000, 500
     ca = rng.integers(0, cols, n)
@@ -139,6 +143,22 @@ def test_add_sub_long_rows_vs_oracle(orc, case):
         ca[rng.random(n) < 0.05] = cols - 1
     if case == "sorted_long":
         ca, cb = np.sort(ca), np.sort(cb)
+    if case == "sorted_duplicates":
+        ca, cb = np.sort(ca // 50), np.sort(cb[: n // 3] // 50)
+    if case == "one_sorted":
+        ca = np.sort(ca)
+    if case == "all_equal":
+        ca, cb = np.full(n, 7), np.full(n // 2, 7)
+    if case == "descending_equal":
+        ca = np.sort(ca)[::-1].copy()
+        cb = ca.copy()
+    if case == "descending":
+        ca, cb = np.sort(ca)[::-1].copy(), np.sort(cb)[::-1].copy()
+    if case == "three_columns":
+        ca, cb = ca % 3, cb % 3
+    if case == "wide_columns":
+        cols = 1 << 30
+        ca, cb = rng.integers(0, cols, n), rng.integers(0, cols, n)
     if case == "one_side_empty":
         cb = cb[:0]
     va = rng.integers(-3, 4, len(ca)).astype(np.int64)
@@ -150,3 +170,16 @@ def test_add_sub_long_rows_vs_oracle(orc, case):
     for op, ref in [(Csr.add_sparse, orc.add_sparse), (Csr.sub_sparse, orc.sub_sparse)]:
         assert_csr_bits(op(a, b), *ref(arrays(a), arrays(b)))
         assert_csr_bits(op(b, a), *ref(arrays(b), arrays(a)))
+
+
+@pytest.mark.parametrize("dtype", [np.uint32, np.float64])
+@pytest.mark.parametrize("e", [300_000])
+def test_add_sub_bench_shape_vs_oracle(orc, dtype, e):
+    """ss_add (benches/sparse_dense_mul.rs:37-67) shape: 1000 x 1000, e random
+    inserts per operand, so ~all entries pile into the last row (running-max
+    rule) with unsorted, repeated columns; rows 990-998 hold hundreds."""
+    rng = np.random.default_rng(e + 1)
+    a = unsorted_random(rng, e, 1000, 1000, dtype)
+    b = unsorted_random(rng, e, 1000, 1000, dtype)
+    assert_csr_bits(a.add_sparse(b), *orc.add_sparse(arrays(a), arrays(b)))
+    assert_csr_bits(a.sub_sparse(b), *orc.sub_sparse(arrays(a), arrays(b)))
