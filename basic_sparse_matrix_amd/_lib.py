@@ -283,10 +283,12 @@ class DeviceCsr:
         return cls(h.value)
 
     def download(self):
+        from . import hostpool  # recycled, page-resident result arrays
+
         lib = load()
-        rp = np.empty(self.rows + 1, dtype=np.uint64)
-        ci = np.empty(self.nnz, dtype=np.uint64)
-        v = np.empty(self.nnz, dtype=self.dtype)
+        rp = hostpool.empty(self.rows + 1, np.uint64)
+        ci = hostpool.empty(self.nnz, np.uint64)
+        v = hostpool.empty(self.nnz, self.dtype)
         check(lib.bsm_csr_download(self.handle, ptr(rp), ptr(ci), ptr(v)))
         return rp, ci, v
 

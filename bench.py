@@ -158,6 +158,19 @@ def end_to_end(cfg_name, m, x, dev, iters=3):
             del dc
         out["public_api_split_ms"] = {"in_library": round(float(np.median(lib_ts)) * 1e3, 4),
                                       "caller_frees_previous_result": round(float(np.median(free_ts)) * 1e3, 4)}
+        del prev, res
+        # the same public call with the host result pool off: fresh numpy
+        # arrays per result, faulted in and later unmapped (hostpool.py)
+        os.environ["BSM_HOST_POOL"] = "0"
+        try:
+            ts = []
+            for _ in range(10):
+                t0 = time.perf_counter()
+                a.mul_dense(xd)
+                ts.append(time.perf_counter() - t0)
+            out["public_api_fresh_arrays_ms"] = round(float(np.median(ts)) * 1e3, 4)
+        finally:
+            os.environ.pop("BSM_HOST_POOL", None)
     return out
 
 
