@@ -2270,9 +2270,32 @@ __device__ __forceinline__ void blk_linv_diag(lds_t<T>* Q, const lds_t<T>* Di, i
 // Linv by row blocks: row block p - 1 on waves 1-3 while wave 0 factors
 // block p, the last one at the end. rd[r] = 1 / L[r][r].
 // Every thread of the workgroup must call it (barriers inside).
+// Progressive publication (dpub != nullptr, BSM_BLK_PROG=1): Linv's row block
+// p - 1 is complete once wave 0 has factored block p; wave 3, idle in the rows
+// below and the trailing update from panel 1 on, stores it to dpub (this
+// tile's Dinv, dpub[s * 64 + l] = Linv[l][s]) and raises rbf[p - 1] when the
+// stores have drained, one panel later. The next diagonal tile forms the
+// matching column block of its sub-diagonal tile and that block's update
+// while this factor runs (blk_chol, `prog`): only row block 3 is left on the
+// chain. Row block 3 goes out with the tile's flag, as before.
+template <typename T>
+__device__ __forceinline__ void blk_publish_rowblock(const lds_t<T>* Q, T* __restrict__ dpub, int c, int lane) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int i = lane + 64 * u, s = i >> 4, j = i & 15;
+        st_sc1(&dpub[s * 64 + 16 * c + j], (T)Q[s * TLD + 16 * c + j]);
+    }
+}
+__device__ __forceinline__ void blk_publish_flag(int* rbf, int c, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&rbf[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T, bool NR1 = false>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
-                                                int* status, int tid, unsigned long long* tdbg = nullptr) {
+                                                int* status, int tid, unsigned long long* tdbg = nullptr,
+                                                T* __restrict__ dpub = nullptr, int* rbf = nullptr,
+                                                int* pflag = nullptr) {
     long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
     asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2282,6 +2305,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
     for (int p = 0; p < 4; ++p) {
         const int c0 = 16 * p;
         const long long t0 = tdbg ? clock64() : 0;
+        if (dpub && w == 3 && p >= 2) blk_publish_flag(rbf, p - 2, tid & 63);  // row block p - 2, stored a panel ago
         if (w > 0) {
             // while wave 0 factors block p: Linv's row block p - 1 (its blocks
             // need row blocks < p - 1, Di[p - 1] and L's columns < p - 1, all
@@ -2334,8 +2358,13 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
 #pragma unroll
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
         }
+        // pflag: the caller's global stores (the sub-diagonal tile) drain on
+        // every wave during block 0's factor; the flag follows the barrier
+        if (pflag && p == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const long long t1 = tdbg ? clock64() : 0;
+        if (pflag && p == 0 && tid == 192) __hip_atomic_store(pflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dpub && w == 3 && p >= 1) blk_publish_rowblock<T>(Q, dpub, p - 1, tid & 63);
         // 2. rows below the block, one 16-row block per wave on f64 MFMA
         //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
         const int l = tid & 63, m = l & 15, kq = l >> 4;
@@ -2382,7 +2411,10 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
     }
     // Linv's last row block and diagonal block
     if (w < 3) blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
-    else blk_linv_diag<T>(Q, Di, 3, tid & 63);
+    else {
+        if (dpub) blk_publish_flag(rbf, 2, tid & 63);
+        blk_linv_diag<T>(Q, Di, 3, tid & 63);
+    }
     __syncthreads();
     if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
     if (tdbg && tid == 0) {
@@ -2582,13 +2614,16 @@ __device__ __forceinline__ void blk_block_update(lds_t<T>* P, const lds_t<T>* X,
     for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
 }
 
-template <typename T>
+// MODE: 0 one workgroup per tile (default), 1 / 2 the chain workgroup and its
+// dataflow form (BSM_BLK_CHAIN): an instance per mode, so the default kernel
+// carries none of the chain's registers.
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                 T* __restrict__ Dinv, int* __restrict__ flags,
                                                 int* __restrict__ ticket, int* __restrict__ status,
                                                 unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
                                                 int panels, T* __restrict__ pend, int* __restrict__ pendf,
-                                                int chain_mode) {
+                                                int chain_mode, int* __restrict__ rbf) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
     __shared__ T AT[64][TLD];  // the dataflow chain: S_{K,K-1}^T, then L_{K,K-1}^T in place
@@ -2660,7 +2695,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
     const int rb = 16 * w + (lane >> 4), cm = lane & 15;
     lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
     lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
-    const bool chain = pend != nullptr;
+    const bool chain = MODE != 0 && pend != nullptr;
     for (;;) {
         if (tid == 0) tk = atomicAdd(ticket, 1);
         __syncthreads();
@@ -2680,7 +2715,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             // workgroups (flag wait + staging of Linv) on the chain.
             T acc[4][4], acc2[4][4];
             long long ck[6] = {0, 0, 0, 0, 0, 0};
-            if (chain_mode == 2) {
+            if (MODE == 2) {
                 // the dataflow form (see kChainTasks)
                 lds_t<T>* const ATl = (lds_t<T>*)&AT[0][0];
                 bool pd = true;
@@ -3013,7 +3048,78 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             continue;
         }
         long long cw0 = 0, cw1 = 0, cs1 = 0, cs2 = 0, cs3 = 0;  // BSM_BLK_DEBUG: the chain's steps
-        if (sub) {
+        if (sub && rbf && panels == 1) {
+            // Progressive (BSM_BLK_PROG=1): column block c of L_{K,K-1} =
+            // S_{K,K-1} (row block c of Linv_{K-1})^T as soon as tile K - 1 has
+            // published that row block, then its share of the update
+            // S_{K,K} -= L_{K,K-1}[:, c] L_{K,K-1}[:, c]^T. Blocks 0-2 overlap
+            // tile K - 1's factor. Per output element the MFMA sequence is
+            // mfma_tile's (k ascending from the same start), so the bits are
+            // those of the one-shot form below.
+            lds_t<T>* const ATl = (lds_t<T>*)&AT[0][0];
+            const int kq = lane >> 4, m = lane & 15;
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
+            bsm_d4 ca[4];
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ca[cb][q] = (double)acc[cb][q];
+            const T* dk = Dinv + (K - 1) * 4096;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (tdbg && c == 3) cw0 = clock64();
+                wait_flag(c < 3 ? &rbf[(K - 1) * 4 + c] : &flags[(K - 1) * DM]);
+                if (tdbg && c == 3) cw1 = clock64();
+                T v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {  // QT[s][16c + j] = Linv[16c + j][s], s < 16c + 16
+                    const int i = tid + 256 * u, s = i >> 4, j = i & 15;
+                    v[u] = s < 16 * c + 16 ? ld_sc1(&dk[s * 64 + 16 * c + j]) : (T)0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = tid + 256 * u, s = i >> 4, j = i & 15;
+                    if (s < 16 * c + 16) QT[s][16 * c + j] = v[u];
+                }
+                __syncthreads();
+                if (tdbg && c == 3) cs1 = clock64();
+                bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k4 = 0; k4 < 4 * c + 4; ++k4) {
+                    const int k = 4 * k4 + kq;
+                    oc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)PT[k][16 * w + m], (double)QT[k][16 * c + m],
+                                                              oc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = rb + 4 * q, cc = 16 * c + cm;
+                    const T o = (T)oc[q];
+                    if (in_band(K, K - 1, r, cc)) st_sc1(&CB[band_idx(K, K - 1, r, cc)], o);
+                    AT[cc][r] = o;  // AT[t][r] = L_{K,K-1}[r][t]
+                }
+                __syncthreads();
+                if (tdbg && c == 3) cs2 = clock64();
+#pragma unroll
+                for (int k4 = 0; k4 < 4; ++k4) {
+                    const int k = 16 * c + 4 * k4 + kq;
+                    const double a = -(double)ATl[k * TLD + 16 * w + m];
+#pragma unroll
+                    for (int cb = 0; cb < 4; ++cb)
+                        ca[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)ATl[k * TLD + 16 * cb + m], ca[cb],
+                                                                      0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[cb][q] = (T)ca[cb][q];
+            // the tile's flag (read by tiles below, not by this chain) is raised
+            // inside the factor, once every wave's stores have drained there
+            if (tdbg) cs3 = clock64();
+        } else if (sub) {
             // L_{K,K-1} = S_{K,K-1} L_{K-1,K-1}^-T once diagonal tile K - 1 is done
             if (tdbg) cw0 = clock64();
             wait_flag(&flags[(K - 1) * DM]);
@@ -3067,7 +3173,9 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default);
                 // one Newton step per pivot: C5 factor 317 -> 311 ms, x error 8.8e-11 -> 9.7e-11
                 blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
-                                         (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg);
+                                         (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg,
+                                         rbf ? Dinv + K * 4096 : nullptr, rbf ? rbf + K * 4 : nullptr,
+                                         rbf && sub ? &flags[(K - 1) * DM + 1] : nullptr);
             } else {  // one-wave factor; the inverse below
                 if (w == 0)
                     blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
@@ -3098,11 +3206,20 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-            // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]
+            // Dinv[K][q * 64 + l] = Linv[l][q] = QT[q][l] (progressive: row blocks
+            // 0-2 are out already, row block 3 is left)
+            if (rbf && panels == 1) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int e = tid + 256 * u;
-                st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+                for (int u = 0; u < 4; ++u) {
+                    const int i = tid + 256 * u, q = i >> 4, j = i & 15;
+                    st_sc1(&Dinv[K * 4096 + q * 64 + 48 + j], QT[q][48 + j]);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int e = tid + 256 * u;
+                    st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
+                }
             }
             if (tdbg) {  // the publication: stores drained, then the flag (below)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3672,19 +3789,30 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const char* ce = getenv("BSM_BLK_CHAIN");
     const int chain_mode = ce ? atoi(ce) : 0;  // 0: per-tile, 1: the chain workgroup, 2: its dataflow form
     const bool chain = chain_mode != 0;
+    // BSM_BLK_PROG (default 1, per-tile form with panels = 1 only): tile K
+    // publishes Linv_K by 16-row blocks as its factor forms them, each with a
+    // flag (rbf[4K + c], c < 3; row block 3 goes with the tile's flag), and
+    // tile K + 1 forms its sub-diagonal tile and update block by block
+    // against them; 0: the whole Linv_K after the factor (round 2 / 3 form).
+    // Same bits either way.
+    const char* pge = getenv("BSM_BLK_PROG");
+    const char* pe0 = getenv("BSM_BLK_PANELS");
+    const bool prog = !chain && (!pge || atoi(pge) != 0) && (!pe0 || atoi(pe0) == 1);
     DBuf fl, pend;
-    const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0));
+    const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0) + (prog ? 4 * nb64 : 0));
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* flags = fl.as<int>();
     int* tix = flags + nb64 * DM;
     int* st = tix + 1;
     int* pendf = chain ? st + 1 : nullptr;
+    int* rbf = prog ? st + 1 : nullptr;  // (chain and prog exclude each other)
     if (chain) BSM_TRY(pend.alloc((size_t)nb64 * 8192 * sizeof(T)));
     int dev = 0, cus = 0, per_cu = 0;
     BSM_HIP_TRY(hipGetDevice(&dev));
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, blk_chol<T>, 256, 0));
+    auto kern = chain_mode == 2 ? blk_chol<T, 2> : chain_mode == 1 ? blk_chol<T, 1> : blk_chol<T, 0>;
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_chol does not fit a CU");
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > nb64 * DM + (chain ? 1 : 0)) grid = nb64 * DM + (chain ? 1 : 0);
@@ -3711,9 +3839,9 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     // waits for the inverse's long rows at the barriers).
     const char* pe = getenv("BSM_BLK_PANELS");
     const int panels = pe ? atoi(pe) : 1;
-    blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
+    kern<<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
                                                tdb.as<unsigned long long>(), panels, chain ? pend.as<T>() : nullptr,
-                                               pendf, chain_mode);
+                                               pendf, chain_mode, prog ? rbf : nullptr);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());

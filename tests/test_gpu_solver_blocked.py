@@ -145,3 +145,28 @@ def test_c5_blocked_poisson_1m_f64_properties(orc, golden_c5):
     r = np.zeros(n)
     np.add.at(r, rows, v * x[ci.astype(np.int64)])
     assert np.linalg.norm(r - b) / np.linalg.norm(b) < 1e-12
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("g", [9, 70, 250])
+def test_blocked_progressive_publication_same_bits(orc, monkeypatch, dtype, g):
+    """BSM_BLK_PROG=1 (tile K publishes Linv_K by 16-row blocks and tile K+1
+    forms its sub-diagonal tile block by block, the default) against the
+    whole-Linv hand-off (BSM_BLK_PROG=0) and the chain workgroup
+    (BSM_BLK_CHAIN=1): the same MFMA sequence per element, so the same bits."""
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v.astype(dtype))
+    b = Dense.from_columns(orc.gen_x_cols(1006, n, 2, dtype=dtype))
+    xs = {}
+    for mode, env in (("prog", {"BSM_BLK_PROG": "1"}), ("whole", {"BSM_BLK_PROG": "0"}),
+                      ("chain", {"BSM_BLK_CHAIN": "1"})):
+        monkeypatch.delenv("BSM_BLK_PROG", raising=False)
+        monkeypatch.delenv("BSM_BLK_CHAIN", raising=False)
+        for k_, v_ in env.items():
+            monkeypatch.setenv(k_, v_)
+        x = solve(A, b, order="blocked")
+        xs[mode] = [np.asarray(x.get_col(j)).copy() for j in range(2)]
+    for j in range(2):
+        assert np.array_equal(xs["prog"][j].view(np.uint8), xs["whole"][j].view(np.uint8)), j
+        assert np.array_equal(xs["prog"][j].view(np.uint8), xs["chain"][j].view(np.uint8)), j
