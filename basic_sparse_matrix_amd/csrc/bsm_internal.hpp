@@ -185,6 +185,7 @@ struct DBuf {
 // Row-block x column-panel copy of a matrix (kernels_tiled.hip).
 struct bsm_tiled {
     int device = 0;
+    int dtype = BSM_F64;         // BSM_F64 or BSM_F32 (the value stream's type)
     uint64_t k = 32;             // right-hand columns the copy serves (32 or 1)
     uint32_t overread = 4;       // chunks of dummy padding past the last task
     uint32_t stage = 4;          // k = 1: chunks per pipeline stage
@@ -194,7 +195,7 @@ struct bsm_tiled {
     uint64_t chunks = 0;         // total, without the over-read padding
     int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
     uint32_t* meta = nullptr;    // (chunks + overread) * 64
-    double* val = nullptr;       // (chunks + overread) * 64
+    void* val = nullptr;         // (chunks + overread) * 64 values of dtype
     unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
 };
 
@@ -222,6 +223,9 @@ struct bsm_csr {
     // cached row-block x column-panel copy (kernels_tiled.hip), same mutex
     mutable bsm_tiled* tiled = nullptr;
     mutable bool tiled_tried = false;
+    // row_ptr / col / vals from the result cache (csr_alloc): their block
+    // capacities, 0 = plain hipMalloc (bsm_csr_free hipFrees those)
+    size_t cache_cap[3] = {0, 0, 0};
 };
 
 
@@ -288,8 +292,8 @@ int spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len);
 // synchronous; the copy must leave `reserve` device bytes free; pt (may be
 // null) receives host times of its phases
-int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve = 0,
+int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                 const void* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve = 0,
                  PlanTimes* pt = nullptr);
 int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, bool neg_init, hipStream_t s);
 void tiled_destroy(bsm_tiled* t);

@@ -99,6 +99,104 @@ int ctx_stream(hipStream_t* s) {
     return BSM_OK;
 }
 
+namespace {
+// Result buffers. Every small call returns a new bsm_csr whose three arrays
+// came from hipMalloc, and the caller's bsm_csr_free gave them back with
+// hipFree, which waits for the device and unmaps: ~60 us a malloc / free pair
+// on the box (profiles/r03_u_*), three pairs per result. Blocks of up to
+// 1 GiB now come from a per-device free list by size class (powers of two to
+// 64 MiB, then 16 MiB steps; at most 2 GiB kept per device, the oldest
+// released first). bsm_csr_free waits for the device once, as hipFree did,
+// so a block is never handed out while work queued on the old result runs.
+// BSM_RESULT_CACHE=0: plain hipMalloc / hipFree.
+struct ResultCache {
+    std::mutex mu;
+    std::vector<std::pair<size_t, void*>> free_;  // (class, block), oldest first
+    size_t bytes = 0;
+};
+ResultCache g_rcache[64];
+constexpr size_t RC_MAX_BLOCK = 1ull << 30, RC_KEEP = 2ull << 30;
+bool rc_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("BSM_RESULT_CACHE");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+size_t rc_class(size_t n) {
+    if (n <= 4096) return 4096;
+    if (n <= (64ull << 20)) return size_t(1) << (64 - __builtin_clzll((unsigned long long)(n - 1)));
+    return (n + (16ull << 20) - 1) & ~((16ull << 20) - 1);
+}
+int rc_alloc(int dev, size_t n, void** p, size_t* cap) {
+    *p = nullptr;
+    *cap = 0;
+    if (n == 0) n = 16;
+    if (!rc_enabled() || n > RC_MAX_BLOCK || dev < 0 || dev >= 64) {
+        hipError_t e = hipMalloc(p, n);
+        if (e != hipSuccess) {
+            *p = nullptr;
+            set_error("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+            return e == hipErrorOutOfMemory ? BSM_ERR_OOM : BSM_ERR_HIP;
+        }
+        return BSM_OK;
+    }
+    const size_t c = rc_class(n);
+    ResultCache& rc = g_rcache[dev];
+    {
+        std::lock_guard<std::mutex> lk(rc.mu);
+        for (size_t i = rc.free_.size(); i-- > 0;) {  // newest first: likeliest still in L2 / TLB
+            if (rc.free_[i].first == c) {
+                *p = rc.free_[i].second;
+                rc.free_.erase(rc.free_.begin() + (ptrdiff_t)i);
+                rc.bytes -= c;
+                *cap = c;
+                return BSM_OK;
+            }
+        }
+    }
+    hipError_t e = hipMalloc(p, c);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and retry once
+        std::vector<std::pair<size_t, void*>> drop;
+        {
+            std::lock_guard<std::mutex> lk(rc.mu);
+            drop.swap(rc.free_);
+            rc.bytes = 0;
+        }
+        for (auto& b : drop) (void)hipFree(b.second);
+        e = hipMalloc(p, c);
+    }
+    if (e != hipSuccess) {
+        *p = nullptr;
+        set_error("hipMalloc(%zu) failed: %s", c, hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? BSM_ERR_OOM : BSM_ERR_HIP;
+    }
+    *cap = c;
+    return BSM_OK;
+}
+// the caller has waited for the device
+void rc_release(int dev, void* p, size_t cap) {
+    if (!p) return;
+    if (!cap) {
+        (void)hipFree(p);
+        return;
+    }
+    std::vector<void*> drop;
+    {
+        ResultCache& rc = g_rcache[dev];
+        std::lock_guard<std::mutex> lk(rc.mu);
+        rc.free_.emplace_back(cap, p);
+        rc.bytes += cap;
+        while (rc.bytes > RC_KEEP && !rc.free_.empty()) {
+            rc.bytes -= rc.free_.front().first;
+            drop.push_back(rc.free_.front().second);
+            rc.free_.erase(rc.free_.begin());
+        }
+    }
+    for (void* q : drop) (void)hipFree(q);
+}
+}  // namespace
+
 int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t nnz) {
     const size_t es = dtype_size(dtype);
     BSM_REQUIRE(es != 0, BSM_ERR_INVALID, "unknown dtype %d", dtype);
@@ -112,17 +210,17 @@ int csr_alloc(bsm_csr** out, int dtype, uint64_t rows, uint64_t cols, uint64_t n
     int dev = 0;
     int rc = current_device(&dev);
     m->device = dev;
-    DBuf rp, col, val;
-    if (rc == BSM_OK) rc = rp.alloc((rows + 1) * sizeof(int64_t));
-    if (rc == BSM_OK) rc = col.alloc(nnz * sizeof(int32_t));
-    if (rc == BSM_OK) rc = val.alloc(nnz * es);
+    void* bufs[3] = {nullptr, nullptr, nullptr};
+    const size_t sizes[3] = {(rows + 1) * sizeof(int64_t), nnz * sizeof(int32_t), nnz * es};
+    for (int i = 0; i < 3 && rc == BSM_OK; ++i) rc = rc_alloc(dev, sizes[i], &bufs[i], &m->cache_cap[i]);
     if (rc != BSM_OK) {
+        for (int i = 0; i < 3; ++i) rc_release(dev, bufs[i], m->cache_cap[i]);  // nothing queued on them yet
         delete m;
         return rc;
     }
-    m->row_ptr = static_cast<int64_t*>(rp.release());
-    m->col = static_cast<int32_t*>(col.release());
-    m->vals = val.release();
+    m->row_ptr = static_cast<int64_t*>(bufs[0]);
+    m->col = static_cast<int32_t*>(bufs[1]);
+    m->vals = bufs[2];
     *out = m;
     return BSM_OK;
 }
@@ -392,12 +490,12 @@ int spmm_prepare_locked(const bsm_csr* a, uint64_t k, int schedule, uint64_t res
     BSM_TRY(csr_analyse(a, s));  // cached; device-built results are analysed here, lazily
     const auto t_start = host_now();
     if (schedule != 2 && !a->tiled_tried && !spmm_wants_split(a->dtype, k, a->max_row_len) &&
-        (schedule == 1 ? a->dtype == BSM_F64 && (k == 1 || k == 32) && a->nnz > 0
+        (schedule == 1 ? (a->dtype == BSM_F64 || a->dtype == BSM_F32) && (k == 1 || k == 32) && a->nnz > 0
                        : tiled_wanted(a->dtype, a->rows, a->cols, a->nnz, k, a->max_row_len))) {
         a->tiled_tried = true;
         bsm_tiled* t = nullptr;
-        const int rc = tiled_create(a->rows, a->cols, a->nnz, a->row_ptr, a->col, static_cast<const double*>(a->vals),
-                                    k, schedule == 1 ? BSM_TILED_ANY_PADDING : 0, &t, s, reserve, pt);
+        const int rc = tiled_create(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k,
+                                    schedule == 1 ? BSM_TILED_ANY_PADDING : 0, &t, s, reserve, pt);
         if (rc == BSM_OK) a->tiled = t;
         else if (rc != BSM_ERR_UNSUPPORTED && rc != BSM_ERR_OOM) return rc;
     }
@@ -678,9 +776,18 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
 
 void bsm_csr_free(bsm_csr* m) {
     if (!m) return;
-    if (m->row_ptr) (void)hipFree(m->row_ptr);
-    if (m->col) (void)hipFree(m->col);
-    if (m->vals) (void)hipFree(m->vals);
+    if (m->cache_cap[0] || m->cache_cap[1] || m->cache_cap[2]) {
+        // what hipFree would wait for: work still queued on the result (any
+        // stream of its device) must finish before the blocks are reused
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != m->device) (void)hipSetDevice(m->device);
+        (void)hipDeviceSynchronize();
+        if (cur != m->device && cur >= 0) (void)hipSetDevice(cur);
+    }
+    rc_release(m->device, m->row_ptr, m->cache_cap[0]);
+    rc_release(m->device, m->col, m->cache_cap[1]);
+    rc_release(m->device, m->vals, m->cache_cap[2]);
     if (m->plan_seg) (void)hipFree(m->plan_seg);
     if (m->tiled) tiled_destroy(m->tiled);
     delete m;
@@ -914,7 +1021,7 @@ int bsm_dev_tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz
 int bsm_dev_tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* row_ptr,
                          const int32_t* col, const double* vals, uint64_t k, int flags, bsm_tiled** out,
                          void* stream) {
-    return tiled_create(rows, n_cols, nnz, row_ptr, col, vals, k, flags, out, static_cast<hipStream_t>(stream));
+    return tiled_create(BSM_F64, rows, n_cols, nnz, row_ptr, col, vals, k, flags, out, static_cast<hipStream_t>(stream));
 }
 
 int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* row_nnz, void* stream) {
@@ -924,7 +1031,7 @@ int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* 
 int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols) {
     BSM_REQUIRE(t, BSM_ERR_INVALID, "null argument");
     const uint64_t n = (t->chunks + t->overread) * 64;
-    if (bytes) *bytes = n * 12 + ((uint64_t)t->nw * t->nb + 1) * 8;
+    if (bytes) *bytes = n * (t->dtype == BSM_F32 ? 8 : 12) + ((uint64_t)t->nw * t->nb + 1) * 8;
     if (slots) *slots = t->chunks * 64;
     if (panel_cols) *panel_cols = 1ull << t->pshift;
     return BSM_OK;

@@ -457,7 +457,11 @@ struct SubPiece {
 // profiles/r03_x_ss_split_stamps.log, r03_za_*): LEAF 64: 182k cycles, the
 // longest piece 632k; LEAF 128: 186k / 786k; LEAF 192: 255k / 909k.
 constexpr int64_t LEAF = 64;
-constexpr int64_t SPLIT_CAP = 2048;  // entries per side staged in LDS by piece_split
+// entries per side staged in LDS by piece_split: 4096 for 4-B values (64 KiB
+// per wave; the benches' pieces average ~950 entries per side and the longest
+// reach ~3,400 at every e, so one staging covers the whole subtree), 2048 for
+// 8-B values (48 KiB)
+template <typename T> constexpr int64_t split_cap() { return sizeof(T) <= 4 ? 4096 : 2048; }
 
 __device__ __forceinline__ int64_t rl64(int64_t v, int l) { return rl(v, l); }
 __device__ __forceinline__ SubPiece sp_read(const SubPiece& x, int l) {
@@ -543,6 +547,7 @@ __global__ __launch_bounds__(64) void piece_split(const Piece* __restrict__ piec
     // row's tail) is cut from global memory until its parts fit.
     extern __shared__ __attribute__((aligned(16))) unsigned char split_sm[];
     lds_i* sac = (lds_i*)split_sm;
+    constexpr int64_t SPLIT_CAP = split_cap<T>();
     lds_i* sbc = sac + SPLIT_CAP;
     lds_v* sav = (lds_v*)(sbc + SPLIT_CAP);
     lds_v* sbv = sav + SPLIT_CAP;
@@ -998,6 +1003,9 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
         tmark("count + long-row scan");
         DBuf long_rows, mval, pstart, pieces, pcnt, poff, first, ws2, tcol, tval;
         DBuf scnt, srow, soff, ws3;  // the split path's used-position flags, long-row starts, offsets
+        // host inputs of queued H2D copies: alive until the call's last sync
+        std::vector<LrChunk> hc;
+        std::vector<int64_t> ps;
         // BSM_SS_SPLIT=0: the round-2 wave-per-piece merge (piece_merge), for A/B
         static const bool split = !getenv("BSM_SS_SPLIT") || atoi(getenv("BSM_SS_SPLIT")) != 0;
         const int64_t n_slots = (int64_t)(a->nnz + b->nnz + 1);
@@ -1017,7 +1025,6 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             BSM_HIP_TRY(hipMemcpyAsync(hx.data(), ext.p, hx.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
             BSM_HIP_TRY(hipStreamSynchronize(s));
         tmark("long rows + extents");
-            std::vector<LrChunk> hc;
             for (int64_t l = 0; l < n_long; ++l)
                 for (int64_t side = 0; side < 2; ++side)
                     for (int64_t b0 = hx[4 * l + 2 * side]; b0 < hx[4 * l + 2 * side + 1]; b0 += LR_CHUNK)
@@ -1040,7 +1047,8 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
             }
         tmark("row maxima + counts");
             // M pairs per row: min of the two sides' counts; chunk offsets
-            std::vector<int64_t> cnt_side(2 * n_long, 0), ps(n_long + 1, 0);
+            std::vector<int64_t> cnt_side(2 * n_long, 0);
+            ps.assign(n_long + 1, 0);
             for (int64_t i = 0; i < n_chunks; ++i) {
                 hc[i].off = cnt_side[2 * hc[i].l + hc[i].side];
                 cnt_side[2 * hc[i].l + hc[i].side] += hcnt[i];
@@ -1070,7 +1078,6 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                                                                 pstart.as<int64_t>(), pieces.as<Piece>());
             }
             BSM_HIP_TRY(hipGetLastError());
-            BSM_HIP_TRY(hipStreamSynchronize(s));  // ps / hc (host) are read by the copies above
         tmark("pieces");
             BSM_TRY(tcol.alloc((a->nnz + b->nnz + 1) * sizeof(int32_t), s));
             BSM_TRY(tval.alloc((a->nnz + b->nnz + 1) * sizeof(T), s));
@@ -1087,7 +1094,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                     BSM_TRY(sdbg.alloc(9 * n_pieces * sizeof(unsigned long long), s));
                     BSM_HIP_TRY(hipMemsetAsync(sdbg.p, 0, 9 * n_pieces * sizeof(unsigned long long), s));
                 }
-                piece_split<T, SUB><<<(unsigned)n_pieces, 64, 2 * SPLIT_CAP * (sizeof(int32_t) + sizeof(T)), s>>>(
+                piece_split<T, SUB><<<(unsigned)n_pieces, 64, 2 * split_cap<T>() * (sizeof(int32_t) + sizeof(T)), s>>>(
                     pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(),
                     sdbg.as<unsigned long long>());
                 pos_flags<<<grid_of((uint64_t)n_slots), 256, 0, s>>>(n_slots, tcol.as<int32_t>(), scnt.as<int32_t>());
@@ -1158,10 +1165,17 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
         }
         BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), orp.as<int64_t>(), rows, ws.p, ws.bytes, s));
         int64_t nnz = 0;
-        BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));
-        BSM_HIP_TRY(hipStreamSynchronize(s));
+        // the output holds at most nnz(a) + nnz(b) entries: allocated at that
+        // bound (when it is small) the fill is queued behind the scan and the
+        // count is read with the call's last sync; else the count first
+        const uint64_t nnz_ub = a->nnz + b->nnz;
+        const bool ub = nnz_ub * (sizeof(int32_t) + sizeof(T)) <= (1ull << 30);
+        if (!ub) {
+            BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));
+            BSM_HIP_TRY(hipStreamSynchronize(s));
+        }
         tmark("row scan + nnz");
-        BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, (uint64_t)nnz));
+        BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, ub ? nnz_ub : (uint64_t)nnz));
         tmark("output alloc");
         BSM_HIP_TRY(hipMemcpyAsync(g.m->row_ptr, orp.p, (rows + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         addsub_fill<T, SUB><<<grid_of(rows), 256, 0, s>>>((int64_t)rows, a->row_ptr, a->col, av, b->row_ptr, b->col,
@@ -1177,6 +1191,10 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                                                             first.as<int64_t>(), orp.as<int64_t>(), tcol.as<int32_t>(),
                                                             tval.as<T>(), g.m->col, static_cast<T*>(g.m->vals));
             BSM_HIP_TRY(hipGetLastError());
+        }
+        if (ub) {
+            BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));  // syncs the stream
+            g.m->nnz = (uint64_t)nnz;
         }
         BSM_HIP_TRY(hipStreamSynchronize(s));  // the piece buffers die with this scope
         tmark("fill + copy");

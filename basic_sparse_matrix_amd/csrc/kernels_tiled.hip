@@ -50,6 +50,7 @@ constexpr int PHASES = 6;        // pipeline unroll; task chunk counts are multi
 constexpr int OVERREAD = 4;      // chunks the pipeline reads past a task's end
 constexpr uint32_t DONE = 0xffffffffu;
 constexpr uint32_t RW_MAX = 155;  // 4 waves x (RW+1) rows x 256 B <= 160 KiB of LDS
+constexpr uint32_t RW_MAX_F32 = 255;  // f32: 128-B rows; the 8-bit row field (dummy row = RW) caps it
 constexpr uint32_t PSHIFT = 12;   // panel = 4096 columns = 1 MiB of X (C4 sweep: 2^10..2^12 flat, 2^13 +12 %, 2^14 +42 %)
 constexpr uint32_t PACE_PCT = 3;  // chunk budget per panel over the task's mean (padding ~ this; C4: 2 % +19 %, 6 % +2 %)
 
@@ -66,15 +67,15 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // layout builder: one wave per task (gw, b). COUNT pass writes the task's
 // chunk count (a multiple of PHASES); WRITE pass fills its chunks from offs.
 // ---------------------------------------------------------------------------
-template <bool WRITE, int SLOTS>
+template <bool WRITE, int SLOTS, typename V>
 __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_cols, double pace, uint32_t rbits,
                                                     uint32_t pad, const int64_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
-                                                    const double* __restrict__ vals, uint32_t nw,
+                                                    const V* __restrict__ vals, uint32_t nw,
                                                     uint32_t rpw, uint32_t nb, uint32_t rw, uint32_t pshift,
                                                     int32_t* __restrict__ counts,
                                                     const int64_t* __restrict__ offs,
-                                                    uint32_t* __restrict__ meta, double* __restrict__ val) {
+                                                    uint32_t* __restrict__ meta, V* __restrict__ val) {
     const int lane = threadIdx.x & (WAVE - 1);
     const uint64_t task = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
     if (task >= (uint64_t)nw * nb) return;
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
         }
         if (WRITE && lane >= taken) {  // dummy entries: scratch row rw, X row 0, value 0
             meta[c * CHUNK + lane] = rw;
-            val[c * CHUNK + lane] = 0.0;
+            val[c * CHUNK + lane] = (V)0;
         }
         ++c;
         ++n;
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
     if (WRITE) {
         for (int64_t p = n; p < padded; ++p, ++c) {
             meta[c * CHUNK + lane] = rw;
-            val[c * CHUNK + lane] = 0.0;
+            val[c * CHUNK + lane] = (V)0;
         }
     } else if (lane == 0) {
         counts[task] = (int32_t)padded;
@@ -174,49 +175,66 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
 // ---------------------------------------------------------------------------
 // the SpMM
 // ---------------------------------------------------------------------------
+// T = f64 (the C4 kernel) or f32: an X / Y row of k = 32 is 16 vec2<T>
+// (256 or 128 B), lane q of a 16-lane group holding columns 2q, 2q + 1.
+template <typename T> struct Vec2;
+template <> struct Vec2<double> { using type = double2; };
+template <> struct Vec2<float> { using type = float2; };
+template <typename T> using vec2_t = typename Vec2<T>::type;
+
+template <typename T = double>
 struct Idx {
     uint32_t mi;  // lane 16g+q: entry (quad q, group g) of the chunk
-    double vi;
+    T vi;
 };
-__device__ __forceinline__ void load_idx(Idx& c, const uint32_t* __restrict__ meta, const double* __restrict__ val,
+template <typename T>
+__device__ __forceinline__ void load_idx(Idx<T>& c, const uint32_t* __restrict__ meta, const T* __restrict__ val,
                                          int64_t chunk, int lane) {
     c.mi = meta[chunk * CHUNK + lane];
     c.vi = val[chunk * CHUNK + lane];
 }
-template <int I>
-__device__ __forceinline__ uint32_t bm(const Idx& c) {  // entry (I, g) to every lane of group g
+template <int I, typename T>
+__device__ __forceinline__ uint32_t bm(const Idx<T>& c) {  // entry (I, g) to every lane of group g
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.mi, 0x150 + I, 0xf, 0xf, false);
 }
 template <int I>
-__device__ __forceinline__ double bv(const Idx& c) {
+__device__ __forceinline__ double bv(const Idx<double>& c) {
     return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(c.vi), 0x150 + I, 0xf, 0xf, false),
                             __builtin_amdgcn_update_dpp(0, __double2loint(c.vi), 0x150 + I, 0xf, 0xf, false));
 }
+template <int I>
+__device__ __forceinline__ float bv(const Idx<float>& c) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.vi), 0x150 + I, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double mul_rn(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ double add_rn(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
 // PROBE (measurement only, wrong results): every gather reads X row
 // (col & xmask), e.g. xmask = 0 leaves the index/value stream alone on the
 // memory side (the PMC calibration of its 4-B / 8-B per-lane reads)
-template <bool PROBE, int... I>
-__device__ __forceinline__ void gather(double2 (&x)[16], const Idx& c, const double2* __restrict__ X, int q,
+template <bool PROBE, typename T, int... I>
+__device__ __forceinline__ void gather(vec2_t<T> (&x)[16], const Idx<T>& c, const vec2_t<T>* __restrict__ X, int q,
                                        uint32_t xmask, std::integer_sequence<int, I...>) {
     if (PROBE) ((x[I] = X[(int64_t)((bm<I>(c) >> 8) & xmask) * 16 + q]), ...);
     else ((x[I] = X[(int64_t)(bm<I>(c) >> 8) * 16 + q]), ...);
 }
-template <int I>
-__device__ __forceinline__ double2* yaddr(const Idx& c, double2* yw, int q) {
+template <int I, typename T>
+__device__ __forceinline__ vec2_t<T>* yaddr(const Idx<T>& c, vec2_t<T>* yw, int q) {
     return yw + (bm<I>(c) & 255u) * 16 + q;
 }
-template <int I>
-__device__ __forceinline__ void madd(double2& y, const double2& x, const Idx& c) {
-    const double v = bv<I>(c);
-    y.x = __dadd_rn(y.x, __dmul_rn(v, x.x));
-    y.y = __dadd_rn(y.y, __dmul_rn(v, x.y));
+template <int I, typename T>
+__device__ __forceinline__ void madd(vec2_t<T>& y, const vec2_t<T>& x, const Idx<T>& c) {
+    const T v = bv<I>(c);
+    y.x = add_rn(y.x, mul_rn(v, x.x));
+    y.y = add_rn(y.y, mul_rn(v, x.y));
 }
 // the chunk's rows are distinct (dummies all hit the scratch row): all 16
 // LDS reads, the 32 multiply-adds, all 16 writes
-template <int... I>
-__device__ __forceinline__ void sum_chunk(const double2 (&x)[16], const Idx& c, double2* yw, int q,
+template <typename T, int... I>
+__device__ __forceinline__ void sum_chunk(const vec2_t<T> (&x)[16], const Idx<T>& c, vec2_t<T>* yw, int q,
                                           std::integer_sequence<int, I...>) {
-    double2 y[16];
+    vec2_t<T> y[16];
     ((y[I] = *yaddr<I>(c, yw, q)), ...);
     (madd<I>(y[I], x[I], c), ...);
     ((*yaddr<I>(c, yw, q) = y[I]), ...);
@@ -226,13 +244,13 @@ __device__ __forceinline__ void sum_chunk(const double2 (&x)[16], const Idx& c, 
 // rounded products (ds_add_f64: y + RN(v*x), the same two roundings), no
 // read-back of the rows into registers
 template <int I>
-__device__ __forceinline__ void madd_lds(double2* yp, const double2& x, const Idx& c) {
+__device__ __forceinline__ void madd_lds(double2* yp, const double2& x, const Idx<double>& c) {
     const double v = bv<I>(c);
     __hip_atomic_fetch_add(&yp->x, __dmul_rn(v, x.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_fetch_add(&yp->y, __dmul_rn(v, x.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 template <int... I>
-__device__ __forceinline__ void sum_chunk_lds(const double2 (&x)[16], const Idx& c, double2* yw, int q,
+__device__ __forceinline__ void sum_chunk_lds(const double2 (&x)[16], const Idx<double>& c, double2* yw, int q,
                                               std::integer_sequence<int, I...>) {
     (madd_lds<I>(yaddr<I>(c, yw, q), x[I], c), ...);
 }
@@ -264,16 +282,18 @@ __device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int l
     return false;  // not all resident: stop pacing
 }
 
-template <bool PROBE, bool ATOM>
+template <bool PROBE, bool ATOM, typename T = double>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
-    const uint32_t* __restrict__ meta, const double* __restrict__ val, const double2* __restrict__ X,
-    double2* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask) {
-    extern __shared__ double2 ylds[];
+    const uint32_t* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
+    vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask) {
+    using V2 = vec2_t<T>;
+    extern __shared__ __align__(16) unsigned char ylds_raw[];
+    V2* const ylds = reinterpret_cast<V2*>(ylds_raw);
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = threadIdx.x / WAVE;
     const int g = lane >> 4, q = lane & 15;
-    double2* yw = ylds + (size_t)wave * (rw + 1) * 16;
+    V2* yw = ylds + (size_t)wave * (rw + 1) * 16;
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
     const uint64_t w0 = gw * rpw;
     const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
@@ -287,11 +307,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane);
         const int nr = (int)min<uint64_t>(rw, wend - r0);
-        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = make_double2(0.0, 0.0);
+        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = V2{(T)0, (T)0};
         const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
         if (c1 > c0) {  // (c1 - c0) % PHASES == 0
-            Idx M[6];
-            double2 XS[3][16];
+            Idx<T> M[6];
+            V2 XS[3][16];
 #pragma unroll
             for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
             gather<PROBE>(XS[0], M[0], X, q, xmask, SEQ);
@@ -302,8 +322,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
                     gather<PROBE>(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
-                    if (ATOM) sum_chunk_lds(XS[k % 3], M[k], yw, q, SEQ);
-                    else sum_chunk(XS[k % 3], M[k], yw, q, SEQ);
+                    if constexpr (ATOM) sum_chunk_lds(XS[k % 3], M[k], yw, q, SEQ);
+                    else sum_chunk<T>(XS[k % 3], M[k], yw, q, SEQ);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -311,9 +331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int rb = 0; rb < nr; rb += 4) {  // Y rows and their nonzero counts
             const int r = rb + g;
             const bool live = r < nr;
-            const double2 y = live ? yw[r * 16 + q] : make_double2(0.0, 0.0);
+            const V2 y = live ? yw[r * 16 + q] : V2{(T)0, (T)0};
             if (live) Y[(r0 + r) * 16 + q] = y;
-            const uint64_t m0 = __ballot(y.x != 0.0), m1 = __ballot(y.y != 0.0);
+            const uint64_t m0 = __ballot(y.x != (T)0), m1 = __ballot(y.y != (T)0);
             if (live && q == 0 && row_nnz)
                 row_nnz[r0 + r] = __popcll((m0 >> (16 * g)) & 0xffffull) + __popcll((m1 >> (16 * g)) & 0xffffull);
         }
@@ -336,16 +356,16 @@ constexpr uint32_t HALF_WAVES_PER_CU = 8;
 constexpr uint32_t HALF_RW_MAX = 155;  // 8 waves x (RW+1) rows x 128 B <= 160 KiB of LDS
 
 template <int... I>
-__device__ __forceinline__ void gather_h(double (&x)[16], const Idx& c, const double* __restrict__ Xh, int q,
+__device__ __forceinline__ void gather_h(double (&x)[16], const Idx<double>& c, const double* __restrict__ Xh, int q,
                                          std::integer_sequence<int, I...>) {
     ((x[I] = Xh[(int64_t)(bm<I>(c) >> 8) * 32 + q]), ...);
 }
 template <int I>
-__device__ __forceinline__ void madd_h(double& y, double x, const Idx& c) {
+__device__ __forceinline__ void madd_h(double& y, double x, const Idx<double>& c) {
     y = __dadd_rn(y, __dmul_rn(bv<I>(c), x));
 }
 template <int... I>
-__device__ __forceinline__ void sum_chunk_h(const double (&x)[16], const Idx& c, double* yw, int q,
+__device__ __forceinline__ void sum_chunk_h(const double (&x)[16], const Idx<double>& c, double* yw, int q,
                                             std::integer_sequence<int, I...>) {
     double y[16];
     ((y[I] = yw[(bm<I>(c) & 255u) * 16 + q]), ...);
@@ -381,7 +401,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const double* Xh = X + 16 * h;
         const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
         if (c1 > c0) {  // (c1 - c0) % PHASES == 0
-            Idx M[6];
+            Idx<double> M[6];
             double XS[3][16];
 #pragma unroll
             for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
@@ -429,50 +449,51 @@ constexpr uint32_t K1_RW_MAX = (1u << K1_RBITS) - 1;
 constexpr uint32_t K1_PSHIFT = 18;           // panel = 2^18 columns = 2 MiB of X
 constexpr uint32_t K1_WAVES_PER_CU = 4;      // one workgroup per CU (C2: 59 us against 69 at 12)
 
-template <int ST>
+template <int ST, typename T>
 struct Stage1 {
     uint32_t m[ST];
-    double v[ST];
-    double x[ST];
+    T v[ST];
+    T x[ST];
 };
-template <int ST>
-__device__ __forceinline__ void k1_load(Stage1<ST>& st, const uint32_t* __restrict__ meta,
-                                        const double* __restrict__ val, int64_t c, int lane) {
+template <int ST, typename T>
+__device__ __forceinline__ void k1_load(Stage1<ST, T>& st, const uint32_t* __restrict__ meta,
+                                        const T* __restrict__ val, int64_t c, int lane) {
 #pragma unroll
     for (int j = 0; j < ST; ++j) {
         st.m[j] = meta[(c + j) * CHUNK + lane];
         st.v[j] = val[(c + j) * CHUNK + lane];
     }
 }
-template <int ST>
-__device__ __forceinline__ void k1_gather(Stage1<ST>& st, const double* __restrict__ X, uint32_t xmask) {
+template <int ST, typename T>
+__device__ __forceinline__ void k1_gather(Stage1<ST, T>& st, const T* __restrict__ X, uint32_t xmask) {
 #pragma unroll
     for (int j = 0; j < ST; ++j) st.x[j] = X[(st.m[j] >> K1_RBITS) & xmask];
 }
-template <int ST>
-__device__ __forceinline__ void k1_sum(const Stage1<ST>& st, double* yl) {
+template <int ST, typename T>
+__device__ __forceinline__ void k1_sum(const Stage1<ST, T>& st, T* yl) {
 #pragma unroll
     for (int j = 0; j < ST; ++j) {
-        double* yp = yl + (st.m[j] & K1_RW_MAX);
-        *yp = __dadd_rn(*yp, __dmul_rn(st.v[j], st.x[j]));
+        T* yp = yl + (st.m[j] & K1_RW_MAX);
+        *yp = add_rn(*yp, mul_rn(st.v[j], st.x[j]));
     }
 }
 
-template <int K1_STAGE>
+template <int K1_STAGE, typename T = double>
 __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw,
                                                      const int64_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ meta,
-                                                     const double* __restrict__ val, const double* __restrict__ X,
-                                                     double* __restrict__ Y, int32_t* __restrict__ row_nnz,
+                                                     const T* __restrict__ val, const T* __restrict__ X,
+                                                     T* __restrict__ Y, int32_t* __restrict__ row_nnz,
                                                      unsigned* bar, bool neg_init, uint32_t xmask) {
-    extern __shared__ double y1lds[];
+    extern __shared__ __align__(16) unsigned char y1lds_raw[];
+    T* const y1lds = reinterpret_cast<T*>(y1lds_raw);
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = threadIdx.x / WAVE;
-    double* yl = y1lds + (size_t)wave * (rw + 1);
+    T* yl = y1lds + (size_t)wave * (rw + 1);
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
     const uint64_t w0 = gw * rpw;
     const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
-    const double init = neg_init ? -0.0 : 0.0;
+    const T init = neg_init ? (T)-0.0 : (T)0.0;
     bool sync = bar != nullptr;
     for (uint32_t b = 0; b < nb; ++b) {
         const uint64_t r0 = w0 + (uint64_t)b * rw;
@@ -487,7 +508,7 @@ __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw
         int64_t i = c0;
         if (c1 - c0 >= 3 * K1_STAGE) {  // whole groups of three stages, pipelined
             constexpr int K1_GROUP = 3 * K1_STAGE;
-            Stage1<K1_STAGE> S0, S1, S2;
+            Stage1<K1_STAGE, T> S0, S1, S2;
             k1_load(S0, meta, val, c0, lane);
             k1_load(S1, meta, val, c0 + K1_STAGE, lane);
             k1_gather(S0, X, xmask);
@@ -511,15 +532,15 @@ __global__ __launch_bounds__(256) void spmm_tiled_k1(uint64_t rows, uint32_t rpw
         }
         for (; i < c1; ++i) {  // the task's last chunks, one at a time
             const uint32_t m = meta[i * CHUNK + lane];
-            const double v = val[i * CHUNK + lane];
-            const double xv = X[(m >> K1_RBITS) & xmask];
-            double* yp = yl + (m & K1_RW_MAX);
-            *yp = __dadd_rn(*yp, __dmul_rn(v, xv));
+            const T v = val[i * CHUNK + lane];
+            const T xv = X[(m >> K1_RBITS) & xmask];
+            T* yp = yl + (m & K1_RW_MAX);
+            *yp = add_rn(*yp, mul_rn(v, xv));
         }
         for (int r = lane; r < nr; r += WAVE) {
-            const double y = yl[r];
+            const T y = yl[r];
             Y[r0 + r] = y;
-            if (row_nnz) row_nnz[r0 + r] = y != 0.0 ? 1 : 0;
+            if (row_nnz) row_nnz[r0 + r] = y != (T)0 ? 1 : 0;
         }
         if (sync) batch_arrive(bar, 1, lane);
     }
@@ -537,24 +558,27 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // Both: rows at most a few times their mean length (a long row serialises
 // its chunks, one entry per chunk).
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len) {
-    const bool shape = dtype == BSM_F64 && rows > 0 && nnz > 0 &&
+    const bool shape = (dtype == BSM_F64 || dtype == BSM_F32) && rows > 0 && nnz > 0 &&
                        ((k == 32 && n_cols < (1u << 24)) || (k == 1 && n_cols < (1u << (32 - K1_RBITS))));
     if (const char* e = getenv("BSM_SPMM_TILED")) {
         if (atoi(e) == 0) return false;
         if (atoi(e) == 2) return shape;
     }
     if (!shape) return false;
-    const uint64_t x_bytes = n_cols * k * sizeof(double);
+    const uint64_t x_bytes = n_cols * k * (dtype == BSM_F32 ? 4 : 8);
     if (x_bytes <= (k == 32 ? (1ull << 30) : (4ull << 20))) return false;
     const uint64_t mean = (nnz + rows - 1) / rows;
     return max_row_len <= 2 * mean + 256;
 }
 
-int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
-                 const double* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve,
+int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp, const int32_t* col,
+                 const void* vals, uint64_t k, int flags, bsm_tiled** out, hipStream_t s, uint64_t reserve,
                  PlanTimes* pt) {
     BSM_REQUIRE(out && rp && (nnz == 0 || (col && vals)), BSM_ERR_INVALID, "tiled: null argument");
     BSM_REQUIRE(k == 32 || k == 1, BSM_ERR_UNSUPPORTED, "tiled: k must be 32 or 1");
+    BSM_REQUIRE(dtype == BSM_F64 || dtype == BSM_F32, BSM_ERR_UNSUPPORTED, "tiled: f64 or f32 only");
+    const bool f32 = dtype == BSM_F32;
+    const size_t es = f32 ? 4 : 8;
     const uint32_t rbits = k == 1 ? K1_RBITS : 8;
     BSM_REQUIRE(n_cols < (1ull << (32 - rbits)), BSM_ERR_UNSUPPORTED, "tiled: columns must be < 2^%u",
                 32 - rbits);
@@ -564,12 +588,12 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     int cus = 0;
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     // k = 32: BSM_TILED_HALF=1 selects the two half-width passes (8 waves per CU)
-    const uint32_t half = k == 32 && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
+    const uint32_t half = k == 32 && !f32 && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
     const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : (half ? HALF_WAVES_PER_CU : 4u);
     const uint32_t nw_env = env_u32("BSM_TILED_WAVES", wpc * (uint32_t)cus);
     const uint32_t nw = half ? (nw_env + wpc - 1) / wpc * wpc : nw_env;  // whole workgroups
     const uint32_t k1_stage = env_u32("BSM_TILED_K1_STAGE", K1_STAGE_DEFAULT) == 8 ? 8u : 4u;
-    const uint32_t rw_cap = k == 1 ? K1_RW_MAX : (half ? HALF_RW_MAX : RW_MAX);
+    const uint32_t rw_cap = k == 1 ? K1_RW_MAX : (half ? HALF_RW_MAX : (f32 ? RW_MAX_F32 : RW_MAX));
     uint32_t rw_max = env_u32("BSM_TILED_RW", rw_cap);
     rw_max = rw_max < 8u ? 8u : (rw_max > rw_cap ? rw_cap : rw_max);
     const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", k == 1 ? K1_PSHIFT : PSHIFT);
@@ -588,14 +612,24 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     BSM_TRY(counts.alloc(tasks * sizeof(int32_t)));
     BSM_TRY(offs.alloc((tasks + 1) * sizeof(int64_t)));
     const uint64_t grid = (tasks + 3) / 4;
-    auto layout = [&](auto write_tag, int32_t* cnt, const int64_t* of, uint32_t* me, double* va) -> int {
+    auto layout = [&](auto write_tag, int32_t* cnt, const int64_t* of, uint32_t* me, void* va) -> int {
         constexpr bool W = decltype(write_tag)::value;
-        if (k == 1)
-            tiled_layout<W, (K1_RW_MAX + 1) / WAVE><<<dim3((unsigned)grid), 256, 0, s>>>(
-                rows, n_cols, pace, rbits, pad, rp, col, vals, nw, rpw, nb, rw, pshift, cnt, of, me, va);
-        else
-            tiled_layout<W, 3><<<dim3((unsigned)grid), 256, 0, s>>>(rows, n_cols, pace, rbits, pad, rp, col, vals, nw,
-                                                                  rpw, nb, rw, pshift, cnt, of, me, va);
+        auto go = [&]<typename V>(V*) {
+            if (k == 1)
+                tiled_layout<W, (K1_RW_MAX + 1) / WAVE, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                    rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
+                    cnt, of, me, static_cast<V*>(va));
+            else if (rw_cap > 192)  // f32 batches up to 255 rows: four row slots per lane
+                tiled_layout<W, 4, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                    rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
+                    cnt, of, me, static_cast<V*>(va));
+            else
+                tiled_layout<W, 3, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                    rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
+                    cnt, of, me, static_cast<V*>(va));
+        };
+        if (f32) go((float*)nullptr);
+        else go((double*)nullptr);
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     };
@@ -625,22 +659,23 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     const uint64_t slots = ((uint64_t)total + overread) * CHUNK;
     size_t free_b = 0, total_b = 0;
     BSM_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    BSM_REQUIRE(slots * 12 + (256ull << 20) + reserve < free_b, BSM_ERR_OOM,
-                "tiled: %llu MB stream (+%llu MB reserved) does not fit", (unsigned long long)(slots * 12 >> 20),
+    BSM_REQUIRE(slots * (4 + es) + (256ull << 20) + reserve < free_b, BSM_ERR_OOM,
+                "tiled: %llu MB stream (+%llu MB reserved) does not fit", (unsigned long long)(slots * (4 + es) >> 20),
                 (unsigned long long)(reserve >> 20));
     DBuf meta, val, bar;
     BSM_TRY(bar.alloc(8 * BAR_STRIDE * sizeof(unsigned)));
     BSM_TRY(meta.alloc(slots * sizeof(uint32_t)));
-    BSM_TRY(val.alloc(slots * sizeof(double)));
+    BSM_TRY(val.alloc(slots * es));
     BSM_TRY(phase_end(pt ? &pt->alloc_ms : nullptr));
-    BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.as<uint32_t>(), val.as<double>()));
+    BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.as<uint32_t>(), val.p));
     // over-read padding: valid dummy entries (X row 0)
     BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 4, s));
-    BSM_HIP_TRY(hipMemsetAsync(val.as<double>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 8, s));
+    BSM_HIP_TRY(hipMemsetAsync(static_cast<char*>(val.p) + (uint64_t)total * CHUNK * es, 0, overread * CHUNK * es, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     BSM_TRY(phase_end(pt ? &pt->write_ms : nullptr));
     auto* t = new bsm_tiled;
     t->device = dev;
+    t->dtype = dtype;
     t->k = k;
     t->rows = rows;
     t->n_cols = n_cols;
@@ -656,7 +691,7 @@ int tiled_create(uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp
     t->stage = k1_stage;
     t->offs = static_cast<int64_t*>(offs.release());
     t->meta = static_cast<uint32_t*>(meta.release());
-    t->val = static_cast<double*>(val.release());
+    t->val = val.release();
     t->bar = static_cast<unsigned*>(bar.release());
     *out = t;
     return BSM_OK;
@@ -671,20 +706,31 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         BSM_HIP_TRY(hipMemsetAsync(t->bar, 0, 8 * BAR_STRIDE * sizeof(unsigned), s));
         bar = t->bar;
     }
-    if (t->k == 1) {
+    // BSM_TILED_K1_PROBE=<mask> (measurement only, wrong results): gather
+    // X[col & mask], e.g. 0 (one line: the stream alone) or 4095 (a 32 KB window)
+    static const uint32_t k1mask = env_u32("BSM_TILED_K1_PROBE", 0xffffffffu);
+    if (t->k == 1 && t->dtype == BSM_F32) {
+        const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(float);
+        auto kern = t->stage == 8 ? spmm_tiled_k1<8, float> : spmm_tiled_k1<4, float>;
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
+                                              static_cast<const float*>(t->val), static_cast<const float*>(x),
+                                              static_cast<float*>(y), row_nnz, bar, neg_init, k1mask);
+    } else if (t->k == 1) {
         const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(double);
         auto kern = t->stage == 8 ? spmm_tiled_k1<8> : spmm_tiled_k1<4>;
-        // BSM_TILED_K1_PROBE=<mask> (measurement only, wrong results): gather
-        // X[col & mask], e.g. 0 (one line: the stream alone) or 4095 (a 32 KB window)
-        static const uint32_t xmask = env_u32("BSM_TILED_K1_PROBE", 0xffffffffu);
-        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
-                                              static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar,
-                                              neg_init, xmask);
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
+                                              static_cast<const double*>(t->val), static_cast<const double*>(x),
+                                              static_cast<double*>(y), row_nnz, bar, neg_init, k1mask);
+    } else if (t->dtype == BSM_F32) {  // k = 32, f32: 128-B rows, up to 255 per batch
+        const size_t lds = (size_t)4 * (t->rw + 1) * 128;
+        spmm_tiled_k32<false, false, float><<<dim3(t->nw / 4), 256, lds, s>>>(
+            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, static_cast<const float*>(t->val),
+            static_cast<const float2*>(x), static_cast<float2*>(y), row_nnz, bar, 0xffffffffu);
     } else if (t->half) {
         const size_t lds = (size_t)HALF_WAVES_PER_CU * (t->rw + 1) * 128;
         spmm_tiled_k32h<<<dim3(t->nw / HALF_WAVES_PER_CU), 64 * HALF_WAVES_PER_CU, lds, s>>>(
-            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val, static_cast<const double*>(x),
-            static_cast<double*>(y), row_nnz, bar);
+            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, static_cast<const double*>(t->val),
+            static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
         // BSM_TILED_PROBE_MASK=<mask> (measurement only, wrong results): see gather()
@@ -692,9 +738,9 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         static const bool atom = env_u32("BSM_TILED_LDSADD", 0) == 1;
         auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true, false>
                                          : (atom ? spmm_tiled_k32<false, true> : spmm_tiled_k32<false, false>);
-        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, t->val,
-                                              static_cast<const double2*>(x), static_cast<double2*>(y), row_nnz, bar,
-                                              xmask);
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
+                                              static_cast<const double*>(t->val), static_cast<const double2*>(x),
+                                              static_cast<double2*>(y), row_nnz, bar, xmask);
     }
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;

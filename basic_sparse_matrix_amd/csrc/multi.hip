@@ -464,6 +464,7 @@ int bsm_mcsr_generate(bsm_multi* ctx, int dtype, uint64_t seed, uint64_t rows, u
             BSM_TRY(val.alloc((uint64_t)pn * dtype_size(dtype)));
             (void)hipFree(piece->col);  // csr_alloc's placeholders for nnz = 0
             (void)hipFree(piece->vals);
+            piece->cache_cap[1] = piece->cache_cap[2] = 0;  // plain allocations from here on
             piece->col = col.as<int32_t>();
             col.release();
             piece->vals = val.release();

@@ -66,14 +66,16 @@ ROWLEN_CONST, ROWLEN_BINOMIAL = 0, 2  # bsm_synth.h row-length families
 SEED_A, SEED_X = 1000, 1001
 
 
-def b_alg(rows, n_cols, nnz, k):
-    return 8 * (rows + 1) + 12 * nnz + 8 * n_cols * k + 8 * rows * k
+def b_alg(rows, n_cols, nnz, k, es=8):
+    """SURVEY.md §8d canonical bytes (es = value size: 8 for f64, 4 for f32):
+    8(N+1) + (4 + es) nnz + es n_cols k + es N k."""
+    return 8 * (rows + 1) + (4 + es) * nnz + es * n_cols * k + es * rows * k
 
 
-def b_gather(rows, nnz, k):
+def b_gather(rows, nnz, k, es=8):
     """SURVEY.md §8d traffic model: every nnz gathers its whole X row (no reuse
-    beyond the caches): 8(N+1) + 12 nnz + 8 nnz k + 8 N k."""
-    return 8 * (rows + 1) + 12 * nnz + 8 * nnz * k + 8 * rows * k
+    beyond the caches): 8(N+1) + (4 + es) nnz + es nnz k + es N k."""
+    return 8 * (rows + 1) + (4 + es) * nnz + es * nnz * k + es * rows * k
 
 
 def kernel_label(rows, nnz, k, panel_cols, tiled=False):
@@ -406,6 +408,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--dtype", default="f64", choices=("f64", "f32"),
+                    help="value type of A, X and Y (BASELINE's configs are f64; f32 = the generic-T path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=100_000,
                     help="rows of the CPU baseline sample (configs with more rows are extrapolated)")
@@ -457,9 +461,13 @@ def main():
 
     rows, n_cols, nnz_r, k = CONFIGS[args.config]
     kind, ra, rb = rowlen_spec(args.config)
+    f32 = args.dtype == "f32"
+    np_dt, torch_dt, es = (np.float32, torch.float32, 4) if f32 else (np.float64, torch.float64, 8)
+    if f32 and args.verify:
+        ap.error("--verify compares f64 Y; the f32 path is checked by tests/test_gpu_tiled.py")
     lib0 = _lib.load()
     tiled_shape = args.schedule != "panel" and k in (1, 32) and bool(lib0.bsm_dev_tiled_wanted(
-        _lib.DTYPE_CODES[np.dtype(np.float64)], rows, n_cols, rows * (nnz_r or 1), k, nnz_r or 1))
+        _lib.DTYPE_CODES[np.dtype(np_dt)], rows, n_cols, rows * (nnz_r or 1), k, nnz_r or 1))
     # the tiled copy's persistent grid wants every CU, so by default its rank
     # runs one round and the all-gather follows it (--chunks overrides)
     chunks = args.chunks if args.chunks else (1 if world == 1 or tiled_shape else 4)
@@ -475,7 +483,7 @@ def main():
     comm_init_ms = (time.perf_counter() - t0) * 1e3
 
     t0 = time.perf_counter()
-    m = MultiCsr.generate(ctx, SEED_A, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np.float64, chunks=chunks)
+    m = MultiCsr.generate(ctx, SEED_A, rows, n_cols, kind, ra, rb, _lib.VAL_UNIFORM, np_dt, chunks=chunks)
     gen_ms = (time.perf_counter() - t0) * 1e3
     nnz_total = m.nnz
     bounds = m.bounds()
@@ -483,11 +491,11 @@ def main():
     my_rows = sum(b - a for a, b in my_pieces)
     # the rows' nnz (the generator's row lengths): constant-length configs by count
     my_nnz = my_rows * nnz_r if nnz_r else None
-    x = torch.empty((n_cols, k), dtype=torch.float64, device=dev)
+    x = torch.empty((n_cols, k), dtype=torch_dt, device=dev)
     if rank == 0:
-        x.copy_(gen_dense(SEED_X, 0, n_cols, k, device=dev))
+        x.copy_(gen_dense(SEED_X, 0, n_cols, k, dtype=np_dt, device=dev))
     torch.cuda.synchronize()
-    ctx.broadcast([x.data_ptr()], x.numel() * 8, root=0)  # X replicated over RCCL (untimed setup)
+    ctx.broadcast([x.data_ptr()], x.numel() * es, root=0)  # X replicated over RCCL (untimed setup)
     log(f"rank {rank}: pieces {my_pieces} of {m.pieces} ({chunks} round(s)), nnz {nnz_total:,} in total, generated in "
         f"{gen_ms:.0f} ms; RCCL context {comm_init_ms:.0f} ms")
     # the schedule's per-matrix preparation (outside the timed region, like the
@@ -540,21 +548,21 @@ def main():
         if launched:
             dist.barrier()
     e2e = None
-    if world == 1 and not args.no_e2e:
+    if world == 1 and not args.no_e2e and not f32:
         e2e = end_to_end(args.config, m, x, dev)
         log(f"end to end: {e2e}")
     ms_per_step = elapsed / args.steps * 1e3
-    value = b_alg(rows, n_cols, nnz_total, k) / (elapsed / args.steps) / 1e9
+    value = b_alg(rows, n_cols, nnz_total, k, es) / (elapsed / args.steps) / 1e9
     # roofline of the dominant kernel (the SpMM rounds on the compute stream,
     # bracketed by the library's HIP events): algorithmic bytes of THIS rank's
     # SpMM over its measured average duration
-    b_launch = b_alg(my_rows, n_cols, my_nnz, k)
+    b_launch = b_alg(my_rows, n_cols, my_nnz, k, es)
     t_k = float(np.mean(kern_ms)) / 1e3
     achieved = b_launch / t_k / 1e9
-    achieved_gather = b_gather(my_rows, my_nnz, k) / t_k / 1e9
+    achieved_gather = b_gather(my_rows, my_nnz, k, es) / t_k / 1e9
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not f32:
             log("timing cpu baseline ...")
             cpu = cpu_baseline(args.config, args.cpu_sample_rows)
         traffic, traffic_src, pmc = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None, None
@@ -565,7 +573,7 @@ def main():
             with open(pmc_json) as f:
                 pmc = json.load(f)
             if pmc.get("panel_cols", 0) == panel_cols and pmc.get("schedule", "panel") == (
-                    "tiled" if tiled else "panel"):  # same schedule as this run
+                    "tiled" if tiled else "panel") and not f32:  # same schedule and dtype as this run
                 traffic = pmc["traffic_bytes_per_launch"] * pmc.get("launches_per_spmm", 1)
                 traffic_src = os.path.relpath(pmc_json, ROOT)
             else:
@@ -583,14 +591,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": args.dtype,
             "data": "synthetic (SplitMix64 random CSR, sorted distinct uniform columns, values U[0.5,1.5); "
                     "generated on device from seeds 1000/1001)",
             "config": {
                 "workload": f"{args.config}: {rows:,} x {n_cols:,} CSR, "
                             + (f"{nnz_r} nnz/row" if nnz_r else f"Binomial({n_cols}, {C1_P:g}) nnz/row")
                             + f" ({100.0 * nnz_total / rows / n_cols:.3g} % density, nnz {nnz_total:,}) x {k}-column "
-                              f"dense RHS, f64; step = SpMM rounds + RCCL all-gather of Y + compaction to Csr",
+                              f"dense RHS, {args.dtype}; step = SpMM rounds + RCCL all-gather of Y + compaction to Csr",
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
                 "parallelism": f"row-block x{world}, {chunks} round(s) of {world} nnz-balanced pieces",
                 "comm": comm,
@@ -638,7 +646,7 @@ def main():
                 "peak_source": L2_GATHER_PEAK_SRC,
                 "unit": "GB/s",
                 "frac": round(achieved_gather / L2_GATHER_PEAK_GBS, 5),
-                "bytes_per_launch_gather": b_gather(my_rows, my_nnz, k),
+                "bytes_per_launch_gather": b_gather(my_rows, my_nnz, k, es),
             },
             "end_to_end_ms": e2e,
             "cpu_baseline": cpu,

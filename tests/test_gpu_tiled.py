@@ -238,3 +238,69 @@ def test_tiled_k1_c2_shape(orc):
     sub = (rp[r0:r1 + 1] - rp[r0]).astype(np.uint64)
     erp, eci, ev = orc.mul_dense(r1 - r0, n_cols, sub, ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]], orc.gen_x_cols(1001, n_cols, 1))
     assert np.array_equal(y1[r0:r1, 0].cpu().numpy().view(np.uint64), ev.view(np.uint64))
+
+
+@pytest.mark.parametrize("k,rw", [(32, None), (32, "100"), (1, None)])
+def test_public_mul_dense_tiled_copy_f32(orc, monkeypatch, k, rw):
+    """Csr<f32>.mul_dense on the tiled copy (f32 value stream, 128-B Y rows in
+    LDS, up to 255 rows per batch at k = 32): the oracle's f32 Csr bit for bit
+    (f32 multiply, then f32 add, in storage order), and the same Csr as the
+    one-row-per-wave kernels with the copy off. Some unsorted rows, signed
+    values with exact cancellations, NaN and inf included."""
+    import ctypes
+
+    from basic_sparse_matrix_amd import Csr, Dense
+
+    rng = np.random.default_rng(21 + k)
+    rows, n_cols = 12_000, 50_000
+    lens = rng.integers(150, 250, size=rows)  # even enough for the copy's padding bound
+    lens[::1000] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    # sorted rows, every 50th with its neighbouring entries swapped pairwise:
+    # unsorted (storage-order sums) but in panel order nearly everywhere. The
+    # public path takes the copy only within its padding bound, which fully
+    # shuffled rows exceed (a row stalls on an early high-panel entry); those
+    # are covered through the forced copy, test_tiled_unsorted_rows_keep_storage_order
+    def row_cols(i, n):
+        c = np.sort(rng.choice(n_cols, size=n, replace=False))
+        if i % 50 == 7 and n > 1:
+            m = n - n % 2
+            c[:m] = c[:m].reshape(-1, 2)[:, ::-1].reshape(-1)
+        return c
+
+    ci = np.concatenate([row_cols(i, n) for i, n in enumerate(lens)]).astype(np.uint64)
+    v = rng.standard_normal(int(rp[-1])).astype(np.float32)
+    v[::97] = rng.integers(-3, 4, size=v[::97].size).astype(np.float32)
+    x_cols = [rng.integers(-2, 3, size=n_cols).astype(np.float32) if j % 3 == 0
+              else rng.standard_normal(n_cols).astype(np.float32) for j in range(k)]
+    x_cols[0][5] = np.nan
+    x_cols[-1][9] = np.inf
+    monkeypatch.setenv("BSM_SPMM_TILED", "2")
+    monkeypatch.setenv("BSM_TILED_WAVES", "64")
+    if rw:
+        monkeypatch.setenv("BSM_TILED_RW", rw)
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    got = a.mul_dense(Dense.from_columns(x_cols))
+    used = ctypes.c_int(-1)
+    _lib.check(_lib.load().bsm_csr_tiled(a._device().handle, ctypes.byref(used)))
+    assert used.value == 1
+    erp, eci, ev = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+    assert np.array_equal(np.asarray(got.row_index), erp)
+    assert np.array_equal(np.asarray(got.col_index), eci)
+    assert np.array_equal(np.asarray(got.v).view(np.uint32), ev.view(np.uint32))
+    monkeypatch.setenv("BSM_SPMM_TILED", "0")
+    b = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    ref = b.mul_dense(Dense.from_columns(x_cols))
+    _lib.check(_lib.load().bsm_csr_tiled(b._device().handle, ctypes.byref(used)))
+    assert used.value == 0
+    assert np.array_equal(np.asarray(ref.v).view(np.uint32), ev.view(np.uint32))
+
+
+def test_tiled_wanted_f32_c4_shape():
+    """The library takes the tiled copy for an f32 C4-shaped product (X beyond
+    1 GiB at k = 32), as for f64."""
+    lib = _lib.load()
+    f32, f64 = _lib.DTYPE_CODES[np.dtype(np.float32)], _lib.DTYPE_CODES[np.dtype(np.float64)]
+    assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
+    assert lib.bsm_dev_tiled_wanted(f64, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
+    assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 1 << 24, 10_000_000_000, 32, 1000) == 0  # cols < 2^24
