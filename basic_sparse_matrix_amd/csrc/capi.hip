@@ -174,6 +174,25 @@ int rc_alloc(int dev, size_t n, void** p, size_t* cap) {
     *cap = c;
     return BSM_OK;
 }
+// A result block owned by a call until it is handed to the bsm_csr (error
+// paths hipFree it: that waits for whatever was queued on it)
+struct RcBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    RcBuf() = default;
+    RcBuf(const RcBuf&) = delete;
+    RcBuf& operator=(const RcBuf&) = delete;
+    ~RcBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int alloc(int dev, size_t n) { return rc_alloc(dev, n, &p, &cap); }
+    void* release() {
+        void* q = p;
+        p = nullptr;
+        return q;
+    }
+    template <typename U> U* as() const { return static_cast<U*>(p); }
+};
 // the caller has waited for the device
 void rc_release(int dev, void* p, size_t cap) {
     if (!p) return;
@@ -565,9 +584,10 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     int32_t* const nz = static_cast<int32_t*>(nzp);
     void* const wsp = ws.p ? ws.p : static_cast<char*>(nzp) + nz_al;
     bsm_csr* r = nullptr;
-    // out row_ptr is allocated first (nnz unknown until the scan completes)
-    DBuf out_rp;
-    BSM_TRY(out_rp.alloc((rows + 1) * sizeof(int64_t)));
+    // out row_ptr is allocated first (nnz unknown until the scan completes);
+    // the result's blocks come from the result cache
+    RcBuf out_rp;
+    BSM_TRY(out_rp.alloc(a->device, (rows + 1) * sizeof(int64_t)));
     {
         // one thread at a time builds and launches with the cached plan (a
         // rebuild frees the old plan; hipFree waits for launches using it).
@@ -588,13 +608,16 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     r->device = a->device;
     r->rows = rows;
     r->cols = k;
-    DBuf oc, ov;
-    int rc = oc.alloc(cap * sizeof(int32_t));
-    if (rc == BSM_OK) rc = ov.alloc(cap * es);
+    RcBuf oc, ov;
+    int rc = oc.alloc(a->device, cap * sizeof(int32_t));
+    if (rc == BSM_OK) rc = ov.alloc(a->device, cap * es);
     if (rc != BSM_OK) {
         delete r;
         return rc;
     }
+    r->cache_cap[0] = out_rp.cap;
+    r->cache_cap[1] = oc.cap;
+    r->cache_cap[2] = ov.cap;
     r->row_ptr = static_cast<int64_t*>(out_rp.release());
     r->col = static_cast<int32_t*>(oc.release());
     r->vals = ov.release();
