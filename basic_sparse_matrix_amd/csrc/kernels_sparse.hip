@@ -39,6 +39,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
 
+#include <cstring>
 #include <vector>
 
 #include "bsm_internal.hpp"
@@ -1030,13 +1031,29 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                     for (int64_t b0 = hx[4 * l + 2 * side]; b0 < hx[4 * l + 2 * side + 1]; b0 += LR_CHUNK)
                         hc.push_back({l, side, b0, std::min(b0 + LR_CHUNK, hx[4 * l + 2 * side + 1]), 0});
             const int64_t n_chunks = (int64_t)hc.size();
+            // the host-built chunk list and piece starts go up from pinned
+            // staging (a pageable copy behind running kernels can stall the
+            // host); three regions, all read before the call's last sync
+            const size_t hc_b = (size_t)n_chunks * sizeof(LrChunk), ps_b = (size_t)(n_long + 1) * sizeof(int64_t);
+            const size_t hc_al = (hc_b + 255) & ~size_t(255);
+            char* pin = static_cast<char*>(pinned(2 * hc_al + ps_b));
+            auto h2d = [&](void* dst, const void* src, size_t bytes, size_t off) -> int {
+                if (!bytes) return BSM_OK;
+                if (pin) {
+                    std::memcpy(pin + off, src, bytes);
+                    BSM_HIP_TRY(hipMemcpyAsync(dst, pin + off, bytes, hipMemcpyHostToDevice, s));
+                } else {
+                    BSM_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+                }
+                return BSM_OK;
+            };
             DBuf chunks, ccnt;
             BSM_TRY(chunks.alloc((n_chunks ? n_chunks : 1) * sizeof(LrChunk), s));
             BSM_TRY(ccnt.alloc((n_chunks ? n_chunks : 1) * sizeof(int64_t), s));
             BSM_HIP_TRY(hipMemsetAsync(mval.p, 0xff, n_long * sizeof(int32_t), s));  // -1
             std::vector<int64_t> hcnt(n_chunks);
             if (n_chunks) {
-                BSM_HIP_TRY(hipMemcpyAsync(chunks.p, hc.data(), n_chunks * sizeof(LrChunk), hipMemcpyHostToDevice, s));
+                BSM_TRY(h2d(chunks.p, hc.data(), hc_b, 0));
                 chunk_reduce<true><<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col,
                                                                       mval.as<int32_t>(), nullptr);
                 chunk_reduce<false><<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col,
@@ -1063,7 +1080,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                 fprintf(stderr, "[bsm ss debug] long rows %lld, chunks %lld, pieces %lld\n", (long long)n_long,
                         (long long)n_chunks, (long long)n_pieces);
             }
-            BSM_HIP_TRY(hipMemcpyAsync(pstart.p, ps.data(), (n_long + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            BSM_TRY(h2d(pstart.p, ps.data(), ps_b, 2 * hc_al));
             BSM_TRY(pieces.alloc(n_pieces * sizeof(Piece), s));
             BSM_TRY(pcnt.alloc(n_pieces * sizeof(int32_t), s));
             BSM_TRY(poff.alloc((n_pieces + 1) * sizeof(int64_t), s));
@@ -1073,7 +1090,7 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                                                              pstart.as<int64_t>(), pieces.as<Piece>(),
                                                              first.as<int64_t>());
             if (n_chunks) {
-                BSM_HIP_TRY(hipMemcpyAsync(chunks.p, hc.data(), n_chunks * sizeof(LrChunk), hipMemcpyHostToDevice, s));
+                BSM_TRY(h2d(chunks.p, hc.data(), hc_b, hc_al));
                 chunk_pieces<<<(unsigned)n_chunks, 256, 0, s>>>(chunks.as<LrChunk>(), a->col, b->col, mval.as<int32_t>(),
                                                                 pstart.as<int64_t>(), pieces.as<Piece>());
             }

@@ -135,6 +135,30 @@ __global__ __launch_bounds__(SCAN_BLOCK) void scan_apply(const int32_t* in, uint
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = tile_prefix[gridDim.x];
 }
 
+// n <= SCAN_TILE (the small calls: C1's 1,024 rows): the whole scan in one
+// launch instead of three
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_one_tile(const int32_t* in, uint64_t n, int64_t* out) {
+    __shared__ int64_t smem[SCAN_BLOCK];
+    int32_t v[SCAN_ITEMS];
+    int64_t local = 0;
+    const uint64_t my0 = (uint64_t)threadIdx.x * SCAN_ITEMS;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const uint64_t idx = my0 + i;
+        v[i] = idx < n ? in[idx] : 0;
+        local += v[i];
+    }
+    int64_t total;
+    int64_t ex = block_exclusive_scan(local, smem, &total);
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const uint64_t idx = my0 + i;
+        if (idx < n) out[idx] = ex;
+        ex += v[i];
+    }
+    if (threadIdx.x == 0) out[n] = total;
+}
+
 __global__ void write_zero_i64(int64_t* p) { *p = 0; }
 
 // ---------------------------------------------------------------------------
@@ -900,6 +924,11 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
                 "scan workspace too small (%llu < %llu)", (unsigned long long)ws_bytes,
                 (unsigned long long)scan_workspace_bytes(n));
     BSM_REQUIRE(tiles < (1ull << 31), BSM_ERR_UNSUPPORTED, "scan too large");
+    if (tiles == 1) {
+        scan_one_tile<<<1, SCAN_BLOCK, 0, s>>>(in, n, out);
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    }
     int64_t* tile_sums = static_cast<int64_t*>(ws);
     scan_tile_sums<<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, tile_sums);
     scan_tile_prefix<<<1, SCAN_BLOCK, 0, s>>>(tile_sums, tiles);

@@ -269,8 +269,8 @@ __device__ __forceinline__ void batch_arrive(unsigned* bar, uint32_t n, int lane
     if (lane == 0) __hip_atomic_fetch_add(bar + (blockIdx.x & 7) * BAR_STRIDE, n, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int lane) {
-    for (int spin = 0; spin < 4000; ++spin) {
+__device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int lane, uint32_t spins = 4000) {
+    for (uint32_t spin = 0; spin < spins; ++spin) {
         uint32_t v = lane < 8 ? __hip_atomic_load(bar + lane * BAR_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : 0u;
         v += (uint32_t)__shfl_xor((int)v, 1);
@@ -286,7 +286,7 @@ template <bool PROBE, bool ATOM, typename T = double>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const uint32_t* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
-    vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask) {
+    vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
     using V2 = vec2_t<T>;
     extern __shared__ __align__(16) unsigned char ylds_raw[];
     V2* const ylds = reinterpret_cast<V2*>(ylds_raw);
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if (sync) batch_arrive(bar, nb - b, lane);
             break;
         }
-        if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane);
+        if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane, spins);
         const int nr = (int)min<uint64_t>(rw, wend - r0);
         for (int r = g; r < nr; r += 4) yw[r * 16 + q] = V2{(T)0, (T)0};
         const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
@@ -723,9 +723,12 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
                                               static_cast<double*>(y), row_nnz, bar, neg_init, k1mask);
     } else if (t->dtype == BSM_F32) {  // k = 32, f32: 128-B rows, up to 255 per batch
         const size_t lds = (size_t)4 * (t->rw + 1) * 128;
+        // BSM_TILED_SPINS: the batch barrier's poll bound (default 4000 polls
+        // of s_sleep 8, ~0.9 ms; A/B for the f32 batches, ~3x longer)
+        static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
         spmm_tiled_k32<false, false, float><<<dim3(t->nw / 4), 256, lds, s>>>(
             t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, static_cast<const float*>(t->val),
-            static_cast<const float2*>(x), static_cast<float2*>(y), row_nnz, bar, 0xffffffffu);
+            static_cast<const float2*>(x), static_cast<float2*>(y), row_nnz, bar, 0xffffffffu, spins);
     } else if (t->half) {
         const size_t lds = (size_t)HALF_WAVES_PER_CU * (t->rw + 1) * 128;
         spmm_tiled_k32h<<<dim3(t->nw / HALF_WAVES_PER_CU), 64 * HALF_WAVES_PER_CU, lds, s>>>(
@@ -738,9 +741,10 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         static const bool atom = env_u32("BSM_TILED_LDSADD", 0) == 1;
         auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true, false>
                                          : (atom ? spmm_tiled_k32<false, true> : spmm_tiled_k32<false, false>);
+        static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
         kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
                                               static_cast<const double*>(t->val), static_cast<const double2*>(x),
-                                              static_cast<double2*>(y), row_nnz, bar, xmask);
+                                              static_cast<double2*>(y), row_nnz, bar, xmask, spins);
     }
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
