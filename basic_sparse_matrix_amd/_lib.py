@@ -89,6 +89,8 @@ SIGNATURES = [
     ("bsm_csr_from_coo", _int, [_int, _u64, _u64, _u64, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     ("bsm_csr_shape", _int, [_vp, _u64p, _u64p, _u64p, ctypes.POINTER(_int)]),
     ("bsm_csr_download", _int, [_vp, _vp, _vp, _vp]),
+    ("bsm_host_register", _int, [_vp, _u64]),
+    ("bsm_host_unregister", _int, [_vp]),
     ("bsm_csr_free", None, [_vp]),
     ("bsm_csr_mul_dense", _int, [_vp, _u64, _u64, _pp, ctypes.POINTER(_vp)]),
     ("bsm_csr_mul_vector", _int, [_vp, _vp, _u64, _vp, _u64]),

@@ -258,6 +258,9 @@ int h2d_staged(void* dst, const void* src, size_t bytes, hipStream_t s);
 int d2h_staged(void* dst, const void* src, size_t bytes, hipStream_t s);
 int h2d_cols_narrow(int32_t* dst, const uint64_t* src, uint64_t n, uint64_t cols, uint64_t* bad, hipStream_t s);
 int h2d_row_ptr(int64_t* dst, const uint64_t* src, uint64_t n, uint64_t base, hipStream_t s);
+bool host_registered(const void* p);
+int d2h_csr_direct(const int64_t* rp, const int32_t* col, const void* vals, uint64_t rows, uint64_t nnz, size_t es,
+                   uint64_t* row_ptr, uint64_t* col_idx, void* vals_out, hipStream_t s);
 int d2h_cols_widen(uint64_t* dst, const int32_t* src, uint64_t n, hipStream_t s);
 
 // kernels (kernels_*.hip), all async on stream s

@@ -772,6 +772,11 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     BSM_TRY(ctx_stream(&s));
     const size_t es = dtype_size(m->dtype);
     const size_t rp_b = (m->rows + 1) * sizeof(int64_t), col_b = m->nnz * sizeof(int32_t), val_b = m->nnz * es;
+    // page-locked destinations (bsm_host_register): direct DMA, no host copies
+    // (row_ptr may be a small pageable array: its copy is tiny either way)
+    if (m->nnz >= 4096 && (col_idx || vals) && (!col_idx || host_registered(col_idx)) &&
+        (!vals || host_registered(vals)))
+        return d2h_csr_direct(m->row_ptr, m->col, m->vals, m->rows, m->nnz, es, row_ptr, col_idx, vals, s);
     char* pin = rp_b + col_b + val_b <= PIN_MAX ? static_cast<char*>(pinned(rp_b + col_b + val_b)) : nullptr;
     if (!pin) {  // large: staged pipelines, columns widened to usize on the device
         if (row_ptr) BSM_TRY(d2h_staged(row_ptr, m->row_ptr, rp_b, s));  // int64 >= 0: the same bits as u64
@@ -794,6 +799,18 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     if (col_idx)
         for (uint64_t e = 0; e < m->nnz; ++e) col_idx[e] = (uint64_t)c32[e];
     if (vals && val_b) std::memcpy(vals, vdst, val_b);
+    return BSM_OK;
+}
+
+int bsm_host_register(void* p, uint64_t bytes) {
+    BSM_REQUIRE(p && bytes, BSM_ERR_INVALID, "null or empty range");
+    BSM_HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return BSM_OK;
+}
+
+int bsm_host_unregister(void* p) {
+    BSM_REQUIRE(p, BSM_ERR_INVALID, "null pointer");
+    BSM_HIP_TRY(hipHostUnregister(p));
     return BSM_OK;
 }
 

@@ -526,12 +526,27 @@ __device__ __forceinline__ int64_t lower_bound_wave(const S& sd, int64_t e0, int
     return bal ? lo + __builtin_ctzll(bal) : hi;
 }
 
-template <typename T, bool SUB>
+// PRESPLIT (a first pass over the long rows' pieces): only cuts, the largest
+// sub-piece first, at most PRE_CUTS per piece and none below PRE_MIN
+// entries; the sub-pieces left go out as pieces of their own (out, *n_out),
+// which the second pass (the full piece_split, its grid bounded by *n_in)
+// takes one workgroup each. A piece's sub-pieces are independent (each
+// writes from its own scratch position a0 + b0), so the longest piece's
+// serial cut chain, which sets the kernel's time, is spread over up to
+// PRE_CUTS + 1 workgroups. Same leaves, same outputs, same positions.
+constexpr int PRE_CUTS = 7;
+constexpr int64_t PRE_MIN = 512;
+
+template <typename T, bool SUB, bool PRESPLIT = false>
 __global__ __launch_bounds__(64) void piece_split(const Piece* __restrict__ pieces, const int32_t* __restrict__ acol,
                                                   const T* __restrict__ av, const int32_t* __restrict__ bcol,
                                                   const T* __restrict__ bv, int32_t* __restrict__ tcol,
-                                                  T* __restrict__ tval, unsigned long long* __restrict__ sdbg) {
+                                                  T* __restrict__ tval, unsigned long long* __restrict__ sdbg,
+                                                  const unsigned* __restrict__ n_in = nullptr,
+                                                  Piece* __restrict__ out = nullptr,
+                                                  unsigned* __restrict__ n_out = nullptr) {
     using A = Arith<T>;
+    if (n_in && blockIdx.x >= *n_in) return;  // the second pass's grid is an upper bound
     // BSM_SS_DEBUG=4: cycles per piece (total, cut scans, leaf merges, one-sided
     // copies, staging), entries scanned, flushes, leaves, the piece's size
     long long k_cut = 0, k_flush = 0, k_bulk = 0, k_stage = 0, n_scan = 0, n_flush = 0, n_leaf = 0;
@@ -634,6 +649,99 @@ __global__ __launch_bounds__(64) void piece_split(const Piece* __restrict__ piec
     // descending rows) stop being cut after ~32 passes over the piece and
     // merge as they stand, one lane per piece
     int64_t budget = 32 * ((pc.a1 - pc.a0) + (pc.b1 - pc.b0)) + 4096;
+    auto cut_piece = [&](const SubPiece& x, int64_t na, int64_t nb) {
+        budget -= na + nb;
+        const long long kc0 = sdbg ? clock64() : 0;
+        n_scan += na + nb;
+        // the piece's largest column, and whether both sides are sorted
+        int mx = -1;
+        bool srt = true;
+        auto scan_side = [&](const SideView<T>& sd, int64_t e0, int64_t e1) {
+            for (int64_t base = e0; base < e1; base += 8 * 64) {  // eight windows' loads in flight
+                int32_t c[8], n[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t e = base + 64 * u + lane;
+                    c[u] = e < e1 ? sd.col(e) : -1;
+                    n[u] = e + 1 < e1 ? sd.col(e + 1) : 0x7fffffff;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    mx = max(mx, c[u]);
+                    srt = srt && c[u] <= n[u];
+                }
+            }
+        };
+        scan_side(SA, x.a0, x.a1);
+        scan_side(SB, x.b0, x.b1);
+        mx = wave_max_i32(mx);
+        if (__ballot(!srt) == 0) {
+            // sorted sides (the cut at the maximum would peel one pair off the
+            // end): cut by value at the longer side's median v. Everything
+            // below v merges first, on both sides, then the rest.
+            const int32_t v = na >= nb ? SA.col(x.a0 + na / 2) : SB.col(x.b0 + nb / 2);
+            int64_t qa = lower_bound_wave(SA, x.a0, x.a1, v, lane), qb = lower_bound_wave(SB, x.b0, x.b1, v, lane);
+            if (qa == x.a0 && qb == x.b0 && v < 0x7fffffff) {  // nothing below v: cut above it
+                qa = lower_bound_wave(SA, x.a0, x.a1, v + 1, lane);
+                qb = lower_bound_wave(SB, x.b0, x.b1, v + 1, lane);
+            }
+            if (!(qa == x.a0 && qb == x.b0) && !(qa == x.a1 && qb == x.b1)) {
+                if (sdbg) k_cut += clock64() - kc0;
+                push({qa, x.a1, qb, x.b1, x.pa, x.pb});
+                push({x.a0, qa, x.b0, qb, -1, -1});
+                return;
+            }
+        }
+        // the first occurrence of the maximum on each side
+        const int64_t qa = first_eq(SA, x.a0, x.a1, mx, lane), qb = first_eq(SB, x.b0, x.b1, mx, lane);
+        if (sdbg) k_cut += clock64() - kc0;
+        if (qa < x.a1 && qb < x.b1) {  // the first pair of m splits the piece
+            push({qa + 1, x.a1, qb + 1, x.b1, x.pa, x.pb});
+            push({x.a0, qa, x.b0, qb, qa, qb});
+        } else if (qa < x.a1) {  // only self holds m: merge up to it, then self alone
+            push({qa, x.a1, x.b1, x.b1, x.pa, x.pb});
+            push({x.a0, qa, x.b0, x.b1, -1, -1});
+        } else {  // only rhs holds m
+            push({x.a1, x.a1, qb, x.b1, x.pa, x.pb});
+            push({x.a0, x.a1, x.b0, qb, -1, -1});
+        }
+    };
+    if constexpr (PRESPLIT) {
+        for (int cuts = 0; cuts < PRE_CUTS && sp > 0; ++cuts) {
+            // the largest sub-piece on the stack to the top
+            const int64_t sz = lane < sp ? (stk.a1 - stk.a0) + (stk.b1 - stk.b0) : -1;
+            int64_t best = sz;
+            int bl = lane;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t ob = __shfl_xor(best, off, 64);
+                const int ol = __shfl_xor(bl, off, 64);
+                if (ob > best || (ob == best && ol < bl)) {
+                    best = ob;
+                    bl = ol;
+                }
+            }
+            bl = __builtin_amdgcn_readfirstlane(bl);
+            const SubPiece x = sp_read(stk, bl);
+            const int64_t na = x.a1 - x.a0, nb = x.b1 - x.b0;
+            if (na + nb <= PRE_MIN || na == 0 || nb == 0) break;  // nothing left worth a workgroup
+            const SubPiece top = sp_read(stk, sp - 1);
+            if (lane == bl) stk = top;
+            --sp;
+            // the top piece, when it fits, is staged with its whole subtree (every
+            // later sub-piece lies inside it); a later one is never staged here,
+            // the stack holding entries outside it
+            if (!staged && sp == 0 && na + (x.pa >= 0 ? 1 : 0) <= SPLIT_CAP && nb + (x.pb >= 0 ? 1 : 0) <= SPLIT_CAP)
+                stage_piece(x);
+            cut_piece(x, na, nb);
+        }
+        // every sub-piece left becomes a piece of the second pass
+        unsigned base = 0;
+        if (lane == 0 && sp > 0) base = atomicAdd(n_out, (unsigned)sp);
+        base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);
+        if (lane < sp) out[base + lane] = Piece{stk.a0, stk.a1, stk.b0, stk.b1, stk.pa, stk.pb, pc.row};
+        return;
+    }
     while (sp > 0) {
         if (staged && sp == sp_base) {  // the staged subtree is done: its leaves first
             flush();
@@ -688,61 +796,7 @@ __global__ __launch_bounds__(64) void piece_split(const Piece* __restrict__ piec
             if (sdbg) k_bulk += clock64() - kb0;
             continue;
         }
-        budget -= na + nb;
-        const long long kc0 = sdbg ? clock64() : 0;
-        n_scan += na + nb;
-        // the piece's largest column, and whether both sides are sorted
-        int mx = -1;
-        bool srt = true;
-        auto scan_side = [&](const SideView<T>& sd, int64_t e0, int64_t e1) {
-            for (int64_t base = e0; base < e1; base += 8 * 64) {  // eight windows' loads in flight
-                int32_t c[8], n[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int64_t e = base + 64 * u + lane;
-                    c[u] = e < e1 ? sd.col(e) : -1;
-                    n[u] = e + 1 < e1 ? sd.col(e + 1) : 0x7fffffff;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    mx = max(mx, c[u]);
-                    srt = srt && c[u] <= n[u];
-                }
-            }
-        };
-        scan_side(SA, x.a0, x.a1);
-        scan_side(SB, x.b0, x.b1);
-        mx = wave_max_i32(mx);
-        if (__ballot(!srt) == 0) {
-            // sorted sides (the cut at the maximum would peel one pair off the
-            // end): cut by value at the longer side's median v. Everything
-            // below v merges first, on both sides, then the rest.
-            const int32_t v = na >= nb ? SA.col(x.a0 + na / 2) : SB.col(x.b0 + nb / 2);
-            int64_t qa = lower_bound_wave(SA, x.a0, x.a1, v, lane), qb = lower_bound_wave(SB, x.b0, x.b1, v, lane);
-            if (qa == x.a0 && qb == x.b0 && v < 0x7fffffff) {  // nothing below v: cut above it
-                qa = lower_bound_wave(SA, x.a0, x.a1, v + 1, lane);
-                qb = lower_bound_wave(SB, x.b0, x.b1, v + 1, lane);
-            }
-            if (!(qa == x.a0 && qb == x.b0) && !(qa == x.a1 && qb == x.b1)) {
-                if (sdbg) k_cut += clock64() - kc0;
-                push({qa, x.a1, qb, x.b1, x.pa, x.pb});
-                push({x.a0, qa, x.b0, qb, -1, -1});
-                continue;
-            }
-        }
-        // the first occurrence of the maximum on each side
-        const int64_t qa = first_eq(SA, x.a0, x.a1, mx, lane), qb = first_eq(SB, x.b0, x.b1, mx, lane);
-        if (sdbg) k_cut += clock64() - kc0;
-        if (qa < x.a1 && qb < x.b1) {  // the first pair of m splits the piece
-            push({qa + 1, x.a1, qb + 1, x.b1, x.pa, x.pb});
-            push({x.a0, qa, x.b0, qb, qa, qb});
-        } else if (qa < x.a1) {  // only self holds m: merge up to it, then self alone
-            push({qa, x.a1, x.b1, x.b1, x.pa, x.pb});
-            push({x.a0, qa, x.b0, x.b1, -1, -1});
-        } else {  // only rhs holds m
-            push({x.a1, x.a1, qb, x.b1, x.pa, x.pb});
-            push({x.a0, x.a1, x.b0, qb, -1, -1});
-        }
+        cut_piece(x, na, nb);
     }
     if (nl) flush();
     if (sdbg && lane == 0) {
@@ -1111,9 +1165,30 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
                     BSM_TRY(sdbg.alloc(9 * n_pieces * sizeof(unsigned long long), s));
                     BSM_HIP_TRY(hipMemsetAsync(sdbg.p, 0, 9 * n_pieces * sizeof(unsigned long long), s));
                 }
-                piece_split<T, SUB><<<(unsigned)n_pieces, 64, 2 * split_cap<T>() * (sizeof(int32_t) + sizeof(T)), s>>>(
-                    pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(),
-                    sdbg.as<unsigned long long>());
+                const size_t split_lds = 2 * split_cap<T>() * (sizeof(int32_t) + sizeof(T));
+                // BSM_SS_PRESPLIT=1 (A/B; off by default, and under BSM_SS_DEBUG=4,
+                // whose stamps are per top piece): a cuts-only pass first spreads
+                // every piece over up to PRE_CUTS + 1 workgroups of the full pass.
+                // Within +-5 % of the single pass at the benches' sizes
+                // (profiles/r03_s2h_*), so the single pass stays the default.
+                static const bool presplit = getenv("BSM_SS_PRESPLIT") && atoi(getenv("BSM_SS_PRESPLIT")) != 0;
+                if (presplit && !sdbg.p && (uint64_t)n_pieces * (PRE_CUTS + 1) < (1ull << 31)) {
+                    const int64_t n2 = n_pieces * (PRE_CUTS + 1);
+                    DBuf pieces2, cnt2;
+                    BSM_TRY(pieces2.alloc(n2 * sizeof(Piece), s));
+                    BSM_TRY(cnt2.alloc(sizeof(unsigned), s));
+                    BSM_HIP_TRY(hipMemsetAsync(cnt2.p, 0, sizeof(unsigned), s));
+                    piece_split<T, SUB, true><<<(unsigned)n_pieces, 64, split_lds, s>>>(
+                        pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(), nullptr, nullptr,
+                        pieces2.as<Piece>(), cnt2.as<unsigned>());
+                    piece_split<T, SUB><<<(unsigned)n2, 64, split_lds, s>>>(
+                        pieces2.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(), nullptr,
+                        cnt2.as<unsigned>());
+                } else {
+                    piece_split<T, SUB><<<(unsigned)n_pieces, 64, split_lds, s>>>(
+                        pieces.as<Piece>(), a->col, av, b->col, bv, tcol.as<int32_t>(), tval.as<T>(),
+                        sdbg.as<unsigned long long>());
+                }
                 pos_flags<<<grid_of((uint64_t)n_slots), 256, 0, s>>>(n_slots, tcol.as<int32_t>(), scnt.as<int32_t>());
                 if (sdbg.p) {
                     std::vector<unsigned long long> h(9 * n_pieces);

@@ -342,6 +342,33 @@ int h2d_row_ptr(int64_t* dst, const uint64_t* src, uint64_t n, uint64_t base, hi
 }
 
 // Device int32 column indices -> host usize, widened on the device.
+// Device -> page-locked host memory (registered or hipHostMalloc'd, e.g. the
+// Python mirror's host result pool): the DMA writes the caller's arrays
+// directly, the columns widened on the device first; one sync.
+bool host_registered(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // plain pageable memory
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+int d2h_csr_direct(const int64_t* rp, const int32_t* col, const void* vals, uint64_t rows, uint64_t nnz, size_t es,
+                   uint64_t* row_ptr, uint64_t* col_idx, void* vals_out, hipStream_t s) {
+    DBuf wide;
+    if (col_idx && nnz) {
+        BSM_TRY(wide.alloc(nnz * 8, s));
+        widen_i32_u64<<<blocks(nnz), 256, 0, s>>>(col, wide.as<uint64_t>(), nnz);
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    if (row_ptr) BSM_HIP_TRY(hipMemcpyAsync(row_ptr, rp, (rows + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (col_idx && nnz) BSM_HIP_TRY(hipMemcpyAsync(col_idx, wide.p, nnz * 8, hipMemcpyDeviceToHost, s));
+    if (vals_out && nnz) BSM_HIP_TRY(hipMemcpyAsync(vals_out, vals, nnz * es, hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    return BSM_OK;
+}
+
 int d2h_cols_widen(uint64_t* dst, const int32_t* src, uint64_t n, hipStream_t s) {
     if (n == 0) return BSM_OK;
     DBuf dstage;

@@ -32,8 +32,22 @@ _HUGE = 2 << 20
 _MIN_POOLED = 1 << 20  # below this numpy's allocator is cheap enough
 
 
+def _register(addr: int, nbytes: int) -> bool:
+    """Page-lock [addr, addr + nbytes) for direct DMA (bsm_host_register)
+    when the library and a device are there; the pool works without it."""
+    if os.environ.get("BSM_HOST_POOL_REGISTER", "1") == "0":
+        return False
+    try:
+        from . import _lib
+
+        lib = _lib.require_device()
+        return lib.bsm_host_register(ctypes.c_void_p(addr), nbytes) == _lib.BSM_OK
+    except Exception:  # no library / device: plain pageable pages
+        return False
+
+
 class _Mapping:
-    __slots__ = ("mm", "base", "cap")
+    __slots__ = ("mm", "base", "cap", "addr", "registered", "__weakref__")
 
     def __init__(self, cap: int):
         # one extra huge page so the usable range can start 2 MiB aligned
@@ -41,11 +55,27 @@ class _Mapping:
         addr = ctypes.addressof(ctypes.c_char.from_buffer(self.mm))
         self.base = (-addr) % _HUGE
         self.cap = cap
+        self.addr = addr + self.base
         if hasattr(mmap, "MADV_HUGEPAGE"):
             try:
                 self.mm.madvise(mmap.MADV_HUGEPAGE)
             except OSError:
                 pass
+        # page-locked once for the mapping's life: every download into it is
+        # then one direct DMA (and its pages are faulted in here, once)
+        self.registered = _register(self.addr, cap)
+        if self.registered:
+            weakref.finalize(self, _unregister, self.addr)
+
+
+def _unregister(addr: int) -> None:
+    try:
+        from . import _lib
+
+        if _lib._lib is not None:
+            _lib._lib.bsm_host_unregister(ctypes.c_void_p(addr))
+    except Exception:
+        pass
 
 
 class HostPool:

@@ -114,6 +114,14 @@ int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nn
                   int* dtype);
 /* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz). */
 int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, void* vals);
+/* Page-lock (hipHostRegister) / release a caller-owned host range that result
+ * arrays are downloaded into again and again (this build's addition; no
+ * reference counterpart). bsm_csr_download into registered arrays is one
+ * direct DMA per array, the columns widened to usize on the device; into
+ * pageable arrays it stages through pinned buffers. The Python mirror's host
+ * result pool (hostpool.py) registers its mappings once. */
+int bsm_host_register(void* p, uint64_t bytes);
+int bsm_host_unregister(void* p);
 void bsm_csr_free(bsm_csr* m);
 
 /* ---- hot path (host buffers in/out, synchronous) ------------------------- */

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session: scripts/gpu_session.sh TAG STEP...
 # STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>[:extra]
-#       | pmc:<config>:<COUNTER>[:extra] | c5 | gather | torchrun:<config>[:extra]
+#       | pmc:<config>:<COUNTER[,COUNTER...]>[:extra] | c5 | gather | torchrun:<config>[:extra]
 #       | py:<script args> | profpy:<name>:<script args> (the script under rocprofv3 --kernel-trace --stats)
 #       | env:VAR=VALUE (for the later steps) | unenv:VAR
 # Every step runs under its own time limit; the session stops at the first
@@ -35,8 +35,9 @@ for step in "$@"; do
     prof:*) IFS=: read -r _ cfg extra <<< "$step"
             run prof_$cfg 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${cfg}_$TAG -o run \
                 --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e $extra || exit $? ;;
-    pmc:*) IFS=: read -r _ cfg ctr extra <<< "$step"
-           run pmc_${cfg}_${ctr} 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${cfg}_${ctr}_$TAG -o run \
+    pmc:*) IFS=: read -r _ cfg ctr extra <<< "$step"  # counters joined by ',' (one pass)
+           cn=${ctr//,/_}
+           run pmc_${cfg}_${cn} 300 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_${cfg}_${cn}_$TAG -o run \
                --output-format csv -- python bench.py --config $cfg --steps 2 --warmup 0 --no-cpu-baseline \
                --no-e2e $extra || exit $? ;;
     gather) run gather 300 bash scripts/perf/gather_ceiling.sh || exit $? ;;
