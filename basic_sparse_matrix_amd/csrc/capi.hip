@@ -774,7 +774,8 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     const size_t rp_b = (m->rows + 1) * sizeof(int64_t), col_b = m->nnz * sizeof(int32_t), val_b = m->nnz * es;
     // page-locked destinations (bsm_host_register): direct DMA, no host copies
     // (row_ptr may be a small pageable array: its copy is tiny either way)
-    if (m->nnz >= 4096 && (col_idx || vals) && (!col_idx || host_registered(col_idx)) &&
+    // (up to 128M entries: the widened columns need an nnz x 8 B device temporary)
+    if (m->nnz >= 4096 && m->nnz <= (128ull << 20) && (col_idx || vals) && (!col_idx || host_registered(col_idx)) &&
         (!vals || host_registered(vals)))
         return d2h_csr_direct(m->row_ptr, m->col, m->vals, m->rows, m->nnz, es, row_ptr, col_idx, vals, s);
     char* pin = rp_b + col_b + val_b <= PIN_MAX ? static_cast<char*>(pinned(rp_b + col_b + val_b)) : nullptr;
