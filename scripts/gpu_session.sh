@@ -37,6 +37,7 @@ for step in "$@"; do
                 --output-format csv -- python bench.py --config $cfg --no-cpu-baseline --no-e2e $extra || exit $? ;;
     pmc:*) IFS=: read -r _ cfg ctr extra <<< "$step"  # counters joined by ',' (one pass)
            cn=${ctr//,/_}
+           [ -n "$extra" ] && cn="${cn}_$(echo "$extra" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)"
            run pmc_${cfg}_${cn} 300 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_${cfg}_${cn}_$TAG -o run \
                --output-format csv -- python bench.py --config $cfg --steps 2 --warmup 0 --no-cpu-baseline \
                --no-e2e $extra || exit $? ;;
