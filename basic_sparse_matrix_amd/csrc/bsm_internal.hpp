@@ -194,7 +194,8 @@ struct bsm_tiled {
     uint32_t half = 0;           // k = 32: 1 = two half-width passes, 8 waves per CU (spmm_tiled_k32h)
     uint64_t chunks = 0;         // total, without the over-read padding
     int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
-    uint32_t* meta = nullptr;    // (chunks + overread) * 64
+    void* meta = nullptr;        // (chunks + overread) * 64 meta words (col << 8 | row, or col << 11 | row at k = 1)
+    uint32_t meta_bytes = 4;     // 8: k = 32 on 2^24 columns or more
     void* val = nullptr;         // (chunks + overread) * 64 values of dtype
     unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
 };

@@ -1072,7 +1072,7 @@ int bsm_dev_spmm_tiled(const bsm_tiled* t, const double* x, double* y, int32_t* 
 int bsm_tiled_info(const bsm_tiled* t, uint64_t* bytes, uint64_t* slots, uint64_t* panel_cols) {
     BSM_REQUIRE(t, BSM_ERR_INVALID, "null argument");
     const uint64_t n = (t->chunks + t->overread) * 64;
-    if (bytes) *bytes = n * (t->dtype == BSM_F32 ? 8 : 12) + ((uint64_t)t->nw * t->nb + 1) * 8;
+    if (bytes) *bytes = n * (t->meta_bytes + (t->dtype == BSM_F32 ? 4 : 8)) + ((uint64_t)t->nw * t->nb + 1) * 8;
     if (slots) *slots = t->chunks * 64;
     if (panel_cols) *panel_cols = 1ull << t->pshift;
     return BSM_OK;

@@ -67,7 +67,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // layout builder: one wave per task (gw, b). COUNT pass writes the task's
 // chunk count (a multiple of PHASES); WRITE pass fills its chunks from offs.
 // ---------------------------------------------------------------------------
-template <bool WRITE, int SLOTS, typename V>
+template <bool WRITE, int SLOTS, typename V, typename M = uint32_t>
 __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_cols, double pace, uint32_t rbits,
                                                     uint32_t pad, const int64_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col,
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
                                                     uint32_t rpw, uint32_t nb, uint32_t rw, uint32_t pshift,
                                                     int32_t* __restrict__ counts,
                                                     const int64_t* __restrict__ offs,
-                                                    uint32_t* __restrict__ meta, V* __restrict__ val) {
+                                                    M* __restrict__ meta, V* __restrict__ val) {
     const int lane = threadIdx.x & (WAVE - 1);
     const uint64_t task = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
     if (task >= (uint64_t)nw * nb) return;
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
             if (sel[j]) {
                 const int64_t e = cur[j];
                 if (WRITE) {
-                    meta[c * CHUNK + pos[j]] = ((uint32_t)col[e] << rbits) | (uint32_t)(lane + WAVE * j);
+                    meta[c * CHUNK + pos[j]] = ((M)(uint32_t)col[e] << rbits) | (M)(lane + WAVE * j);
                     val[c * CHUNK + pos[j]] = vals[e];
                 }
                 cur[j] = e + 1;
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
             }
         }
         if (WRITE && lane >= taken) {  // dummy entries: scratch row rw, X row 0, value 0
-            meta[c * CHUNK + lane] = rw;
+            meta[c * CHUNK + lane] = (M)rw;
             val[c * CHUNK + lane] = (V)0;
         }
         ++c;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
     const int64_t padded = (n + pad - 1) / pad * pad;
     if (WRITE) {
         for (int64_t p = n; p < padded; ++p, ++c) {
-            meta[c * CHUNK + lane] = rw;
+            meta[c * CHUNK + lane] = (M)rw;
             val[c * CHUNK + lane] = (V)0;
         }
     } else if (lane == 0) {
@@ -179,31 +179,54 @@ __global__ __launch_bounds__(256) void tiled_layout(uint64_t rows, uint64_t n_co
 // (256 or 128 B), lane q of a 16-lane group holding columns 2q, 2q + 1.
 template <typename T> struct Vec2;
 template <> struct Vec2<double> { using type = double2; };
-template <> struct Vec2<float> { using type = float2; };
+// f32: two floats in one 64-bit word (an 8-B lane load, unpacked for the
+// math). With HIP's float2 the compiler parked the gathered rows in AGPRs and
+// waited for every outstanding load before the copies (vmcnt(0) in the loop,
+// the pipeline collapsed: 338 ms at C4).
+struct F2 {
+    uint64_t u;
+};
+template <> struct Vec2<float> { using type = F2; };
+__device__ __forceinline__ double lo_of(const double2& v) { return v.x; }
+__device__ __forceinline__ double hi_of(const double2& v) { return v.y; }
+__device__ __forceinline__ float lo_of(const F2& v) { return __uint_as_float((uint32_t)v.u); }
+__device__ __forceinline__ float hi_of(const F2& v) { return __uint_as_float((uint32_t)(v.u >> 32)); }
+__device__ __forceinline__ double2 make_v2(double a, double b) { return make_double2(a, b); }
+__device__ __forceinline__ F2 make_v2(float a, float b) {
+    return F2{((uint64_t)__float_as_uint(b) << 32) | (uint64_t)__float_as_uint(a)};
+}
 template <typename T> using vec2_t = typename Vec2<T>::type;
 
-template <typename T = double>
+// M: the meta word, col << 8 | row-in-batch: uint32_t for columns < 2^24,
+// uint64_t for wider matrices (k = 32; 8 B more per entry)
+template <typename T = double, typename M = uint32_t>
 struct Idx {
-    uint32_t mi;  // lane 16g+q: entry (quad q, group g) of the chunk
+    M mi;  // lane 16g+q: entry (quad q, group g) of the chunk
     T vi;
 };
-template <typename T>
-__device__ __forceinline__ void load_idx(Idx<T>& c, const uint32_t* __restrict__ meta, const T* __restrict__ val,
+template <typename T, typename M>
+__device__ __forceinline__ void load_idx(Idx<T, M>& c, const M* __restrict__ meta, const T* __restrict__ val,
                                          int64_t chunk, int lane) {
     c.mi = meta[chunk * CHUNK + lane];
     c.vi = val[chunk * CHUNK + lane];
 }
 template <int I, typename T>
-__device__ __forceinline__ uint32_t bm(const Idx<T>& c) {  // entry (I, g) to every lane of group g
+__device__ __forceinline__ uint32_t bm(const Idx<T, uint32_t>& c) {  // entry (I, g) to every lane of group g
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.mi, 0x150 + I, 0xf, 0xf, false);
 }
-template <int I>
-__device__ __forceinline__ double bv(const Idx<double>& c) {
+template <int I, typename T>
+__device__ __forceinline__ uint64_t bm(const Idx<T, uint64_t>& c) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)c.mi, 0x150 + I, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(c.mi >> 32), 0x150 + I, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int I, typename M>
+__device__ __forceinline__ double bv(const Idx<double, M>& c) {
     return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(c.vi), 0x150 + I, 0xf, 0xf, false),
                             __builtin_amdgcn_update_dpp(0, __double2loint(c.vi), 0x150 + I, 0xf, 0xf, false));
 }
-template <int I>
-__device__ __forceinline__ float bv(const Idx<float>& c) {
+template <int I, typename M>
+__device__ __forceinline__ float bv(const Idx<float, M>& c) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.vi), 0x150 + I, 0xf, 0xf, false));
 }
 __device__ __forceinline__ double mul_rn(double a, double b) { return __dmul_rn(a, b); }
@@ -213,26 +236,25 @@ __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, 
 // PROBE (measurement only, wrong results): every gather reads X row
 // (col & xmask), e.g. xmask = 0 leaves the index/value stream alone on the
 // memory side (the PMC calibration of its 4-B / 8-B per-lane reads)
-template <bool PROBE, typename T, int... I>
-__device__ __forceinline__ void gather(vec2_t<T> (&x)[16], const Idx<T>& c, const vec2_t<T>* __restrict__ X, int q,
+template <bool PROBE, typename T, typename M, int... I>
+__device__ __forceinline__ void gather(vec2_t<T> (&x)[16], const Idx<T, M>& c, const vec2_t<T>* __restrict__ X, int q,
                                        uint32_t xmask, std::integer_sequence<int, I...>) {
     if (PROBE) ((x[I] = X[(int64_t)((bm<I>(c) >> 8) & xmask) * 16 + q]), ...);
     else ((x[I] = X[(int64_t)(bm<I>(c) >> 8) * 16 + q]), ...);
 }
-template <int I, typename T>
-__device__ __forceinline__ vec2_t<T>* yaddr(const Idx<T>& c, vec2_t<T>* yw, int q) {
-    return yw + (bm<I>(c) & 255u) * 16 + q;
+template <int I, typename T, typename M>
+__device__ __forceinline__ vec2_t<T>* yaddr(const Idx<T, M>& c, vec2_t<T>* yw, int q) {
+    return yw + (uint32_t)(bm<I>(c) & 255u) * 16 + q;
 }
-template <int I, typename T>
-__device__ __forceinline__ void madd(vec2_t<T>& y, const vec2_t<T>& x, const Idx<T>& c) {
+template <int I, typename T, typename M>
+__device__ __forceinline__ void madd(vec2_t<T>& y, const vec2_t<T>& x, const Idx<T, M>& c) {
     const T v = bv<I>(c);
-    y.x = add_rn(y.x, mul_rn(v, x.x));
-    y.y = add_rn(y.y, mul_rn(v, x.y));
+    y = make_v2(add_rn(lo_of(y), mul_rn(v, lo_of(x))), add_rn(hi_of(y), mul_rn(v, hi_of(x))));
 }
 // the chunk's rows are distinct (dummies all hit the scratch row): all 16
 // LDS reads, the 32 multiply-adds, all 16 writes
-template <typename T, int... I>
-__device__ __forceinline__ void sum_chunk(const vec2_t<T> (&x)[16], const Idx<T>& c, vec2_t<T>* yw, int q,
+template <typename T, typename M, int... I>
+__device__ __forceinline__ void sum_chunk(const vec2_t<T> (&x)[16], const Idx<T, M>& c, vec2_t<T>* yw, int q,
                                           std::integer_sequence<int, I...>) {
     vec2_t<T> y[16];
     ((y[I] = *yaddr<I>(c, yw, q)), ...);
@@ -282,10 +304,10 @@ __device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int l
     return false;  // not all resident: stop pacing
 }
 
-template <bool PROBE, bool ATOM, typename T = double>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
+template <bool PROBE, bool ATOM, typename T, typename M>
+__device__ __forceinline__ void spmm_tiled_k32_body(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
-    const uint32_t* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
+    const M* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
     vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
     using V2 = vec2_t<T>;
     extern __shared__ __align__(16) unsigned char ylds_raw[];
@@ -307,23 +329,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         if (sync && b > 0) sync = batch_wait(bar, (uint32_t)gridDim.x * (blockDim.x / WAVE) * b, lane, spins);
         const int nr = (int)min<uint64_t>(rw, wend - r0);
-        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = V2{(T)0, (T)0};
+        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = make_v2((T)0, (T)0);
         const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
         if (c1 > c0) {  // (c1 - c0) % PHASES == 0
-            Idx<T> M[6];
+            Idx<T, M> MI[6];
             V2 XS[3][16];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
-            gather<PROBE>(XS[0], M[0], X, q, xmask, SEQ);
-            gather<PROBE>(XS[1], M[1], X, q, xmask, SEQ);
+            for (int k = 0; k < 4; ++k) load_idx(MI[k], meta, val, c0 + k, lane);
+            gather<PROBE>(XS[0], MI[0], X, q, xmask, SEQ);
+            gather<PROBE>(XS[1], MI[1], X, q, xmask, SEQ);
             for (int64_t i = c0; i < c1; i += PHASES) {
 #pragma unroll
                 for (int k = 0; k < PHASES; ++k) {
-                    load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
-                    gather<PROBE>(XS[(k + 2) % 3], M[(k + 2) % 6], X, q, xmask, SEQ);
+                    load_idx(MI[(k + 4) % 6], meta, val, i + k + 4, lane);
+                    gather<PROBE>(XS[(k + 2) % 3], MI[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
-                    if constexpr (ATOM) sum_chunk_lds(XS[k % 3], M[k], yw, q, SEQ);
-                    else sum_chunk<T>(XS[k % 3], M[k], yw, q, SEQ);
+                    if constexpr (ATOM) sum_chunk_lds(XS[k % 3], MI[k], yw, q, SEQ);
+                    else sum_chunk<T>(XS[k % 3], MI[k], yw, q, SEQ);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -331,14 +353,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int rb = 0; rb < nr; rb += 4) {  // Y rows and their nonzero counts
             const int r = rb + g;
             const bool live = r < nr;
-            const V2 y = live ? yw[r * 16 + q] : V2{(T)0, (T)0};
+            const V2 y = live ? yw[r * 16 + q] : make_v2((T)0, (T)0);
             if (live) Y[(r0 + r) * 16 + q] = y;
-            const uint64_t m0 = __ballot(y.x != (T)0), m1 = __ballot(y.y != (T)0);
+            const uint64_t m0 = __ballot(lo_of(y) != (T)0), m1 = __ballot(hi_of(y) != (T)0);
             if (live && q == 0 && row_nnz)
                 row_nnz[r0 + r] = __popcll((m0 >> (16 * g)) & 0xffffull) + __popcll((m1 >> (16 * g)) & 0xffffull);
         }
         if (sync) batch_arrive(bar, 1, lane);
     }
+}
+
+// f64: the whole 512-register budget of one wave per SIMD (LDS allows one
+// workgroup per CU anyway); the gathers two chunks ahead take 192 of it.
+template <bool PROBE, bool ATOM, typename T = double, typename M = uint32_t>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
+    uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
+    const M* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
+    vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
+    spmm_tiled_k32_body<PROBE, ATOM, T, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
+}
+// f32 (F2 words, see Vec2<float>)
+template <typename M = uint32_t>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32_f32(
+    uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
+    const M* __restrict__ meta, const float* __restrict__ val, const F2* __restrict__ X, F2* __restrict__ Y,
+    int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
+    spmm_tiled_k32_body<false, false, float, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
 }
 
 // ---------------------------------------------------------------------------
@@ -559,7 +599,7 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // its chunks, one entry per chunk).
 bool tiled_wanted(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, uint64_t k, uint64_t max_row_len) {
     const bool shape = (dtype == BSM_F64 || dtype == BSM_F32) && rows > 0 && nnz > 0 &&
-                       ((k == 32 && n_cols < (1u << 24)) || (k == 1 && n_cols < (1u << (32 - K1_RBITS))));
+                       ((k == 32 && n_cols <= 0x7fffffffull) || (k == 1 && n_cols < (1u << (32 - K1_RBITS))));
     if (const char* e = getenv("BSM_SPMM_TILED")) {
         if (atoi(e) == 0) return false;
         if (atoi(e) == 2) return shape;
@@ -579,16 +619,19 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     BSM_REQUIRE(dtype == BSM_F64 || dtype == BSM_F32, BSM_ERR_UNSUPPORTED, "tiled: f64 or f32 only");
     const bool f32 = dtype == BSM_F32;
     const size_t es = f32 ? 4 : 8;
+    // k = 32 on 2^24 columns or more: 64-bit meta words (col << 8 | row)
+    const bool wide = k == 32 && n_cols >= (1ull << 24);
+    const size_t mb = wide ? 8 : 4;
     const uint32_t rbits = k == 1 ? K1_RBITS : 8;
-    BSM_REQUIRE(n_cols < (1ull << (32 - rbits)), BSM_ERR_UNSUPPORTED, "tiled: columns must be < 2^%u",
-                32 - rbits);
+    BSM_REQUIRE(k == 32 ? n_cols <= 0x7fffffffull : n_cols < (1ull << (32 - rbits)), BSM_ERR_UNSUPPORTED,
+                "tiled: columns must be < 2^%u", k == 32 ? 31u : 32 - rbits);
     *out = nullptr;
     int dev = 0;
     BSM_TRY(current_device(&dev));
     int cus = 0;
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     // k = 32: BSM_TILED_HALF=1 selects the two half-width passes (8 waves per CU)
-    const uint32_t half = k == 32 && !f32 && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
+    const uint32_t half = k == 32 && !f32 && !wide && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
     const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : (half ? HALF_WAVES_PER_CU : 4u);
     const uint32_t nw_env = env_u32("BSM_TILED_WAVES", wpc * (uint32_t)cus);
     const uint32_t nw = half ? (nw_env + wpc - 1) / wpc * wpc : nw_env;  // whole workgroups
@@ -612,24 +655,26 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     BSM_TRY(counts.alloc(tasks * sizeof(int32_t)));
     BSM_TRY(offs.alloc((tasks + 1) * sizeof(int64_t)));
     const uint64_t grid = (tasks + 3) / 4;
-    auto layout = [&](auto write_tag, int32_t* cnt, const int64_t* of, uint32_t* me, void* va) -> int {
+    auto layout = [&](auto write_tag, int32_t* cnt, const int64_t* of, void* me, void* va) -> int {
         constexpr bool W = decltype(write_tag)::value;
-        auto go = [&]<typename V>(V*) {
+        auto go = [&]<typename V, typename MT>(V*, MT*) {
             if (k == 1)
-                tiled_layout<W, (K1_RW_MAX + 1) / WAVE, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                tiled_layout<W, (K1_RW_MAX + 1) / WAVE, V, MT><<<dim3((unsigned)grid), 256, 0, s>>>(
                     rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
-                    cnt, of, me, static_cast<V*>(va));
+                    cnt, of, static_cast<MT*>(me), static_cast<V*>(va));
             else if (rw_cap > 192)  // f32 batches up to 255 rows: four row slots per lane
-                tiled_layout<W, 4, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                tiled_layout<W, 4, V, MT><<<dim3((unsigned)grid), 256, 0, s>>>(
                     rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
-                    cnt, of, me, static_cast<V*>(va));
+                    cnt, of, static_cast<MT*>(me), static_cast<V*>(va));
             else
-                tiled_layout<W, 3, V><<<dim3((unsigned)grid), 256, 0, s>>>(
+                tiled_layout<W, 3, V, MT><<<dim3((unsigned)grid), 256, 0, s>>>(
                     rows, n_cols, pace, rbits, pad, rp, col, static_cast<const V*>(vals), nw, rpw, nb, rw, pshift,
-                    cnt, of, me, static_cast<V*>(va));
+                    cnt, of, static_cast<MT*>(me), static_cast<V*>(va));
         };
-        if (f32) go((float*)nullptr);
-        else go((double*)nullptr);
+        if (f32 && wide) go((float*)nullptr, (uint64_t*)nullptr);
+        else if (f32) go((float*)nullptr, (uint32_t*)nullptr);
+        else if (wide) go((double*)nullptr, (uint64_t*)nullptr);
+        else go((double*)nullptr, (uint32_t*)nullptr);
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     };
@@ -659,17 +704,17 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     const uint64_t slots = ((uint64_t)total + overread) * CHUNK;
     size_t free_b = 0, total_b = 0;
     BSM_HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    BSM_REQUIRE(slots * (4 + es) + (256ull << 20) + reserve < free_b, BSM_ERR_OOM,
-                "tiled: %llu MB stream (+%llu MB reserved) does not fit", (unsigned long long)(slots * (4 + es) >> 20),
+    BSM_REQUIRE(slots * (mb + es) + (256ull << 20) + reserve < free_b, BSM_ERR_OOM,
+                "tiled: %llu MB stream (+%llu MB reserved) does not fit", (unsigned long long)(slots * (mb + es) >> 20),
                 (unsigned long long)(reserve >> 20));
     DBuf meta, val, bar;
     BSM_TRY(bar.alloc(8 * BAR_STRIDE * sizeof(unsigned)));
-    BSM_TRY(meta.alloc(slots * sizeof(uint32_t)));
+    BSM_TRY(meta.alloc(slots * mb));
     BSM_TRY(val.alloc(slots * es));
     BSM_TRY(phase_end(pt ? &pt->alloc_ms : nullptr));
-    BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.as<uint32_t>(), val.p));
+    BSM_TRY(layout(std::true_type{}, nullptr, offs.as<int64_t>(), meta.p, val.p));
     // over-read padding: valid dummy entries (X row 0)
-    BSM_HIP_TRY(hipMemsetAsync(meta.as<uint32_t>() + (uint64_t)total * CHUNK, 0, overread * CHUNK * 4, s));
+    BSM_HIP_TRY(hipMemsetAsync(static_cast<char*>(meta.p) + (uint64_t)total * CHUNK * mb, 0, overread * CHUNK * mb, s));
     BSM_HIP_TRY(hipMemsetAsync(static_cast<char*>(val.p) + (uint64_t)total * CHUNK * es, 0, overread * CHUNK * es, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     BSM_TRY(phase_end(pt ? &pt->write_ms : nullptr));
@@ -690,7 +735,8 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     t->overread = overread;
     t->stage = k1_stage;
     t->offs = static_cast<int64_t*>(offs.release());
-    t->meta = static_cast<uint32_t*>(meta.release());
+    t->meta_bytes = (uint32_t)mb;
+    t->meta = meta.release();
     t->val = val.release();
     t->bar = static_cast<unsigned*>(bar.release());
     *out = t;
@@ -712,13 +758,15 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
     if (t->k == 1 && t->dtype == BSM_F32) {
         const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(float);
         auto kern = t->stage == 8 ? spmm_tiled_k1<8, float> : spmm_tiled_k1<4, float>;
-        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs,
+                                              static_cast<const uint32_t*>(t->meta),
                                               static_cast<const float*>(t->val), static_cast<const float*>(x),
                                               static_cast<float*>(y), row_nnz, bar, neg_init, k1mask);
     } else if (t->k == 1) {
         const size_t lds = (size_t)4 * (t->rw + 1) * sizeof(double);
         auto kern = t->stage == 8 ? spmm_tiled_k1<8> : spmm_tiled_k1<4>;
-        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
+        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs,
+                                              static_cast<const uint32_t*>(t->meta),
                                               static_cast<const double*>(t->val), static_cast<const double*>(x),
                                               static_cast<double*>(y), row_nnz, bar, neg_init, k1mask);
     } else if (t->dtype == BSM_F32) {  // k = 32, f32: 128-B rows, up to 255 per batch
@@ -726,14 +774,21 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         // BSM_TILED_SPINS: the batch barrier's poll bound (default 4000 polls
         // of s_sleep 8, ~0.9 ms; A/B for the f32 batches, ~3x longer)
         static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
-        spmm_tiled_k32<false, false, float><<<dim3(t->nw / 4), 256, lds, s>>>(
-            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, static_cast<const float*>(t->val),
-            static_cast<const float2*>(x), static_cast<float2*>(y), row_nnz, bar, 0xffffffffu, spins);
+        if (t->meta_bytes == 8)
+            spmm_tiled_k32_f32<uint64_t><<<dim3(t->nw / 4), 256, lds, s>>>(
+                t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint64_t*>(t->meta),
+                static_cast<const float*>(t->val), static_cast<const F2*>(x), static_cast<F2*>(y), row_nnz,
+                bar, 0xffffffffu, spins);
+        else
+            spmm_tiled_k32_f32<uint32_t><<<dim3(t->nw / 4), 256, lds, s>>>(
+                t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint32_t*>(t->meta),
+                static_cast<const float*>(t->val), static_cast<const F2*>(x), static_cast<F2*>(y), row_nnz,
+                bar, 0xffffffffu, spins);
     } else if (t->half) {
         const size_t lds = (size_t)HALF_WAVES_PER_CU * (t->rw + 1) * 128;
         spmm_tiled_k32h<<<dim3(t->nw / HALF_WAVES_PER_CU), 64 * HALF_WAVES_PER_CU, lds, s>>>(
-            t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta, static_cast<const double*>(t->val),
-            static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar);
+            t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint32_t*>(t->meta),
+            static_cast<const double*>(t->val), static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
         // BSM_TILED_PROBE_MASK=<mask> (measurement only, wrong results): see gather()
@@ -742,9 +797,16 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
         auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true, false>
                                          : (atom ? spmm_tiled_k32<false, true> : spmm_tiled_k32<false, false>);
         static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
-        kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs, t->meta,
-                                              static_cast<const double*>(t->val), static_cast<const double2*>(x),
-                                              static_cast<double2*>(y), row_nnz, bar, xmask, spins);
+        if (t->meta_bytes == 8)  // 2^24 columns or more
+            spmm_tiled_k32<false, false, double, uint64_t><<<dim3(t->nw / 4), 256, lds, s>>>(
+                t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint64_t*>(t->meta),
+                static_cast<const double*>(t->val), static_cast<const double2*>(x), static_cast<double2*>(y), row_nnz,
+                bar, 0xffffffffu, spins);
+        else
+            kern<<<dim3(t->nw / 4), 256, lds, s>>>(t->rows, t->rpw, t->nb, t->rw, t->offs,
+                                                  static_cast<const uint32_t*>(t->meta),
+                                                  static_cast<const double*>(t->val), static_cast<const double2*>(x),
+                                                  static_cast<double2*>(y), row_nnz, bar, xmask, spins);
     }
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;

@@ -304,3 +304,34 @@ def test_tiled_wanted_f32_c4_shape():
     assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
     assert lib.bsm_dev_tiled_wanted(f64, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
     assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 1 << 24, 10_000_000_000, 32, 1000) == 0  # cols < 2^24
+
+
+def test_tiled_wide_columns_64bit_meta(geometry):
+    """2^25 columns (X = 8.6 GB): the copy's meta word is 64-bit (col << 8 |
+    row no longer fits 32 bits past 2^24 columns). The same Y and counts as the
+    one-row-per-wave kernel, bit for bit, and a row sample summed in storage
+    order on the host from the same X rows (multiply, then add, in f64)."""
+    device = _dev()
+    geometry(None, 256, None)
+    rows, n_cols, k = 20_000, 1 << 25, 32
+    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_UNIFORM, 40, 160)
+    x = device.gen_dense(1001, 0, n_cols, k)
+    assert blk.plan_tiled(k, force=True) is not None
+    info = blk.tiled.info()
+    assert info["bytes"] >= info["slots"] * 16  # 8-B meta + 8-B value per slot
+    y1, n1 = _spmm(blk, x, True)
+    y0, n0 = _spmm(blk, x, False)
+    assert _same(y1, y0) and torch.equal(n1, n0)
+    rp = blk.row_ptr.cpu().numpy()
+    ci = blk.col.cpu().numpy()
+    v = blk.vals.cpu().numpy()
+    assert int(ci.max()) >= 1 << 24
+    for r in (0, 777, 12_345, rows - 1):
+        cols = ci[rp[r]:rp[r + 1]].astype(np.int64)
+        xr = x[torch.as_tensor(cols, device="cuda")].cpu().numpy()
+        acc = np.zeros(k)
+        for e in range(len(cols)):
+            acc = acc + v[rp[r] + e] * xr[e]  # f64 multiply, then add: the reference's order
+        assert np.array_equal(y1[r].cpu().numpy().view(np.uint64), acc.view(np.uint64)), r
+    del x
+    torch.cuda.empty_cache()
