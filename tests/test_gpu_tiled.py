@@ -298,12 +298,14 @@ def test_public_mul_dense_tiled_copy_f32(orc, monkeypatch, k, rw):
 
 def test_tiled_wanted_f32_c4_shape():
     """The library takes the tiled copy for an f32 C4-shaped product (X beyond
-    1 GiB at k = 32), as for f64."""
+    1 GiB at k = 32), as for f64, and for matrices wider than 2^24 columns."""
     lib = _lib.load()
     f32, f64 = _lib.DTYPE_CODES[np.dtype(np.float32)], _lib.DTYPE_CODES[np.dtype(np.float64)]
     assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
     assert lib.bsm_dev_tiled_wanted(f64, 10_000_000, 10_000_000, 10_000_000_000, 32, 1000) == 1
-    assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 1 << 24, 10_000_000_000, 32, 1000) == 0  # cols < 2^24
+    # 2^24 columns and more: the 64-bit meta copy; device columns are int32
+    assert lib.bsm_dev_tiled_wanted(f32, 10_000_000, 1 << 24, 10_000_000_000, 32, 1000) == 1
+    assert lib.bsm_dev_tiled_wanted(f64, 10_000_000, 1 << 31, 10_000_000_000, 32, 1000) == 0
 
 
 def test_tiled_wide_columns_64bit_meta(geometry):
