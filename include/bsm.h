@@ -225,14 +225,16 @@ int bsm_dev_spmm_panelled(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nn
                           const void* x, void* y, int32_t* row_nnz, uint64_t panel_cols,
                           const int32_t* seg, void* stream);
 /* Row-block x column-panel schedule of bsm_dev_spmm (Csr::mul_dense,
- * sparse.rs:426-446) for f64 with k = 32 and X beyond the Infinity Cache (the
- * C4 shape), or k = 1 and X beyond an XCD's L2 (C2); the copy is built for
- * one k (DESIGN.md "SpMM: row blocks x column panels"). bsm_dev_tiled_create
- * re-lays the matrix once (12 B per entry plus chunk padding, a copy beside
- * the CSR; synchronous on `stream`) and returns BSM_ERR_UNSUPPORTED for a
- * shape it does not serve (cols >= 2^24 at k = 32, 2^21 at k = 1; rows so uneven that chunk padding
- * passes 25 % of the entries, unless flags has BSM_TILED_ANY_PADDING) or
- * BSM_ERR_OOM.
+ * sparse.rs:426-446) with k = 32 and X beyond the Infinity Cache (the C4
+ * shape), or k = 1 and X beyond an XCD's L2 (C2); the copy is built for one k
+ * (DESIGN.md "SpMM: row blocks x column panels"). bsm_csr_mul_dense builds
+ * it for f64 and f32; these device-level entry points are the f64 form.
+ * bsm_dev_tiled_create re-lays the matrix once (12 B per entry, 16 B from
+ * 2^24 columns on at k = 32, plus chunk padding: a copy beside the CSR;
+ * synchronous on `stream`) and returns BSM_ERR_UNSUPPORTED for a shape it
+ * does not serve (cols >= 2^31 at k = 32, >= 2^21 at k = 1; rows so uneven
+ * that chunk padding passes 25 % of the entries, unless flags has
+ * BSM_TILED_ANY_PADDING) or BSM_ERR_OOM.
  * bsm_dev_spmm_tiled = bsm_dev_spmm on that copy: the same Y and row_nnz,
  * bit for bit (each row still sums in storage order). bsm_dev_tiled_wanted
  * says whether the library would use it for this shape (env BSM_SPMM_TILED:
