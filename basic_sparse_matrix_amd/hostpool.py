@@ -30,6 +30,7 @@ import numpy as np
 
 _HUGE = 2 << 20
 _MIN_POOLED = 1 << 20  # below this numpy's allocator is cheap enough
+_REGISTER_MAX = 1 << 30
 
 
 def _register(addr: int, nbytes: int) -> bool:
@@ -62,8 +63,11 @@ class _Mapping:
             except OSError:
                 pass
         # page-locked once for the mapping's life: every download into it is
-        # then one direct DMA (and its pages are faulted in here, once)
-        self.registered = _register(self.addr, cap)
+        # then one direct DMA (and its pages are faulted in here, once). Not
+        # past 1 GiB: the direct path stops at 128M entries, and pinning a
+        # C4-sized result (2.56 GB per array) each time the free list's cap
+        # evicts it cost more than it saved (multi_api_ms 343 -> 507 ms)
+        self.registered = cap <= _REGISTER_MAX and _register(self.addr, cap)
         if self.registered:
             weakref.finalize(self, _unregister, self.addr)
 
