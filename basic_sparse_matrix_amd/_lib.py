@@ -24,7 +24,9 @@ try:  # see module docstring: one HIP runtime per process
 except Exception:  # pragma: no cover - torch is optional for the library
     torch = None
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libbsm_hip.so")
+# BSM_LIB_PATH: another build of the library (A/B of two builds in one process tree)
+LIB_PATH = os.environ.get("BSM_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                          "libbsm_hip.so")
 
 # bsm_dtype (include/bsm.h)
 BSM_F64, BSM_F32, BSM_I32, BSM_U32, BSM_I64, BSM_U64 = range(6)
