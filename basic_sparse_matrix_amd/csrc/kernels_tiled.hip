@@ -251,15 +251,29 @@ __device__ __forceinline__ void madd(vec2_t<T>& y, const vec2_t<T>& x, const Idx
     const T v = bv<I>(c);
     y = make_v2(add_rn(lo_of(y), mul_rn(v, lo_of(x))), add_rn(hi_of(y), mul_rn(v, hi_of(x))));
 }
-// the chunk's rows are distinct (dummies all hit the scratch row): all 16
-// LDS reads, the 32 multiply-adds, all 16 writes
-template <typename T, typename M, int... I>
+// the chunk's rows are distinct (dummies all hit the scratch row), so its
+// 16 read-add-write updates are independent: done in parts of SUM_PART
+// entries (LDS reads, multiply-adds, writes). With all 16 at once (64 VGPRs
+// of Y rows for f64) the allocator parked gathered rows in AGPRs and waited
+// for every outstanding load at the loop's back edge (vmcnt(0) once per
+// PHASES chunks); parts of 8 keep the pipeline (vmcnt >= 21 in the loop).
+#ifndef BSM_SUM_PART
+#define BSM_SUM_PART 16
+#endif
+constexpr int SUM_PART = BSM_SUM_PART;
+static_assert(16 % SUM_PART == 0, "SUM_PART divides the chunk");
+template <int B, typename T, typename M, int... I>
+__device__ __forceinline__ void sum_part(const vec2_t<T> (&x)[16], const Idx<T, M>& c, vec2_t<T>* yw, int q,
+                                         std::integer_sequence<int, I...>) {
+    vec2_t<T> y[sizeof...(I)];
+    ((y[I] = *yaddr<B + I>(c, yw, q)), ...);
+    (madd<B + I>(y[I], x[B + I], c), ...);
+    ((*yaddr<B + I>(c, yw, q) = y[I]), ...);
+}
+template <typename T, typename M, int... P>
 __device__ __forceinline__ void sum_chunk(const vec2_t<T> (&x)[16], const Idx<T, M>& c, vec2_t<T>* yw, int q,
-                                          std::integer_sequence<int, I...>) {
-    vec2_t<T> y[16];
-    ((y[I] = *yaddr<I>(c, yw, q)), ...);
-    (madd<I>(y[I], x[I], c), ...);
-    ((*yaddr<I>(c, yw, q) = y[I]), ...);
+                                          std::integer_sequence<int, P...>) {
+    (sum_part<P * SUM_PART>(x, c, yw, q, std::make_integer_sequence<int, SUM_PART>{}), ...);
 }
 
 // BSM_TILED_LDSADD=1 (A/B): the chunk's Y update as LDS atomic adds of the
@@ -345,7 +359,7 @@ __device__ __forceinline__ void spmm_tiled_k32_body(
                     gather<PROBE>(XS[(k + 2) % 3], MI[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
                     if constexpr (ATOM) sum_chunk_lds(XS[k % 3], MI[k], yw, q, SEQ);
-                    else sum_chunk<T>(XS[k % 3], MI[k], yw, q, SEQ);
+                    else sum_chunk<T>(XS[k % 3], MI[k], yw, q, std::make_integer_sequence<int, 16 / SUM_PART>{});
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
