@@ -128,6 +128,9 @@ SIGNATURES = [
     ("bsm_multi_create", _int, [_int, ctypes.POINTER(_int), ctypes.POINTER(_vp)]),
     ("bsm_multi_unique_id", _int, [_vp]),
     ("bsm_multi_create_rank", _int, [_vp, _int, _int, _int, ctypes.POINTER(_vp)]),
+    ("bsm_multi_create_external", _int, [_int, _int, _int, ctypes.POINTER(_vp)]),
+    ("bsm_multi_is_external", _int, [_vp, ctypes.POINTER(_int)]),
+    ("bsm_partition_rows", _int, [_vp, _u64, _u32, _vp]),
     ("bsm_multi_info", _int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     ("bsm_multi_broadcast", _int, [_vp, _pp, _u64, _int]),
     ("bsm_multi_destroy", None, [_vp]),
@@ -143,6 +146,9 @@ SIGNATURES = [
     ("bsm_mcsr_reset_times", None, [_vp]),
     ("bsm_mcsr_copy_y", _int, [_vp, _int, _vp, _vp]),
     ("bsm_mcsr_output", _int, [_vp, ctypes.POINTER(_vp)]),
+    ("bsm_mcsr_compact", _int, [_vp]),
+    ("bsm_mcsr_slot_read", _int, [_vp, _int, _u32, _u32, _vp, _vp]),
+    ("bsm_mcsr_slot_write", _int, [_vp, _int, _u32, _u32, _vp, _vp]),
     ("bsm_mcsr_free", None, [_vp]),
 ]
 

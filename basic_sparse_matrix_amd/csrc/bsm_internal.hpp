@@ -120,9 +120,11 @@ hipError_t read_dev(void* host, const void* dev, size_t bytes, hipStream_t s);
 // waits for the whole device, and a call such as add_sparse makes ~25 of
 // them (1.3-2 ms per call at the reference bench's e = 300k,
 // profiles/r03_u_*). A cached block is only handed out again to the same
-// thread for the same stream, so stream order separates its uses.
-void* tmp_get(size_t n, hipStream_t s, size_t* cap);
-void tmp_put(void* p, size_t cap, hipStream_t s);
+// thread for the same device and stream, so stream order separates its uses
+// (the device is part of the key: the null stream names a different queue on
+// every device). Every block is a plain hipMalloc allocation.
+void* tmp_get(size_t n, int device, hipStream_t s, size_t* cap);
+void tmp_put(void* p, size_t cap, int device, hipStream_t s);
 
 // RAII device buffer for host-path temporaries. alloc(n) is hipMalloc /
 // hipFree; alloc(n, s) takes the block from the calling thread's cache for
@@ -131,6 +133,7 @@ struct DBuf {
     void* p = nullptr;
     size_t bytes = 0;
     hipStream_t st = nullptr;
+    int dev = -1;
     size_t cap = 0;  // > 0: a cached temporary of this capacity
     DBuf() = default;
     DBuf(const DBuf&) = delete;
@@ -138,7 +141,7 @@ struct DBuf {
     ~DBuf() { reset(); }
     void reset() {
         if (p) {
-            if (cap) tmp_put(p, cap, st);
+            if (cap) tmp_put(p, cap, dev, st);
             else (void)hipFree(p);
         }
         p = nullptr;
@@ -148,7 +151,11 @@ struct DBuf {
     int alloc(size_t n, hipStream_t s) {
         reset();
         if (n == 0) n = 16;
-        p = tmp_get(n, s, &cap);
+        if (hipGetDevice(&dev) != hipSuccess) {
+            set_error("device temporary: no current device");
+            return BSM_ERR_HIP;
+        }
+        p = tmp_get(n, dev, s, &cap);
         if (!p) {
             cap = 0;
             set_error("device temporary of %zu bytes: out of memory", n);
@@ -170,11 +177,13 @@ struct DBuf {
         bytes = n;
         return BSM_OK;
     }
-    void* release() {  // a cached temporary is never released (it goes back to the cache)
-        if (cap) return nullptr;
+    // The caller takes the block and frees it with hipFree. A cached
+    // temporary is a hipMalloc block too: it simply leaves the cache's care.
+    void* release() {
         void* q = p;
         p = nullptr;
         bytes = 0;
+        cap = 0;
         return q;
     }
     template <typename T> T* as() const { return static_cast<T*>(p); }

@@ -249,6 +249,7 @@ struct TmpCache {
     struct Ent {
         void* p;
         size_t cap;
+        int device;
         hipStream_t s;
     };
     std::vector<Ent> free_list;
@@ -265,12 +266,12 @@ constexpr size_t TMP_CACHE_MAX = 512ull << 20;   // bytes kept per thread
 constexpr size_t TMP_BLOCK_MAX = 256ull << 20;   // larger temporaries are not cached
 }  // namespace
 
-void* tmp_get(size_t n, hipStream_t s, size_t* cap) {
+void* tmp_get(size_t n, int device, hipStream_t s, size_t* cap) {
     size_t c = 4096;
     while (c < n) c <<= 1;  // power-of-two classes
     TmpCache& tc = tmp_cache();
     for (size_t i = 0; i < tc.free_list.size(); ++i) {
-        if (tc.free_list[i].cap == c && tc.free_list[i].s == s) {
+        if (tc.free_list[i].cap == c && tc.free_list[i].s == s && tc.free_list[i].device == device) {
             void* p = tc.free_list[i].p;
             tc.held -= c;
             tc.free_list[i] = tc.free_list.back();
@@ -286,13 +287,13 @@ void* tmp_get(size_t n, hipStream_t s, size_t* cap) {
     return p;
 }
 
-void tmp_put(void* p, size_t cap, hipStream_t s) {
+void tmp_put(void* p, size_t cap, int device, hipStream_t s) {
     TmpCache& tc = tmp_cache();
     if (cap > TMP_BLOCK_MAX || (cap & (cap - 1)) || tc.held + cap > TMP_CACHE_MAX) {
         (void)hipFree(p);
         return;
     }
-    tc.free_list.push_back({p, cap, s});
+    tc.free_list.push_back({p, cap, device, s});
     tc.held += cap;
 }
 

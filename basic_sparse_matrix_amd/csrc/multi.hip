@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -44,6 +45,9 @@
 
 struct bsm_multi {
     int world = 1, first_rank = 0, n_local = 0;
+    // no communicator (bsm_multi_create_external): step stops before the
+    // all-gathers and the caller moves the slots between ranks
+    bool external = false;
     std::vector<int> devices;
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> compute, comm;
@@ -87,6 +91,10 @@ struct bsm_mcsr {
     uint64_t k = 0;
     bool prepared = false, squeeze = false;
     int schedule = 0;
+    // one call at a time per matrix: the gathered Y, the output buffers, the
+    // events and the collectives of a step are shared state (recursive:
+    // mul_dense runs prepare, step and output under the same hold)
+    mutable std::recursive_mutex mu;
 };
 
 namespace bsm {
@@ -127,22 +135,28 @@ int for_each_local(int n, F&& f) {
     return BSM_OK;
 }
 
-// bound i = the first row whose start is >= i*nnz/P (binary search on
-// row_ptr), bounds[0] = 0, bounds[P] = rows; even rows for an empty matrix
-// (the rule of distributed.partition_rows_by_nnz).
+// Piece bounds: contiguous row blocks of near-equal cost, where a row costs
+// its entries plus c = max(1, nnz/rows) (its Y row, its count and its share of
+// the compaction). bound i = the first row r with cost(rows before r) >=
+// i*total/P (binary search on row_ptr), bounds[0] = 0, bounds[P] = rows.
+// For equal row lengths (C4) this is the nnz-balanced split; on skewed
+// matrices (long runs of empty rows, one huge row) it caps a piece at
+// 2*rows/P + 1 rows, so the P*pad slot rows of the gathered Y stay <= ~2x
+// rows (a pure nnz split lets one piece take nearly every row, and every
+// device would then hold P times the single-GPU Y). Exact integer
+// arithmetic: cost is scaled by rows, cost(r) = rp[r]*rows + r*max(nnz, rows).
 template <typename RP>
-std::vector<uint64_t> partition_by_nnz(const RP* rp, uint64_t rows, uint64_t nnz, uint32_t P) {
+std::vector<uint64_t> partition_by_cost(const RP* rp, uint64_t rows, uint64_t nnz, uint32_t P) {
     std::vector<uint64_t> b(P + 1);
+    using u128 = unsigned __int128;
+    const u128 per_row = std::max<uint64_t>(nnz, rows);
+    const u128 total = (u128)nnz * rows + (u128)rows * per_row;
     for (uint32_t i = 0; i <= P; ++i) {
-        if (nnz == 0) {
-            b[i] = rows * i / P;
-            continue;
-        }
-        const uint64_t target = (uint64_t)((unsigned __int128)nnz * i / P);
-        uint64_t lo = 0, hi = rows;  // first r in [0, rows) with rp[r] >= target, else rows
+        const u128 target = total * i / P;
+        uint64_t lo = 0, hi = rows;  // first r in [0, rows) with cost(r) >= target, else rows
         while (lo < hi) {
             const uint64_t mid = (lo + hi) / 2;
-            if ((uint64_t)rp[mid] >= target) hi = mid;
+            if ((u128)(uint64_t)rp[mid] * rows + (u128)mid * per_row >= target) hi = mid;
             else lo = mid + 1;
         }
         b[i] = lo;
@@ -250,6 +264,21 @@ void free_mcsr(bsm_mcsr* m) {
     delete m;
 }
 
+// The gathered Y (P*pad slot rows) -> the output Csr: scan of the row counts,
+// compaction (insert's zero skip, sparse.rs:229), and the slot -> row map of
+// row_ptr when a piece other than the last is short.
+int compact_local(bsm_mcsr* m, Local& L, hipStream_t s) {
+    const uint64_t slot_rows = (uint64_t)m->P * m->pad;
+    BSM_TRY(exclusive_scan_i32_to_i64(L.nz, L.rp_pad, slot_rows, L.ws, L.ws_b, s));
+    BSM_TRY(compact_dispatch(m->dtype, slot_rows, m->k, L.y, L.rp_pad, L.ocol, L.oval, s));
+    if (m->squeeze) {
+        squeeze_row_ptr<<<(unsigned)((m->rows + 1 + 255) / 256), 256, 0, s>>>(L.rp_pad, L.bounds, m->P, m->pad,
+                                                                              m->rows, L.rp_out);
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    return BSM_OK;
+}
+
 }  // namespace
 
 // Upload rows [r0, r1) of a host finalised Csr (absolute row_ptr) as a handle
@@ -350,6 +379,46 @@ int bsm_multi_create_rank(const void* id, int world, int rank, int device, bsm_m
     return BSM_OK;
 }
 
+int bsm_multi_create_external(int world, int rank, int device, bsm_multi** out) {
+    BSM_REQUIRE(out && world >= 1 && rank >= 0 && rank < world && device >= 0, BSM_ERR_INVALID,
+                "bsm_multi_create_external: bad argument (world %d, rank %d, device %d)", world, rank, device);
+    *out = nullptr;
+    int have = 0;
+    if (hipGetDeviceCount(&have) != hipSuccess || have == 0) {
+        (void)hipGetLastError();
+        set_error("bsm_multi_create_external: no HIP device visible");
+        return BSM_ERR_NO_DEVICE;
+    }
+    BSM_REQUIRE(device < have, BSM_ERR_INVALID, "bsm_multi_create_external: device %d of %d", device, have);
+    auto* c = new bsm_multi();
+    c->world = world;
+    c->n_local = 1;
+    c->first_rank = rank;
+    c->external = true;
+    c->devices = {device};
+    c->comms.assign(1, nullptr);
+    const int rc = create_streams(c);
+    if (rc != BSM_OK) {
+        destroy_multi(c);
+        return rc;
+    }
+    *out = c;
+    return BSM_OK;
+}
+
+int bsm_multi_is_external(const bsm_multi* ctx, int* external) {
+    BSM_REQUIRE(ctx && external, BSM_ERR_INVALID, "null argument");
+    *external = ctx->external ? 1 : 0;
+    return BSM_OK;
+}
+
+int bsm_partition_rows(const uint64_t* row_ptr, uint64_t rows, uint32_t pieces, uint64_t* bounds) {
+    BSM_REQUIRE(row_ptr && bounds && pieces >= 1, BSM_ERR_INVALID, "bsm_partition_rows: bad argument");
+    const auto b = partition_by_cost(row_ptr, rows, row_ptr[rows], pieces);
+    std::copy(b.begin(), b.end(), bounds);
+    return BSM_OK;
+}
+
 int bsm_multi_info(const bsm_multi* ctx, int* world, int* n_local, int* first_rank) {
     BSM_REQUIRE(ctx, BSM_ERR_INVALID, "null context");
     if (world) *world = ctx->world;
@@ -361,6 +430,8 @@ int bsm_multi_info(const bsm_multi* ctx, int* world, int* n_local, int* first_ra
 int bsm_multi_broadcast(bsm_multi* ctx, void* const* bufs, uint64_t bytes, int root) {
     BSM_REQUIRE(ctx && (bytes == 0 || bufs) && root >= 0 && root < ctx->world, BSM_ERR_INVALID,
                 "bsm_multi_broadcast: bad argument");
+    BSM_REQUIRE(!ctx->external, BSM_ERR_UNSUPPORTED,
+                "bsm_multi_broadcast: an external context has no communicator (copy X to every rank yourself)");
     if (bytes == 0) return BSM_OK;
     for (int i = 0; i < ctx->n_local; ++i) BSM_REQUIRE(bufs[i], BSM_ERR_INVALID, "null buffer %d", i);
     BSM_NCCL_TRY(ncclGroupStart());
@@ -394,7 +465,7 @@ int bsm_mcsr_upload(bsm_multi* ctx, int dtype, uint64_t rows, uint64_t cols, uin
     *out = nullptr;
     bsm_mcsr* m = new_mcsr(ctx, dtype, rows, cols, chunks);
     m->nnz = nnz;
-    set_bounds(m, partition_by_nnz(row_ptr, rows, nnz, m->P));
+    set_bounds(m, partition_by_cost(row_ptr, rows, nnz, m->P));
     const int rc = for_each_local(ctx->n_local, [&](int i) -> int {
         Local& L = m->loc[i];
         DeviceGuard g(L.device);
@@ -440,7 +511,7 @@ int bsm_mcsr_generate(bsm_multi* ctx, int dtype, uint64_t seed, uint64_t rows, u
             return rc;
         }
         m->nnz = (uint64_t)h[rows];
-        set_bounds(m, partition_by_nnz(h.data(), rows, m->nnz, m->P));
+        set_bounds(m, partition_by_cost(h.data(), rows, m->nnz, m->P));
     }
     const int rc = for_each_local(ctx->n_local, [&](int i) -> int {
         Local& L = m->loc[i];
@@ -496,6 +567,7 @@ int bsm_mcsr_info(const bsm_mcsr* m, uint64_t* rows, uint64_t* cols, uint64_t* n
 
 int bsm_mcsr_prepare(bsm_mcsr* m, uint64_t k, int schedule, double* plan_ms) {
     BSM_REQUIRE(m && schedule >= 0 && schedule <= 2, BSM_ERR_INVALID, "bsm_mcsr_prepare: bad argument");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     BSM_REQUIRE(k < (1ull << 31), BSM_ERR_UNSUPPORTED, "k too large");
     bsm_multi* ctx = m->ctx;
     const size_t es = dtype_size(m->dtype);
@@ -582,6 +654,7 @@ int bsm_mcsr_prepare(bsm_mcsr* m, uint64_t k, int schedule, double* plan_ms) {
 int bsm_mcsr_plan_info(const bsm_mcsr* m, int* tiled_pieces, int* local_pieces, uint64_t* copy_bytes,
                        uint64_t* panel_cols) {
     BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     int nt = 0, np = 0;
     uint64_t bytes = 0, pc = 0;
     for (const auto& L : m->loc)
@@ -606,7 +679,9 @@ int bsm_mcsr_plan_info(const bsm_mcsr* m, int* tiled_pieces, int* local_pieces, 
 }
 
 int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
-    BSM_REQUIRE(m && m->prepared, BSM_ERR_INVALID, "bsm_mcsr_step: prepare the matrix first");
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "bsm_mcsr_step: null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_step: prepare the matrix first");
     bsm_multi* ctx = m->ctx;
     const uint64_t k = m->k;
     BSM_REQUIRE(k == 0 || x_dev, BSM_ERR_INVALID, "null X");
@@ -644,6 +719,9 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
                 BSM_HIP_TRY(hipEventRecord(L.ev[L.steps * EV_PER_STEP + 1], ctx->compute[i]));
         }
         // round c of every rank lands at slots c*world .. c*world + world - 1
+        // (an external context leaves that to the caller: bsm_mcsr_slot_read /
+        // _write, then bsm_mcsr_compact)
+        if (ctx->external) continue;
         BSM_NCCL_TRY(ncclGroupStart());
         for (int i = 0; i < ctx->n_local; ++i) {
             Local& L = m->loc[i];
@@ -672,16 +750,7 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
         BSM_HIP_TRY(hipEventRecord(E[2], ctx->comm[i]));
         BSM_HIP_TRY(hipStreamWaitEvent(s, E[2], 0));
         BSM_HIP_TRY(hipEventRecord(E[3], s));
-        if (L.compacts) {
-            const uint64_t slot_rows = (uint64_t)m->P * m->pad;
-            BSM_TRY(exclusive_scan_i32_to_i64(L.nz, L.rp_pad, slot_rows, L.ws, L.ws_b, s));
-            BSM_TRY(compact_dispatch(m->dtype, slot_rows, k, L.y, L.rp_pad, L.ocol, L.oval, s));
-            if (m->squeeze) {
-                squeeze_row_ptr<<<(unsigned)((m->rows + 1 + 255) / 256), 256, 0, s>>>(L.rp_pad, L.bounds, m->P,
-                                                                                      m->pad, m->rows, L.rp_out);
-                BSM_HIP_TRY(hipGetLastError());
-            }
-        }
+        if (L.compacts && !ctx->external) BSM_TRY(compact_local(m, L, s));
         BSM_HIP_TRY(hipEventRecord(E[4], s));
         ++L.steps;
     }
@@ -690,6 +759,7 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
 
 int bsm_mcsr_sync(bsm_mcsr* m) {
     BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     for (int i = 0; i < m->ctx->n_local; ++i) {
         DeviceGuard g(m->loc[i].device);
         BSM_HIP_TRY(hipStreamSynchronize(m->ctx->compute[i]));
@@ -701,6 +771,7 @@ int bsm_mcsr_sync(bsm_mcsr* m) {
 int bsm_mcsr_step_times(bsm_mcsr* m, int local, int max, int* n, double* ms) {
     BSM_REQUIRE(m && n && local >= 0 && local < m->ctx->n_local && (max <= 0 || ms), BSM_ERR_INVALID,
                 "bsm_mcsr_step_times: bad argument");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     Local& L = m->loc[local];
     DeviceGuard g(L.device);
     *n = L.steps;
@@ -722,12 +793,14 @@ int bsm_mcsr_step_times(bsm_mcsr* m, int local, int max, int* n, double* ms) {
 
 void bsm_mcsr_reset_times(bsm_mcsr* m) {
     if (!m) return;
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     for (auto& L : m->loc) L.steps = 0;  // events are reused
 }
 
 int bsm_mcsr_copy_y(const bsm_mcsr* m, int local, void* y, int32_t* row_nnz) {
-    BSM_REQUIRE(m && m->prepared && local >= 0 && local < m->ctx->n_local, BSM_ERR_INVALID,
-                "bsm_mcsr_copy_y: bad argument");
+    BSM_REQUIRE(m && local >= 0 && local < m->ctx->n_local, BSM_ERR_INVALID, "bsm_mcsr_copy_y: bad argument");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_copy_y: prepare the matrix first");
     const Local& L = m->loc[local];
     DeviceGuard g(L.device);
     hipStream_t s = m->ctx->compute[local];
@@ -749,7 +822,9 @@ int bsm_mcsr_copy_y(const bsm_mcsr* m, int local, void* y, int32_t* row_nnz) {
 }
 
 int bsm_mcsr_output(const bsm_mcsr* m, bsm_csr** out) {
-    BSM_REQUIRE(m && out && m->prepared, BSM_ERR_INVALID, "bsm_mcsr_output: bad argument");
+    BSM_REQUIRE(m && out, BSM_ERR_INVALID, "bsm_mcsr_output: bad argument");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_output: prepare the matrix first");
     const Local& L = m->loc[0];
     DeviceGuard g(L.device);
     hipStream_t s = m->ctx->compute[0];
@@ -787,6 +862,10 @@ int bsm_mcsr_mul_dense(bsm_mcsr* m, uint64_t k, uint64_t x_rows, const void* con
     BSM_REQUIRE(m->cols == x_rows, BSM_ERR_DIMENSIONS, "IncorrectDimensions: cols %llu != rhs rows %llu",
                 (unsigned long long)m->cols, (unsigned long long)x_rows);
     bsm_multi* ctx = m->ctx;
+    BSM_REQUIRE(!ctx->external, BSM_ERR_UNSUPPORTED,
+                "bsm_mcsr_mul_dense: an external context has no communicator (bsm_mcsr_step, exchange the slots, "
+                "bsm_mcsr_compact)");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
     if (!m->prepared || m->k != k) BSM_TRY(bsm_mcsr_prepare(m, k, m->prepared ? m->schedule : 0, nullptr));
     // X to every local device (each over its own link, in parallel)
     std::vector<DBuf> xs(ctx->n_local);
@@ -801,6 +880,69 @@ int bsm_mcsr_mul_dense(bsm_mcsr* m, uint64_t k, uint64_t x_rows, const void* con
     BSM_TRY(bsm_mcsr_sync(m));
     for (auto& L : m->loc) L.steps = std::max(0, L.steps - 1);  // not a timed step
     return bsm_mcsr_output(m, out);
+}
+
+int bsm_mcsr_compact(bsm_mcsr* m) {
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "bsm_mcsr_compact: null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_compact: prepare the matrix first");
+    for (int i = 0; i < m->ctx->n_local; ++i) {
+        Local& L = m->loc[i];
+        if (!L.compacts) continue;
+        DeviceGuard g(L.device);
+        hipStream_t s = m->ctx->compute[i];
+        hipEvent_t e;  // after anything still queued on the communication stream
+        BSM_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        int rc = hipEventRecord(e, m->ctx->comm[i]) == hipSuccess && hipStreamWaitEvent(s, e, 0) == hipSuccess
+                     ? BSM_OK
+                     : BSM_ERR_HIP;
+        (void)hipEventDestroy(e);
+        if (rc != BSM_OK) {
+            set_error("bsm_mcsr_compact: stream ordering failed");
+            return rc;
+        }
+        BSM_TRY(compact_local(m, L, s));
+    }
+    return BSM_OK;
+}
+
+namespace {
+// slots [first, first + n) of the gathered Y and its row counts on local
+// device `local` <-> caller buffers (host or device); synchronous
+int slot_copy(const bsm_mcsr* m, int local, uint32_t first, uint32_t n, void* y, int32_t* nz, bool to_slots) {
+    BSM_REQUIRE(m && local >= 0 && local < m->ctx->n_local, BSM_ERR_INVALID, "bsm_mcsr_slot_*: bad argument");
+    BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_slot_*: prepare the matrix first");
+    BSM_REQUIRE((uint64_t)first + n <= m->P, BSM_ERR_INVALID, "bsm_mcsr_slot_*: slots [%u, %u) of %u", first,
+                first + n, m->P);
+    const Local& L = m->loc[local];
+    DeviceGuard g(L.device);
+    hipStream_t s = m->ctx->compute[local];
+    const uint64_t slot_b = m->pad * m->k * dtype_size(m->dtype);
+    char* ys = static_cast<char*>(L.y) + (uint64_t)first * slot_b;
+    int32_t* ns = L.nz + (uint64_t)first * m->pad;
+    const uint64_t yb = (uint64_t)n * slot_b, nb = (uint64_t)n * m->pad * sizeof(int32_t);
+    BSM_HIP_TRY(hipStreamSynchronize(m->ctx->comm[local]));
+    if (y && yb)
+        BSM_HIP_TRY(to_slots ? hipMemcpyAsync(ys, y, yb, hipMemcpyDefault, s)
+                             : hipMemcpyAsync(y, ys, yb, hipMemcpyDefault, s));
+    if (nz && nb)
+        BSM_HIP_TRY(to_slots ? hipMemcpyAsync(ns, nz, nb, hipMemcpyDefault, s)
+                             : hipMemcpyAsync(nz, ns, nb, hipMemcpyDefault, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    return BSM_OK;
+}
+}  // namespace
+
+int bsm_mcsr_slot_read(const bsm_mcsr* m, int local, uint32_t first, uint32_t n, void* y, int32_t* row_nnz) {
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    return slot_copy(m, local, first, n, y, row_nnz, false);
+}
+
+int bsm_mcsr_slot_write(bsm_mcsr* m, int local, uint32_t first, uint32_t n, const void* y, const int32_t* row_nnz) {
+    BSM_REQUIRE(m, BSM_ERR_INVALID, "null handle");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    return slot_copy(m, local, first, n, const_cast<void*>(y), const_cast<int32_t*>(row_nnz), true);
 }
 
 void bsm_mcsr_free(bsm_mcsr* m) { free_mcsr(m); }

@@ -1,15 +1,20 @@
-"""Row-block multi-GPU SpMM (BASELINE.json north_star).
+"""Multi-rank Csr::mul_dense with the caller's own transport
+(BASELINE.json north_star row split).
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
-The CSR is split into contiguous row blocks of (nearly) equal nnz; the dense
-RHS X is replicated on every rank; each rank computes its block of Y = A X
-with the local HIP kernels, and the full dense Y is assembled on every rank
-with ONE all-gather (equal-count blocks, padded). Per-row results do not
-depend on the partition (each row is reduced by one wavefront in entry
-order), so the assembled Y is bit-identical to the single-GPU one.
+The library's multi-GPU path (csrc/multi.hip, include/bsm.h "multi-GPU")
+cuts the CSR into P = chunks x world row blocks ("pieces"); piece c*world + r
+is computed by rank r in round c and lands in slot c*world + r of the
+gathered Y, which RCCL's in-place all-gathers fill on a context with a
+communicator. On an external context (``MultiGpu.external``: no
+communicator) ``MultiCsr.step`` stops after this rank's rounds and
+:func:`exchange_slots` moves the slots between the ranks over any
+torch.distributed process group (gloo here: host buffers). Every rank then
+holds exactly what the all-gathers would have left, and ``MultiCsr.compact``
+builds the output Csr through the same slot / padding / row_ptr squeeze code
+as the RCCL path.
 
-Only the partitioning / padding / assembly logic lives here; it is used by
-bench.py on GPUs and by tests/test_distributed_cpu.py with the gloo backend.
+:func:`partition_rows` restates the library's piece bounds
+(``bsm_partition_rows``) in Python for the CPU tests.
 """
 
 from __future__ import annotations
@@ -17,80 +22,86 @@ from __future__ import annotations
 import numpy as np
 
 
-def partition_rows_by_nnz(row_ptr, world: int) -> np.ndarray:
-    """Contiguous row bounds (world+1 entries) splitting nnz as evenly as a
-    row boundary allows: bound g is the first row whose start >= g*nnz/world
-    (binary search on row_ptr). Empty matrices split rows evenly."""
-    rp = np.asarray(row_ptr, dtype=np.int64)
+def partition_rows(row_ptr, pieces: int) -> np.ndarray:
+    """Contiguous row blocks of near-equal cost, a row costing its entries plus
+    c = max(1, nnz/rows) (csrc/multi.hip partition_by_cost): bound i is the
+    first row r with rows*rp[r] + r*max(nnz, rows) >= i*total/P, total =
+    nnz*rows + rows*max(nnz, rows). Exact integers (Python ints)."""
+    rp = [int(v) for v in np.asarray(row_ptr, dtype=np.uint64)]
     rows = len(rp) - 1
-    nnz = int(rp[-1]) if rows >= 0 else 0
-    if world < 1:
-        raise ValueError("world must be >= 1")
-    if nnz == 0:
-        return np.array([(rows * g) // world for g in range(world + 1)], dtype=np.int64)
-    targets = [(nnz * g) // world for g in range(world + 1)]
-    bounds = np.searchsorted(rp[:-1], targets, side="left").astype(np.int64)
+    if pieces < 1:
+        raise ValueError("pieces must be >= 1")
+    nnz = rp[-1] if rows >= 0 else 0
+    per_row = max(nnz, rows)
+    total = nnz * rows + rows * per_row
+    bounds = []
+    for i in range(pieces + 1):
+        target = total * i // pieces
+        lo, hi = 0, rows
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if rp[mid] * rows + mid * per_row >= target:
+                hi = mid
+            else:
+                lo = mid + 1
+        bounds.append(lo)
     bounds[0], bounds[-1] = 0, rows
-    return np.maximum.accumulate(bounds)
+    return np.maximum.accumulate(np.array(bounds, dtype=np.uint64))
 
 
-def partition_rows_even(rows: int, world: int) -> np.ndarray:
-    """Equal row counts (equal nnz when every row has the same length, as in
-    the C4 bench matrix); the last block is the short one."""
-    per = (rows + world - 1) // world
-    return np.array([min(rows, g * per) for g in range(world + 1)], dtype=np.int64)
+def exchange_slots(slots, world: int, rank: int, chunks: int, group=None) -> None:
+    """All-gather the gathered-Y slots of an external-context matrix over a
+    torch.distributed group: rank r's slots c*world + r (c < chunks) go to
+    every rank, in place, as ncclAllGather would put them.
 
-
-def padded_block_rows(bounds) -> int:
-    b = np.asarray(bounds)
-    return int(np.max(np.diff(b))) if len(b) > 1 else 0
-
-
-def all_gather_blocks(y_local_padded, group=None):
-    """All-gather equal-size (pad_rows x k) blocks -> (world*pad_rows x k)."""
+    `slots` has ``slot_read(first, n) -> (y, nz)`` and ``slot_write(first, y,
+    nz)`` (``MultiCsr`` or a host stand-in), host numpy arrays shaped (n,
+    piece_rows, k) and (n, piece_rows)."""
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
-    out = torch.empty((world * y_local_padded.shape[0],) + tuple(y_local_padded.shape[1:]),
-                      dtype=y_local_padded.dtype, device=y_local_padded.device)
-    dist.all_gather_into_tensor(out, y_local_padded.contiguous(), group=group)
-    return out
-
-
-def unpad_blocks(y_gathered, bounds, pad_rows: int):
-    """Drop the padding rows of each gathered block -> (rows x k)."""
-    import torch
-
-    b = np.asarray(bounds)
-    world = len(b) - 1
-    if world == 1 or np.all(np.diff(b)[:-1] == pad_rows):
-        return y_gathered[: int(b[-1])]  # only the last block can be short
-    parts = [y_gathered[g * pad_rows: g * pad_rows + int(b[g + 1] - b[g])] for g in range(world)]
-    return torch.cat(parts, dim=0)
-
-
-def partition_rows_cyclic(rows: int, world: int, chunks: int):
-    """Block-cyclic row partition for an all-gather overlapped with compute.
-
-    The rows are cut into `chunks` rounds of world*cr consecutive rows
-    (cr = ceil(rows / (chunks*world))); in round c rank g owns rows
-    [c*world*cr + g*cr, ... + cr), clipped to `rows`. Round c of every rank
-    is finished by the same SpMM launch, and the equal-count all-gather of
-    round c lands contiguously, already in global row order, at rows
-    [c*world*cr, (c+1)*world*cr) of the gathered buffer: no reordering copy,
-    and only the last round holds padding (rows >= `rows`, never read).
-
-    Returns (cr, [[(row0, nrows) for c in range(chunks)] for g in range(world)]);
-    nrows may be 0 for trailing pieces."""
-    if world < 1 or chunks < 1:
-        raise ValueError("world and chunks must be >= 1")
-    cr = -(-rows // (chunks * world)) if rows else 0
-    pieces = []
-    for g in range(world):
-        mine = []
+    mine_y, mine_nz = [], []
+    for c in range(chunks):
+        y, nz = slots.slot_read(c * world + rank, 1)
+        mine_y.append(y[0])
+        mine_nz.append(nz[0])
+    ty = torch.from_numpy(np.ascontiguousarray(np.stack(mine_y)))
+    tn = torch.from_numpy(np.ascontiguousarray(np.stack(mine_nz)))
+    # gloo gathers raw bytes fine; view floats as same-width integers so no
+    # backend ever touches the values (NaN payloads, -0.0 stay as they are)
+    iview = {8: torch.int64, 4: torch.int32, 2: torch.int16, 1: torch.uint8}[ty.element_size()]
+    ty_i = ty.view(iview)
+    all_y = [torch.empty_like(ty_i) for _ in range(world)]
+    all_n = [torch.empty_like(tn) for _ in range(world)]
+    dist.all_gather(all_y, ty_i, group=group)
+    dist.all_gather(all_n, tn, group=group)
+    for r in range(world):
+        if r == rank:
+            continue
+        yr = all_y[r].view(ty.dtype).numpy()
+        nr = all_n[r].numpy()
         for c in range(chunks):
-            r0 = c * world * cr + g * cr
-            mine.append((min(r0, rows), max(0, min(rows, r0 + cr) - r0)))
-        pieces.append(mine)
-    return cr, pieces
+            slots.slot_write(c * world + r, yr[c:c + 1], nr[c:c + 1])
+
+
+class HostSlots:
+    """Host stand-in of a matrix's gathered-Y slots (P slots of piece_rows x k),
+    with MultiCsr's slot_read / slot_write interface (CPU tests)."""
+
+    def __init__(self, pieces: int, piece_rows: int, k: int, dtype=np.float64):
+        self.y = np.zeros((pieces, piece_rows, k), dtype=dtype)
+        self.nz = np.zeros((pieces, piece_rows), dtype=np.int32)
+
+    def slot_read(self, first: int, n: int):
+        return self.y[first:first + n].copy(), self.nz[first:first + n].copy()
+
+    def slot_write(self, first: int, y, nz) -> None:
+        self.y[first:first + len(y)] = y
+        self.nz[first:first + len(nz)] = nz
+
+    def assembled(self, bounds) -> tuple:
+        """Y (rows x k) and row counts in global row order (bsm_mcsr_copy_y)."""
+        b = np.asarray(bounds, dtype=np.int64)
+        ys = [self.y[i, :b[i + 1] - b[i]] for i in range(len(b) - 1)]
+        ns = [self.nz[i, :b[i + 1] - b[i]] for i in range(len(b) - 1)]
+        return np.concatenate(ys), np.concatenate(ns)

@@ -90,19 +90,31 @@ class HostPool:
         self._free: list[_Mapping] = []
         self._free_bytes = 0
         self._mu = threading.RLock()  # a finalizer may run inside _take (GC)
+        self._busy = False
+        self._pending: list[_Mapping] = []
         self.hits = 0
         self.misses = 0
 
     def _take(self, nbytes: int) -> _Mapping:
         cap = -(-nbytes // _HUGE) * _HUGE
         with self._mu:
-            best = None
-            for i, m in enumerate(self._free):
-                # reuse when it wastes at most a quarter (+ one huge page)
-                if cap <= m.cap <= cap + cap // 4 + _HUGE and (best is None or m.cap < self._free[best].cap):
-                    best = i
-            if best is not None:
-                m = self._free.pop(best)
+            # give-backs that a finalizer (GC) runs on this thread while the
+            # list is scanned are queued and applied after the removal, so the
+            # chosen mapping is the one removed
+            self._busy = True
+            try:
+                best = None
+                for i, m in enumerate(self._free):
+                    # reuse when it wastes at most a quarter (+ one huge page)
+                    if cap <= m.cap <= cap + cap // 4 + _HUGE and (best is None or m.cap < self._free[best].cap):
+                        best = i
+                m = self._free.pop(best) if best is not None else None
+            finally:
+                self._busy = False
+                pending, self._pending = self._pending, []
+                for p in pending:
+                    self._give_back(p)
+            if m is not None:
                 self._free_bytes -= m.cap
                 self.hits += 1
                 return m
@@ -111,6 +123,9 @@ class HostPool:
 
     def _give_back(self, m: _Mapping) -> None:
         with self._mu:
+            if self._busy:
+                self._pending.append(m)
+                return
             self._free.append(m)
             self._free_bytes += m.cap
             while self._free_bytes > self.keep and self._free:

@@ -10,7 +10,11 @@ the C-ABI (csrc/multi.hip), where a Rust ``mul_dense`` reaches them too
 * :class:`MultiGpu` -- ``bsm_multi_create(n_gpus)`` (one process, n devices,
   ``ncclCommInitAll``) or, one process per GPU, ``MultiGpu.for_rank(id, world,
   rank, device)`` (``ncclCommInitRank``; rank 0 makes the id with
-  :func:`unique_id` and the caller ships it).
+  :func:`unique_id` and the caller ships it), or, with the caller's own
+  transport, ``MultiGpu.external(world, rank, device)`` (no communicator:
+  ``step`` runs this rank's rounds into its slots, the caller exchanges the
+  slots, e.g. :func:`basic_sparse_matrix_amd.distributed.exchange_slots` over
+  any torch.distributed backend, then ``compact``).
 * :class:`MultiCsr` -- a matrix partitioned over a context:
   ``upload`` (host arrays) or ``generate`` (bsm_synth.h, on each device),
   ``mul_dense_cols`` (host columns in, a device Csr out), and the device-level
@@ -30,6 +34,14 @@ from . import _lib
 
 SCHEDULES = {"auto": 0, "tiled": 1, "panel": 2}
 PLAN_KEYS = ("total", "tiled_count", "tiled_scan", "tiled_alloc", "tiled_write", "panel_plans", "buffers")
+
+
+def partition_rows(row_ptr, pieces: int) -> np.ndarray:
+    """bsm_partition_rows: the piece bounds the library uses (host only)."""
+    rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+    out = np.empty(pieces + 1, dtype=np.uint64)
+    _lib.check(_lib.load().bsm_partition_rows(_lib.ptr(rp), rp.size - 1, pieces, _lib.ptr(out)))
+    return out
 
 
 def unique_id() -> bytes:
@@ -66,6 +78,22 @@ class MultiGpu:
         buf = ctypes.create_string_buffer(uid, _lib.BSM_UNIQUE_ID_BYTES)
         _lib.check(lib.bsm_multi_create_rank(buf, world, rank, device, ctypes.byref(h)))
         return cls(_handle=h.value)
+
+    @classmethod
+    def external(cls, world: int, rank: int, device: int) -> "MultiGpu":
+        """bsm_multi_create_external: rank `rank` of `world` on `device`, no
+        RCCL communicator (the slots of the gathered Y move by the caller's
+        transport)."""
+        lib = _lib.require_device()
+        h = ctypes.c_void_p()
+        _lib.check(lib.bsm_multi_create_external(world, rank, device, ctypes.byref(h)))
+        return cls(_handle=h.value)
+
+    @property
+    def is_external(self) -> bool:
+        e = ctypes.c_int(0)
+        _lib.check(_lib.load().bsm_multi_is_external(self.handle, ctypes.byref(e)))
+        return bool(e.value)
 
     def broadcast(self, ptrs, nbytes: int, root: int = 0) -> None:
         """ncclBroadcast of `nbytes` from global rank `root` into ptrs[i] on
@@ -175,6 +203,30 @@ class MultiCsr:
         """The assembled Y (rows x k row-major) and per-row nonzero counts on
         local device `local` into caller device buffers (0 = skip)."""
         _lib.check(_lib.load().bsm_mcsr_copy_y(self.handle, local, y_ptr, nnz_ptr))
+
+    def compact(self) -> None:
+        """bsm_mcsr_compact: the gathered Y -> the output Csr (async; after the
+        slot exchange on an external context)."""
+        _lib.check(_lib.load().bsm_mcsr_compact(self.handle))
+
+    def slot_read(self, first: int, n: int, local: int = 0):
+        """Slots [first, first+n) of the gathered Y and its row counts on local
+        device `local` -> host arrays ((n, piece_rows, k) values, (n,
+        piece_rows) int32). Slot c*world + r is round c of rank r."""
+        k = self.k or 0
+        y = np.empty((n, self.piece_rows, k), dtype=self.dtype)
+        nz = np.empty((n, self.piece_rows), dtype=np.int32)
+        _lib.check(_lib.load().bsm_mcsr_slot_read(self.handle, local, first, n, _lib.ptr(y), _lib.ptr(nz)))
+        return y, nz
+
+    def slot_write(self, first: int, y, nz, local: int = 0) -> None:
+        """Host arrays shaped as slot_read's -> slots [first, first+len(y))."""
+        y = np.ascontiguousarray(y, dtype=self.dtype)
+        nz = np.ascontiguousarray(nz, dtype=np.int32)
+        n = y.shape[0]
+        if y.shape[1:] != (self.piece_rows, self.k or 0) or nz.shape != (n, self.piece_rows):
+            raise ValueError("slot arrays must be (n, piece_rows, k) and (n, piece_rows)")
+        _lib.check(_lib.load().bsm_mcsr_slot_write(self.handle, local, first, n, _lib.ptr(y), _lib.ptr(nz)))
 
     def output(self) -> "_lib.DeviceCsr":
         out = ctypes.c_void_p()

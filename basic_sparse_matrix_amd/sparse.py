@@ -453,7 +453,6 @@ class Csr(GetDims):
         short = [j for j, c in enumerate(cols) if len(c) < x_rows]
         if short:  # host logic: the reference panics here whatever runs the sums
             self._panic_on_short_columns(cols, short)
-        dev = self._device()
         lib = _lib.require_device()
         arrs = []
         for c in cols:
@@ -462,7 +461,9 @@ class Csr(GetDims):
                 a = np.concatenate([a, np.zeros(x_rows - a.shape[0], dtype=a.dtype)])
             arrs.append(np.ascontiguousarray(a[:x_rows]))
         if _multi.gpus() is not None:  # row blocks on n GPUs + RCCL all-gather (csrc/multi.hip)
+            # only the partitioned copy: no whole-matrix upload to the current device
             return Csr._from_device(self._multi_device().mul_dense_cols(arrs, x_rows))
+        dev = self._device()
         out = ctypes.c_void_p()
         _raise_for(lib.bsm_csr_mul_dense(dev.handle, len(arrs), x_rows, _lib.ptr_array(arrs), ctypes.byref(out)))
         return Csr._from_device(_lib.DeviceCsr(out.value))

@@ -263,8 +263,10 @@ int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y,
 
 /* ---- multi-GPU: row blocks + RCCL all-gather (north_star) ----
  * Csr::mul_dense (sparse.rs:426-446) has independent rows (:431-444), so the
- * CSR is cut into P = chunks x world contiguous row blocks of near-equal nnz
- * ("pieces"; bound i is the first row whose start is >= i*nnz/P). Piece
+ * CSR is cut into P = chunks x world contiguous row blocks ("pieces") of
+ * near-equal cost, a row costing its entries plus max(1, nnz/rows) (its output
+ * row): bsm_partition_rows. For equal row lengths that is the nnz split; on
+ * skewed matrices it keeps every piece under 2*rows/P + 1 rows. Piece
  * c*world + g belongs to global rank g and is computed in round c. Every
  * device keeps a replica of X. The dense Y blocks are assembled on every
  * device by RCCL all-gathers, one per round, in place and issued on a
@@ -280,14 +282,31 @@ int bsm_dev_compact(int dtype, uint64_t rows, uint64_t k, const void* y,
  *  - one process per GPU (bench.py under torch.distributed.run): rank 0 calls
  *    bsm_multi_unique_id, the caller ships the BSM_UNIQUE_ID_BYTES bytes to
  *    every rank, and each rank calls bsm_multi_create_rank (ncclCommInitRank).
+ *  - one process per rank with the caller's own transport (no RCCL
+ *    communicator): bsm_multi_create_external. bsm_mcsr_step then only runs
+ *    this rank's SpMM rounds into its slots of the gathered Y; the caller moves
+ *    the slots between ranks (bsm_mcsr_slot_read / _write: slot c*world + r is
+ *    round c of rank r, as the all-gather would place it) and calls
+ *    bsm_mcsr_compact. bsm_mcsr_mul_dense and bsm_multi_broadcast return
+ *    BSM_ERR_UNSUPPORTED on such a context.
  * Every rank of a communicator must make the same collective calls
- * (bsm_mcsr_mul_dense, bsm_mcsr_step, bsm_multi_broadcast) in the same order. */
+ * (bsm_mcsr_mul_dense, bsm_mcsr_step, bsm_multi_broadcast) in the same order.
+ * Threading: the calls on one bsm_mcsr are serialised by a lock held for the
+ * whole call (a mul_dense from several threads on one matrix runs one after
+ * the other); different matrices on one context may be driven from different
+ * threads only if the context's communicator is not in use by two of them at
+ * once (RCCL's rule for a communicator). */
 typedef struct bsm_multi bsm_multi;
 typedef struct bsm_mcsr bsm_mcsr;
 #define BSM_UNIQUE_ID_BYTES 128
 int bsm_multi_create(int n_gpus, const int* devices, bsm_multi** out);
 int bsm_multi_unique_id(void* id);
 int bsm_multi_create_rank(const void* id, int world, int rank, int device, bsm_multi** out);
+int bsm_multi_create_external(int world, int rank, int device, bsm_multi** out);
+int bsm_multi_is_external(const bsm_multi* ctx, int* external);
+/* The piece bounds the multi-GPU path uses (host only, no device needed):
+ * bounds[0..pieces] for row_ptr[0..rows]. */
+int bsm_partition_rows(const uint64_t* row_ptr, uint64_t rows, uint32_t pieces, uint64_t* bounds);
 /* world size, devices driven by this process, global rank of the first one */
 int bsm_multi_info(const bsm_multi* ctx, int* world, int* n_local, int* first_rank);
 /* Broadcast `bytes` from global rank `root` (its first local device's buffer)
@@ -345,6 +364,16 @@ void bsm_mcsr_reset_times(bsm_mcsr* m);
 int bsm_mcsr_copy_y(const bsm_mcsr* m, int local, void* y, int32_t* row_nnz);
 /* The last step's output Csr as a new handle on the first local device. */
 int bsm_mcsr_output(const bsm_mcsr* m, bsm_csr** out);
+/* The compaction of the gathered Y into the output Csr (asynchronous, on the
+ * compute stream; bsm_mcsr_step does it itself on a context with a
+ * communicator). For an external context, after the slot exchange. */
+int bsm_mcsr_compact(bsm_mcsr* m);
+/* Slots [first, first + n) of the gathered Y (each piece_rows x k values,
+ * ROW-major) and of its per-row nonzero counts (piece_rows int32 each) on local
+ * device `local`, to / from caller buffers, host or device (either may be
+ * NULL); synchronous. Slot c*world + r holds round c of rank r. */
+int bsm_mcsr_slot_read(const bsm_mcsr* m, int local, uint32_t first, uint32_t n, void* y, int32_t* row_nnz);
+int bsm_mcsr_slot_write(bsm_mcsr* m, int local, uint32_t first, uint32_t n, const void* y, const int32_t* row_nnz);
 void bsm_mcsr_free(bsm_mcsr* m);
 
 #ifdef __cplusplus

@@ -27,7 +27,7 @@ for step in "$@"; do
   case $step in
     tests) run gpu_tests 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 \
              --timeout-method thread --durations=8 || exit $? ;;
-    tests:*) run gpu_tests_sel 600 python -u -m pytest ${step#tests:} -m gpu -x -q -p no:cacheprovider \
+    tests:*) n=$((n + 1)); run gpu_tests_sel${n} 600 python -u -m pytest ${step#tests:} -m gpu -x -q -p no:cacheprovider \
              --timeout 150 --timeout-method thread --durations=8 || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench:*) IFS=: read -r _ cfg extra <<< "$step"

@@ -13,8 +13,9 @@ operation order; blocked = reassociated, within 1e-6 on f64) with
   once, against 8 TB/s);
 * the CPU baseline: the oracle's band restatement of the same solve (the
   reference's order, one thread; the literal O(N^4) reference loops are out
-  of reach beyond N ~ 256): at g = 1000 the measured run that made the
-  committed fixture, and g = 250, 500 measured here;
+  of reach beyond N ~ 256), timed on this host's cores on the leading 25 grid
+  rows of the system and scaled by N/R (per-row work is constant past the
+  first g rows), with a whole 250^2 solve beside it;
 * the error of x against x_true (and, for the reference order, bit-equality
   with the committed full-size oracle fixture, tests/golden/c5_poisson_1000.json).
 """
@@ -46,38 +47,55 @@ def system(g, dt):
     return rp, ci, v.astype(dt), b.astype(dt), x_true
 
 
-def cpu_baseline(fixture, sizes=(250, 500), target=1000):
+def leading_system(g, rows_g):
+    """The leading principal block of the g x g system: the first rows_g grid
+    rows (R = rows_g * g unknowns, band g). Its band Cholesky is the first R
+    rows of the full factor, and every row past the first g costs the same
+    (g^2/2 multiply-add pairs), so its time x N/R is the full solve's."""
+    rp, ci, v = orc.poisson2d(g)
+    R = rows_g * g
+    lo = rp[:R + 1].astype(np.int64)
+    keep = ci[:lo[-1]].astype(np.int64) < R
+    row_of = np.repeat(np.arange(R), np.diff(lo))
+    rp_s = np.concatenate([[0], np.cumsum(np.bincount(row_of[keep], minlength=R))]).astype(np.uint64)
+    ci_s, v_s = ci[:lo[-1]][keep], v[:lo[-1]][keep]
+    x_true = orc.gen_x_cols(1002, R, 1)[0]
+    b = np.zeros(R)
+    np.add.at(b, row_of[keep], v_s * x_true[ci_s.astype(np.int64)])
+    return R, rp_s, ci_s, v_s, b
+
+
+def cpu_baseline(fixture, g=1000, sample_rows_g=25, small=250):
     """The oracle's band restatement of solve (the reference's operation order,
-    one thread), timed here at 250^2 and 500^2. At 1000^2 the value is the
-    MEASURED run that made the committed fixture (scripts/make_c5_fixture.py:
-    factor passes + transpose + forward + backward, one thread of the build
-    container's CPU); the g^4 extrapolation from 500^2 is kept beside it as a
-    cross-check (it under-estimates: the band no longer fits the caches)."""
-    pts = {}
-    for g in sizes:
-        rp, ci, v, b, _ = system(g, np.float64)
-        t0 = time.perf_counter()
-        orc.solve(g * g, rp, ci, v, [b], band=True)
-        pts[g] = time.perf_counter() - t0
-    g_hi = max(sizes)
-    est = pts[g_hi] * (target / g_hi) ** 4
-    measured = None
-    if fixture and fixture.get("cpu_seconds") and target == 1000:
-        measured = float(sum(fixture["cpu_seconds"].values()))
+    one thread of THIS host: on the GPU box, the node's own cores) on a bounded
+    sample: the leading sample_rows_g grid rows of the g x g system (its factor
+    is the first rows of the full factor; transpose and the tri-solves are
+    linear in rows too), scaled by N/R. A whole small system (small^2) is
+    timed beside it. The full 1000^2 run of the build container (the committed
+    fixture's cpu_seconds) is kept as a cross-check."""
+    n = g * g
+    R, rp, ci, v, b = leading_system(g, sample_rows_g)
+    t0 = time.perf_counter()
+    orc.solve(R, rp, ci, v, [b], band=True)
+    t_sample = time.perf_counter() - t0
+    est = t_sample * n / R
+    rp2, ci2, v2, b2, _ = system(small, np.float64)
+    t0 = time.perf_counter()
+    orc.solve(small * small, rp2, ci2, v2, [b2], band=True)
+    t_small = time.perf_counter() - t0
+    container = float(sum(fixture["cpu_seconds"].values())) if fixture and fixture.get("cpu_seconds") else None
     return {
-        "value_s": round(measured if measured is not None else est, 2),
+        "value_s": round(est, 2),
         "unit": "s per solve",
         "cores": 1,
         "kind": "port",
-        "measured_s": {f"{g}x{g}": round(t, 3) for g, t in pts.items()},
-        "extrapolated_g4_s": round(est, 2),
-        "sample": (f"oracle band restatement of solve (lib.rs:11-24, reference operation order, C, -O2 "
-                   f"-ffp-contract=off, 1 thread): {target}^2 MEASURED when the committed fixture was made "
-                   f"(tests/golden/c5_poisson_1000.json cpu_seconds: factor passes, transpose, forward, backward; "
-                   f"the build container's CPU), {', '.join(f'{g}^2' for g in sizes)} measured here"
-                   if measured is not None else
-                   f"oracle band restatement of solve measured at {', '.join(f'{g}^2' for g in sizes)}; "
-                   f"{target}^2 EXTRAPOLATED from {g_hi}^2 by the g^4 (= N b^2) work law"),
+        "sample": (f"oracle band restatement of solve (lib.rs:11-24, reference operation order; C, -O2 "
+                   f"-ffp-contract=off, 1 thread) timed on this host on the leading {sample_rows_g} grid rows "
+                   f"of the {g}^2 system (R = {R:,} of N = {n:,} unknowns, band {g}: {t_sample:.2f} s), "
+                   f"x N/R = {n / R:g}"),
+        "sample_s": round(t_sample, 3),
+        "measured_s": {f"{small}x{small}": round(t_small, 3)},
+        "build_container_full_run_s": round(container, 1) if container else None,
         "host_cpus": os.cpu_count(),
     }
 
@@ -89,6 +107,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2, help="timed solves per order (after one warm-up)")
     ap.add_argument("--orders", default="reference,blocked")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-grid-rows", type=int, default=25,
+                    help="CPU baseline: leading grid rows of the system timed on this host (x N/R)")
     args = ap.parse_args()
     dt = np.float64 if args.dtype == "f64" else np.float32
     g = args.g
@@ -101,7 +121,7 @@ def main():
     if os.path.exists(fx_path) and args.dtype == "f64":
         with open(fx_path) as f:
             fixture = json.load(f)
-    cpu = None if args.no_cpu_baseline else cpu_baseline(fixture)
+    cpu = None if args.no_cpu_baseline else cpu_baseline(fixture, g, min(args.cpu_sample_grid_rows, g))
     es = np.dtype(dt).itemsize
     flops = float(n) * g * g  # sum over rows of b^2 / 2 multiply-add pairs, x 2
     band_bytes = float(es) * n * (g + 1)

@@ -1,21 +1,25 @@
-"""One rank of the multi-rank SpMM path that bench.py --gpus N runs
+"""One rank of the library's multi-GPU Csr::mul_dense at world > 1 on ONE GPU
 (launched as a fresh child process by tests/test_gpu_distributed.py; not a
 test module itself).
 
-Each rank generates its block-cyclic row pieces on the device
-(partition_rows_cyclic + DeviceCsrBlock.generate), runs the HIP SpMM on each
-piece (optionally with the column-panel plan), and all-gathers Y and the
-per-row nonzero counts round by round with async collectives, exactly as
-bench.py's step does. Rank 0 then recomputes the whole product on its own
-GPU in one piece and compares bit for bit, compacts the assembled Y into the
-output Csr, and checks a sampled row range against the CPU oracle
-(Csr::mul_dense, src/sparse.rs:426-446). The verdict is written as JSON to
-argv[1].
+Each rank makes an external context (bsm_multi_create_external: rank r of
+world on cuda:0, no RCCL communicator, since RCCL allows one rank per
+device) and the partitioned matrix (bsm_mcsr_upload of the oracle's host
+arrays, or bsm_mcsr_generate on the device), prepares the schedule asked
+for, runs bsm_mcsr_step (this rank's rounds into its slots c*world + r of the
+gathered Y), exchanges the slots with the other ranks over gloo
+(distributed.exchange_slots: what the in-place ncclAllGather of the RCCL path
+leaves), and compacts with bsm_mcsr_compact. So the library's own rank != 0
+slot placement, slot padding, row_ptr squeeze and compaction run with
+several ranks. Every rank's output Csr must be the same; rank 0 checks it
+bit for bit against the single-GPU bsm_csr_mul_dense and the CPU oracle
+(Csr::mul_dense, src/sparse.rs:426-446). The verdict goes to argv[1] as
+JSON.
 
-argv: out_json rows n_cols nnz_per_row k chunks panel_cols(0 = none, -1 = the
-tiled row-block x column-panel copy, forced, per piece)
+argv: out_json mode(upload|generate) rows n_cols kind a b k chunks schedule(auto|tiled|panel) dtype(f64|f32|i32)
 """
 
+import hashlib
 import json
 import os
 import sys
@@ -28,73 +32,111 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint64 if a.dtype.itemsize == 8 else np.uint32) if a.dtype.kind == "f" else a
+
+
+def same_csr(got, want):
+    rp, ci, v = got
+    erp, eci, ev = want
+    return bool(np.array_equal(np.asarray(rp, np.uint64), np.asarray(erp, np.uint64))
+                and np.array_equal(np.asarray(ci, np.uint64), np.asarray(eci, np.uint64))
+                and np.array_equal(bits(v), bits(np.asarray(ev, dtype=np.asarray(v).dtype))))
+
+
 def main():
-    out_json = sys.argv[1]
-    rows, n_cols, nnz_r, k, chunks, panel = (int(a) for a in sys.argv[2:8])
+    out_json, mode = sys.argv[1], sys.argv[2]
+    rows, n_cols, kind, a, b, k, chunks = (int(x) for x in sys.argv[3:10])
+    schedule, dts = sys.argv[10], sys.argv[11]
+    dtype = {"f64": np.float64, "f32": np.float32, "i32": np.int32}[dts]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)  # every rank shares the one GPU of the box
     dev = torch.device("cuda", 0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from basic_sparse_matrix_amd import _lib
-    from basic_sparse_matrix_amd.device import Compactor, DeviceCsrBlock, gen_dense
-    from basic_sparse_matrix_amd.distributed import partition_rows_cyclic
+    from basic_sparse_matrix_amd import Csr, Dense, _lib
+    from basic_sparse_matrix_amd.device import DeviceCsrBlock, gen_dense
+    from basic_sparse_matrix_amd.distributed import exchange_slots, partition_rows
+    from basic_sparse_matrix_amd.multi import MultiCsr, MultiGpu
+    from oracle import pyoracle as orc
 
-    cr, pieces = partition_rows_cyclic(rows, world, chunks)
-    blks = [DeviceCsrBlock.generate(1000, r0, n, n_cols, _lib.ROWLEN_UNIFORM, 0, 2 * nnz_r, _lib.VAL_UNIFORM,
-                                    np.float64, device=dev) for r0, n in pieces[rank]]
-    if panel == -1:
-        widths = [-1 if b.nnz and b.plan_tiled(k, force=True) is not None else 0 for b in blks]
+    ctx = MultiGpu.external(world, rank, 0)
+    assert ctx.is_external and (ctx.world, ctx.n_local, ctx.first_rank) == (world, 1, rank)
+    vk = 1 if np.dtype(dtype).kind == "i" else 0
+    res = {"rank": rank}
+    if mode == "upload":
+        rp, ci, v = orc.gen_csr(1000, rows, n_cols, kind, a, b, vk, dtype=np.float64)
+        v = v.astype(dtype)
+        x_cols = [c.astype(dtype) for c in orc.gen_x_cols(1001, n_cols, k, value_kind=vk)]
+        m = MultiCsr.upload(ctx, rows, n_cols, rp, ci, v, chunks=chunks)
+        x = torch.from_numpy(np.ascontiguousarray(np.stack(x_cols, axis=1) if k else
+                                                  np.zeros((n_cols, 0), dtype))).to(dev)
+        res["bounds_equal_mirror"] = bool(np.array_equal(m.bounds(), partition_rows(rp, chunks * world)))
     else:
-        widths = [b.plan(k, panel) if panel else 0 for b in blks]
-    x = gen_dense(1001, 0, n_cols, k, device=dev)
-    y_local = torch.full((chunks, cr, k), float("nan"), dtype=torch.float64, device=dev)
-    nnz_local = torch.full((chunks, cr), -1, dtype=torch.int32, device=dev)
-    y_full = torch.empty((chunks * world * cr, k), dtype=torch.float64, device=dev)
-    nnz_full = torch.empty(chunks * world * cr, dtype=torch.int32, device=dev)
-    works = []
-    rr = world * cr
-    for c, b in enumerate(blks):
-        if b.rows:
-            b.spmm(x, y_local[c, :b.rows], nnz_local[c, :b.rows])
-        torch.cuda.synchronize()  # gloo reads the tensors from the host side
-        works.append(dist.all_gather_into_tensor(y_full[c * rr:(c + 1) * rr], y_local[c], async_op=True))
-        works.append(dist.all_gather_into_tensor(nnz_full[c * rr:(c + 1) * rr], nnz_local[c], async_op=True))
-    for w in works:
-        w.wait()
+        assert dtype == np.float64, "generate mode: f64 (the bench's matrices)"
+        m = MultiCsr.generate(ctx, 1000, rows, n_cols, kind, a, b, 0, dtype, chunks=chunks)
+        x = gen_dense(1001, 0, n_cols, k, device=dev)
+    assert m.pieces == chunks * world
+    res["pieces"], res["piece_rows"] = m.pieces, m.piece_rows
+    bd = m.bounds().astype(np.int64)
+    res["squeeze"] = bool(np.any(np.diff(bd)[:-1] != m.piece_rows))
+    res["empty_pieces"] = int(np.sum(np.diff(bd) == 0))
+    m.prepare(k, schedule)
+    res["plan"] = m.plan_info()
     torch.cuda.synchronize()
-    res = {"rank": rank, "widths": widths}
+    outs = []
+    for it in range(2):  # a second step over the slots of the first exchange
+        m.step([x.data_ptr()])
+        m.sync()
+        exchange_slots(m, world, rank, chunks)
+        m.compact()
+        m.sync()
+        outs.append(m.output().download())
+    got = outs[-1]
+    res["steps_equal"] = same_csr(outs[0], got)
+    h = hashlib.sha256()
+    for arr in got:
+        h.update(np.ascontiguousarray(arr).tobytes())
+    digests = [None] * world
+    dist.all_gather_object(digests, h.hexdigest())
+    res["ranks_agree"] = len(set(digests)) == 1
     if rank == 0:
-        full = DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_UNIFORM, 0, 2 * nnz_r, _lib.VAL_UNIFORM,
-                                       np.float64, device=dev)
-        y_ref = torch.empty((rows, k), dtype=torch.float64, device=dev)
-        nnz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
-        full.spmm(x, y_ref, nnz_ref)
-        torch.cuda.synchronize()
-        res["y_equal"] = bool(torch.equal(y_ref.view(torch.int64), y_full[:rows].view(torch.int64)))
-        res["nnz_equal"] = bool(torch.equal(nnz_ref, nnz_full[:rows]))
-        comp = Compactor(rows, k, np.float64, device=dev)
-        comp(y_full[:rows], nnz_full[:rows])
-        torch.cuda.synchronize()
-        # oracle on a sampled row range of the assembled, compacted product
-        from oracle import pyoracle as orc
-
-        s0, sn = rows // 3, min(300, rows - rows // 3)
-        frp = orc.gen_row_ptr(1000, rows, n_cols, orc.ROWLEN_UNIFORM, 0, 2 * nnz_r)
-        ci, v = orc.gen_entries(1000, frp, n_cols, r0=s0, r1=s0 + sn)
-        lo, hi = int(frp[s0]), int(frp[s0 + sn])
-        lrp = (frp[s0:s0 + sn + 1] - frp[s0]).astype(np.uint64)
-        x_cols = orc.gen_x_cols(1001, n_cols, k)
-        erp, eci, ev = orc.mul_dense(sn, n_cols, lrp, ci[lo:hi], v[lo:hi], x_cols)
-        crp = comp.row_ptr.cpu().numpy()
-        a, e = int(crp[s0]), int(crp[s0 + sn])
-        res["oracle_rows"] = [s0, s0 + sn]
-        res["oracle_equal"] = bool(
-            np.array_equal((crp[s0:s0 + sn + 1] - crp[s0]).astype(np.uint64), erp)
-            and np.array_equal(comp.col[a:e].cpu().numpy().astype(np.uint64), eci)
-            and np.array_equal(comp.vals[a:e].cpu().numpy().view(np.uint64), ev.view(np.uint64)))
-        res["out_nnz"] = comp.nnz()
+        if mode == "upload":
+            want = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
+            res["oracle_equal"] = same_csr(got, want)
+            single = Csr.from_csr_arrays((rows, n_cols), rp, ci, v).mul_dense(
+                Dense.from_columns(x_cols) if k else Dense(0, n_cols, []))
+            res["single_equal"] = same_csr((single.row_index, single.col_index, single.v), want)
+        else:
+            # the assembled Y (slot order -> row order) against one block on
+            # the single-GPU kernel, and sampled rows against the oracle
+            tdt = torch.float64
+            y = torch.empty((rows, k), dtype=tdt, device=dev)
+            nz = torch.empty(rows, dtype=torch.int32, device=dev)
+            m.copy_y(0, y.data_ptr(), nz.data_ptr())
+            blk = DeviceCsrBlock.generate(1000, 0, rows, n_cols, kind, a, b, 0, dtype, device=dev)
+            y_ref = torch.empty((rows, k), dtype=tdt, device=dev)
+            nz_ref = torch.empty(rows, dtype=torch.int32, device=dev)
+            blk.spmm(x, y_ref, nz_ref)
+            torch.cuda.synchronize()
+            res["single_equal"] = bool(torch.equal(y.view(torch.int64), y_ref.view(torch.int64))
+                                       and torch.equal(nz, nz_ref))
+            rp_o, ci_o, v_o = got
+            grp = orc.gen_row_ptr(1000, rows, n_cols, kind, a, b)
+            xc = orc.gen_x_cols(1001, n_cols, k)
+            ok = int(rp_o[-1]) == int(nz_ref.sum().item())
+            for r in np.linspace(0, rows - 1, 60).astype(np.int64):
+                gci, gv = orc.gen_entries(1000, grp, n_cols, r0=int(r), r1=int(r) + 1)
+                a0, a1 = int(grp[r]), int(grp[r + 1])
+                srp = np.array([0, a1 - a0], np.uint64)
+                erp, eci, ev = orc.mul_dense(1, n_cols, srp, gci[a0:a1], gv[a0:a1], xc)
+                o0, o1 = int(rp_o[r]), int(rp_o[r + 1])
+                ok &= bool(np.array_equal(ci_o[o0:o1], eci) and np.array_equal(bits(v_o[o0:o1]), bits(ev)))
+            res["oracle_equal"] = ok
     dist.barrier()
+    del m
+    ctx.close()
     dist.destroy_process_group()
     with open(out_json, "w") as f:
         json.dump(res, f)

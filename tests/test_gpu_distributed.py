@@ -1,10 +1,16 @@
-"""The multi-rank SpMM path (BASELINE.json north_star config 4: rows
-partitioned across GPUs, RHS replicated, Y all-gathered) run
-on the GPU: 2 and 3 ranks as fresh child processes (gloo, all on cuda:0),
-each running the HIP SpMM on its block-cyclic row pieces exactly as
-bench.py's step does. The assembled Y and per-row counts must be bit-identical
-to the single-GPU product, and the compacted Csr equal to the CPU oracle on a
-sampled row range (rows are independent in src/sparse.rs:431-444).
+"""The library's multi-GPU Csr::mul_dense at world 2 and 3 (BASELINE.json
+north_star / configs[3]: rows partitioned across GPUs, X replicated, Y
+assembled) on the one GPU of the box.
+
+Each rank is a fresh process on cuda:0 with an external context
+(bsm_multi_create_external: RCCL allows one rank per device, so the slots of
+the gathered Y move over gloo instead of ncclAllGather; see
+tests/dist_spmm_worker.py). Everything else is the library's own multi-GPU
+code: the piece bounds, round c of rank r in slot c*world + r, the slot
+padding, the row_ptr squeeze over short pieces, empty pieces, the tiled and
+panelled schedules per piece, and the compaction. Rows are independent in
+the reference (src/sparse.rs:431-444), so the output Csr of every rank must
+be bit-identical to the single-GPU bsm_csr_mul_dense and to the oracle.
 """
 
 import json
@@ -29,25 +35,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,rows,n_cols,nnz_r,k,chunks,panel", [
-    (2, 20_011, 5_000, 12, 32, 3, 0),     # k = 32 rows kernel, clipped last round
-    (2, 20_011, 5_000, 12, 32, 3, 350),   # column-panel plan (15 panels of 350 columns)
-    (3, 9_001, 3_000, 6, 1, 3, 0),        # SpMV arm (k = 1)
-    (2, 4_099, 4_000, 40, 7, 3, 0),       # general-k kernel
-    (2, 20_011, 5_000, 12, 32, 3, -1),    # tiled copy per piece (k = 32), several batches: the batch pacing
-    (3, 9_001, 3_000, 6, 1, 2, -1),       # tiled copy, k = 1   barrier with two grids sharing the CUs
-])
-def test_block_cyclic_spmm_on_gpu_matches_single(tmp_path, world, rows, n_cols, nnz_r, k, chunks, panel):
+def _run(tmp_path, world, args, env_extra=None):
     port = _free_port()
     outs = [tmp_path / f"rank{r}.json" for r in range(world)]
     procs = []
     for r in range(world):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        if panel == -1:  # small batches so the pacing barrier is live
-            env.update(BSM_TILED_RW="64" if k == 32 else "40", BSM_TILED_WAVES="16")
-        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, str(outs[r]), str(rows), str(n_cols),
-                                       str(nnz_r), str(k), str(chunks), str(panel)], env=env,
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, str(outs[r])] + [str(a) for a in args], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     try:
@@ -59,10 +55,58 @@ def test_block_cyclic_spmm_on_gpu_matches_single(tmp_path, world, rows, n_cols, 
             if p.poll() is None:
                 p.kill()
     assert all(p.returncode == 0 for p in procs), logs
-    res = json.loads(outs[0].read_text())
-    if panel == -1:
-        assert any(w == -1 for w in res["widths"]), res  # the tiled kernel really ran
-    elif panel:
-        assert all(w == panel for w in res["widths"]), res  # the panelled kernel really ran
-    assert res["y_equal"] and res["nnz_equal"], res
-    assert res["oracle_equal"], res
+    return [json.loads(o.read_text()) for o in outs]
+
+
+# rows, n_cols, kind, a, b, k, chunks, schedule, dtype
+UPLOAD_CASES = [
+    (2, 3000, 2000, 1, 0, 40, 32, 1, "auto", "f64"),   # uneven pieces: squeeze
+    (2, 3000, 2000, 1, 0, 40, 32, 3, "auto", "f64"),
+    (3, 3000, 2000, 1, 0, 40, 32, 1, "auto", "f64"),
+    (3, 3001, 2000, 1, 0, 40, 32, 3, "panel", "f64"),
+    (3, 2000, 3000, 0, 20, 20, 32, 3, "auto", "f64"),  # equal pieces: no squeeze
+    (2, 1000, 5000, 1, 0, 7, 1, 3, "auto", "f64"),     # SpMV arm
+    (3, 777, 513, 1, 0, 20, 5, 2, "auto", "f32"),      # general k, f32
+    (2, 500, 400, 1, 1, 9, 3, 3, "auto", "i32"),       # integer (wrapping) sums
+    (3, 10, 30, 1, 0, 12, 2, 4, "auto", "f64"),        # 12 pieces for 10 rows: empty pieces
+    (2, 64, 64, 1, 0, 3, 0, 2, "auto", "f64"),         # k = 0: every output row empty
+]
+
+
+@pytest.mark.parametrize("world,rows,n_cols,kind,a,b,k,chunks,schedule,dtype", UPLOAD_CASES)
+def test_external_ranks_upload_match_single_and_oracle(tmp_path, world, rows, n_cols, kind, a, b, k, chunks,
+                                                       schedule, dtype):
+    res = _run(tmp_path, world, ["upload", rows, n_cols, kind, a, b, k, chunks, schedule, dtype])
+    r0 = res[0]
+    assert r0["pieces"] == world * chunks
+    assert all(r["ranks_agree"] and r["steps_equal"] and r["bounds_equal_mirror"] for r in res), res
+    assert r0["oracle_equal"] and r0["single_equal"], r0
+    if rows == 10:
+        assert r0["empty_pieces"] > 0
+    if kind == 1 and rows >= 1000:
+        assert r0["squeeze"], r0  # short pieces before the last: the row_ptr squeeze ran
+
+
+GEN_CASES = [
+    # tiled copy per piece (forced), small batches so the pacing barrier is live
+    # with two or three grids sharing the CUs
+    (2, 20_011, 5_000, 1, 0, 24, 32, 1, "tiled"),
+    (3, 20_011, 5_000, 1, 0, 24, 32, 3, "tiled"),
+    (3, 9_001, 3_000, 1, 0, 12, 1, 2, "tiled"),       # tiled k = 1
+    (2, 20_011, 30_000, 1, 0, 24, 32, 3, "panel"),    # never the copy
+]
+
+
+@pytest.mark.parametrize("world,rows,n_cols,kind,a,b,k,chunks,schedule", GEN_CASES)
+def test_external_ranks_generate_schedules(tmp_path, world, rows, n_cols, kind, a, b, k, chunks, schedule):
+    env = {"BSM_TILED_RW": "64" if k == 32 else "40", "BSM_TILED_WAVES": "16"} if schedule == "tiled" else {}
+    res = _run(tmp_path, world, ["generate", rows, n_cols, kind, a, b, k, chunks, schedule, "f64"], env)
+    r0 = res[0]
+    assert all(r["ranks_agree"] and r["steps_equal"] for r in res), res
+    assert r0["single_equal"] and r0["oracle_equal"], r0
+    for r in res:
+        assert r["plan"]["local_pieces"] == chunks
+        if schedule == "tiled":
+            assert r["plan"]["tiled_pieces"] == chunks, r  # the copy really ran on every piece
+        else:
+            assert r["plan"]["tiled_pieces"] == 0, r

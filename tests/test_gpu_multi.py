@@ -231,3 +231,81 @@ def test_bench_under_torchrun_nccl(chunks):
     assert line["verified_vs_single_gpu"] is True and line["verified_rows"] == 1_000_000
     assert "RCCL" in line["config"]["comm"] and "nccl" in line["config"]["comm"]
     assert line["n_gpus"] == 1 and line["value"] > 0
+
+
+def test_multi_skewed_rows_pieces_capped(ctx, orc):
+    """nnz-balanced pieces on a matrix with a long run of empty rows
+    gave one piece nearly every row, and every device P x the single-GPU Y.
+    The cost split (a row costs its entries + max(1, nnz/rows)) caps a piece
+    at 2*rows/P + 1 rows; the product stays bit-exact."""
+    rows, cols, k, chunks = 10_000, 3000, 32, 4
+    lens = np.concatenate([np.zeros(9000, np.int64), np.full(1000, 60)])
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    rng = np.random.default_rng(3)
+    ci = np.concatenate([np.sort(rng.choice(cols, 60, replace=False)) for _ in range(1000)]).astype(np.uint64)
+    v = rng.uniform(0.5, 1.5, ci.size)
+    x_cols = orc.gen_x_cols(1001, cols, k)
+    m = MultiCsr.upload(ctx, rows, cols, rp, ci, v, chunks=chunks)
+    assert m.piece_rows <= 2 * rows / chunks + 1, m.piece_rows
+    assert_same_csr(m.mul_dense_cols(x_cols, cols).download(), orc.mul_dense(rows, cols, rp, ci, v, x_cols))
+
+
+def test_multi_concurrent_calls_one_matrix(ctx, orc):
+    """calls on one bsm_mcsr from several threads (a cached
+    partition reached from &self) are serialised by the handle's lock; with
+    different k each call re-prepares, so without it one call would free the
+    buffers under the other."""
+    import threading
+
+    rows, cols = 3000, 2000
+    rp, ci, v = orc.gen_csr(1000, rows, cols, 1, 0, 30)
+    m = MultiCsr.upload(ctx, rows, cols, rp, ci, v, chunks=2)
+    xs = {k: orc.gen_x_cols(1001, cols, k) for k in (1, 8, 32)}
+    want = {k: orc.mul_dense(rows, cols, rp, ci, v, x) for k, x in xs.items()}
+    errors = []
+
+    def run(k):
+        try:
+            for _ in range(4):
+                assert_same_csr(m.mul_dense_cols(xs[k], cols).download(), want[k])
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    th = [threading.Thread(target=run, args=(k,)) for k in (1, 8, 32, 8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors
+
+
+def test_external_context_world1_and_refusals(orc):
+    """bsm_multi_create_external at world 1: step fills every slot itself; the
+    exchange is a no-op, compact builds the output. mul_dense and broadcast
+    need a communicator and say so."""
+    c = MultiGpu.external(1, 0, 0)
+    assert c.is_external
+    rows, cols, k = 2000, 3000, 32
+    rp, ci, v = orc.gen_csr(1000, rows, cols, 1, 0, 30)
+    x_cols = orc.gen_x_cols(1001, cols, k)
+    m = MultiCsr.upload(c, rows, cols, rp, ci, v, chunks=3)
+    m.prepare(k)
+    x = torch.from_numpy(np.ascontiguousarray(np.stack(x_cols, axis=1))).cuda()
+    m.step([x.data_ptr()])
+    m.sync()
+    y, nz = m.slot_read(0, m.pieces)
+    assert y.shape == (m.pieces, m.piece_rows, k)
+    m.slot_write(0, y, nz)  # round trip
+    m.compact()
+    m.sync()
+    assert_same_csr(m.output().download(), orc.mul_dense(rows, cols, rp, ci, v, x_cols))
+    with pytest.raises(_lib.BsmError) as e:
+        m.mul_dense_cols(x_cols, cols)
+    assert e.value.code == _lib.BSM_ERR_UNSUPPORTED
+    with pytest.raises(_lib.BsmError) as e:
+        c.broadcast([x.data_ptr()], 8, 0)
+    assert e.value.code == _lib.BSM_ERR_UNSUPPORTED
+    with pytest.raises(_lib.BsmError):
+        m.slot_read(m.pieces, 1)  # past the last slot
+    del m
+    c.close()

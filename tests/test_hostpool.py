@@ -61,3 +61,32 @@ def test_module_empty_small_and_disabled(monkeypatch):
     monkeypatch.setenv("BSM_HOST_POOL", "0")
     big = hostpool.empty(4 << 20, np.float64)
     assert big.base is None and big.size == 4 << 20
+
+
+def test_give_back_during_take_scan_keeps_the_chosen_mapping():
+    """a give-back (a finalizer run by GC on the same thread) while
+    _take scans the free list must not make it remove a different mapping."""
+    H = 2 << 20
+    p = hostpool.HostPool(64 * H)
+    small, big = hostpool._Mapping(2 * H), hostpool._Mapping(4 * H)
+    p._give_back(small)
+    p._give_back(big)
+    late = hostpool._Mapping(2 * H)
+
+    class Hooked(list):
+        fired = False
+
+        def __iter__(self):
+            it = super().__iter__()
+            for m in it:
+                if not Hooked.fired:
+                    Hooked.fired = True
+                    p._give_back(late)  # lands while the scan runs
+                yield m
+
+    p._free = Hooked(p._free)
+    got = p._take(4 * H)  # only `big` fits (small is too small, late arrives mid-scan)
+    assert got is big
+    assert any(m is small for m in p._free) and any(m is late for m in p._free)
+    assert not any(m is big for m in p._free)
+    assert p.free_bytes == 4 * H
