@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 
 namespace bsm {
@@ -644,6 +645,18 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     BSM_TRY(current_device(&dev));
     int cus = 0;
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    // a CU-masked stream (multi.hip leaves CUs to the all-gathers): one
+    // workgroup per CU the stream may use, so the persistent grid stays resident
+    if (s && cus > 0) {
+        std::vector<uint32_t> mk((size_t)(cus + 31) / 32, 0u);
+        if (hipExtStreamGetCUMask(s, (uint32_t)mk.size(), mk.data()) == hipSuccess) {
+            int n = 0;
+            for (int i = 0; i < cus; ++i) n += (mk[i / 32] >> (i % 32)) & 1u;
+            if (n > 0 && n < cus) cus = n;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     // k = 32: BSM_TILED_HALF=1 selects the two half-width passes (8 waves per CU)
     const uint32_t half = k == 32 && !f32 && !wide && env_u32("BSM_TILED_HALF", 0) == 1 ? 1u : 0u;
     const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : (half ? HALF_WAVES_PER_CU : 4u);

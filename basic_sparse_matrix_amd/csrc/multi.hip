@@ -200,13 +200,41 @@ void free_local_buffers(Local& L) {
     L.steps = 0;
 }
 
+// CUs per XCD left to the communication stream (the all-gathers), the
+// compute stream masked to the rest: the SpMM's persistent grid holds every CU
+// it may use (LDS full, one wave per SIMD), so without a mask an all-gather
+// issued beside the next round's SpMM waits for it, or holds CUs that grid
+// then lacks. BSM_COMM_CUS=n (default 0 = no masks). The mask's bit order
+// is BSM_CU_MASK_ORDER: "xcd" (bit i on XCD i % 8; default) or "linear"
+// (bits [32x, 32x + 32) on XCD x). scripts/perf/cu_mask_probe.hip shows which.
+int comm_cus_per_xcd() {
+    const char* e = getenv("BSM_COMM_CUS");
+    return e ? std::max(0, atoi(e)) : 0;
+}
+
 int create_streams(bsm_multi* c) {
     c->compute.assign(c->n_local, nullptr);
     c->comm.assign(c->n_local, nullptr);
+    const int keep = comm_cus_per_xcd();
+    const char* ord = getenv("BSM_CU_MASK_ORDER");
+    const bool linear = ord && std::string(ord) == "linear";
     for (int i = 0; i < c->n_local; ++i) {
         DeviceGuard g(c->devices[i]);
-        BSM_HIP_TRY(hipStreamCreateWithFlags(&c->compute[i], hipStreamNonBlocking));
-        BSM_HIP_TRY(hipStreamCreateWithFlags(&c->comm[i], hipStreamNonBlocking));
+        int cus = 0;
+        BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->devices[i]));
+        const int per_xcd = cus / 8;
+        if (keep > 0 && keep < per_xcd && cus % 8 == 0) {
+            std::vector<uint32_t> mc((size_t)(cus + 31) / 32, 0u), mm(mc.size(), 0u);
+            for (int b = 0; b < cus; ++b) {
+                const int in_xcd = linear ? b % per_xcd : b / 8;
+                (in_xcd < keep ? mm : mc)[b / 32] |= 1u << (b % 32);
+            }
+            BSM_HIP_TRY(hipExtStreamCreateWithCUMask(&c->compute[i], (uint32_t)mc.size(), mc.data()));
+            BSM_HIP_TRY(hipExtStreamCreateWithCUMask(&c->comm[i], (uint32_t)mm.size(), mm.data()));
+        } else {
+            BSM_HIP_TRY(hipStreamCreateWithFlags(&c->compute[i], hipStreamNonBlocking));
+            BSM_HIP_TRY(hipStreamCreateWithFlags(&c->comm[i], hipStreamNonBlocking));
+        }
     }
     return BSM_OK;
 }

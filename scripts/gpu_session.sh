@@ -3,7 +3,7 @@
 # STEP: tests | tests:<paths> | smoke | bench:<config>[:extra bench args] | prof:<config>[:extra]
 #       | pmc:<config>:<COUNTER[,COUNTER...]>[:extra] | c5 | gather | torchrun:<config>[:extra]
 #       | py:<script args> | profpy:<name>:<script args> (the script under rocprofv3 --kernel-trace --stats)
-#       | env:VAR=VALUE (for the later steps) | unenv:VAR
+#       | cmd:<program args> (a built binary, e.g. a probe) | env:VAR=VALUE (for the later steps) | unenv:VAR
 # Every step runs under its own time limit; the session stops at the first
 # failing step (no retries).
 set -u
@@ -47,6 +47,7 @@ for step in "$@"; do
                     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --config $cfg $extra || exit $? ;;
     c5) run c5 600 python scripts/solve_c5.py || exit $? ;;
     py:*) n=$((n + 1)); run py${n} 600 python ${step#py:} || exit $? ;;
+    cmd:*) n=$((n + 1)); run cmd${n} 300 ${step#cmd:} || exit $? ;;
     profpy:*) IFS=: read -r _ nm args <<< "$step"
               run profpy_$nm 600 rocprofv3 --kernel-trace --stats -d $OUT/profpy_${nm}_$TAG -o run \
                   --output-format csv -- python $args || exit $? ;;
