@@ -3999,7 +3999,14 @@ static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const 
             band_backward_reg<T, SEG, NL, true><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
         };
         const BwCfg c = band_walk_cfg(b);
-        if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
+        // BSM_BW_SEG=25|40|50 (A/B, 896 < b <= 1000): longer segments on fewer
+        // lanes, the same W = 1000 terms in the same order (fewer lane hops,
+        // more registers per lane)
+        static const int bw_seg = getenv("BSM_BW_SEG") ? atoi(getenv("BSM_BW_SEG")) : 0;
+        if (c.seg == 20 && bw_seg == 25) go.template operator()<25, 40>();
+        else if (c.seg == 20 && bw_seg == 40) go.template operator()<40, 25>();
+        else if (c.seg == 20 && bw_seg == 50) go.template operator()<50, 20>();
+        else if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
         else if (c.seg == 1) go.template operator()<1, 64>();
         else if (c.seg == 2) go.template operator()<2, 64>();
         else if (c.seg == 4) go.template operator()<4, 64>();
