@@ -1466,8 +1466,10 @@ __device__ __forceinline__ T lane_walk(const T (&p)[SEG], std::integer_sequence<
 
 // (SEG, NL) of band_backward_reg for bandwidth b: NL lanes of SEG terms,
 // W = SEG * NL >= b terms walked per row. Fewer, longer segments save lane
-// hops (3 instructions each) but cost registers; (20, 50) is exact for the
-// C5 band (b = 1000). The band is stored with ld = max(b, W) + 1.
+// hops (3 instructions each) but cost registers; (40, 25) walks exactly the
+// C5 band (b = 1000): 2,428 ms at C5 against 2,488 for (20, 50) and 2,669
+// for (25, 40), same box (profiles/r04_b_*). The band is stored with
+// ld = max(b, W) + 1.
 struct BwCfg {
     int seg, nl;
 };
@@ -1478,7 +1480,7 @@ inline BwCfg band_walk_cfg(int64_t b) {
     if (b <= 512) return {8, 64};
     if (b <= 768) return {12, 64};
     if (b <= 896) return {16, 56};
-    if (b <= 1000) return {20, 50};
+    if (b <= 1000) return {40, 25};
     if (b <= 1024) return {16, 64};
     if (b <= 2048) return {32, 64};
     return {0, 0};
@@ -2295,7 +2297,7 @@ template <typename T, bool NR1 = false>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
                                                 int* status, int tid, unsigned long long* tdbg = nullptr,
                                                 T* __restrict__ dpub = nullptr, int* rbf = nullptr,
-                                                int* pflag = nullptr) {
+                                                int* pflag = nullptr, T* __restrict__ p3 = nullptr) {
     long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
     asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2357,6 +2359,16 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];  // Di[p][row][col]
 #pragma unroll
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
+            if (p3 && p == 3) {
+                // BSM_BLK_PROG=2: Di[3] out at once, with its own flag (rbf[3]):
+                // the next tile's last column block needs only it (and L's
+                // blocks (3, c) < 3, published with Linv's row blocks)
+                if ((tid & 63) < 16) {
+#pragma unroll
+                    for (int q2 = 0; q2 < 16; ++q2) st_sc1(&p3[768 + q2 * 16 + r], x[q2]);
+                }
+                blk_publish_flag(rbf, 3, tid & 63);
+            }
         }
         // pflag: the caller's global stores (the sub-diagonal tile) drain on
         // every wave during block 0's factor; the flag follows the barrier
@@ -2365,6 +2377,13 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
         const long long t1 = tdbg ? clock64() : 0;
         if (pflag && p == 0 && tid == 192) __hip_atomic_store(pflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (dpub && w == 3 && p >= 1) blk_publish_rowblock<T>(Q, dpub, p - 1, tid & 63);
+        if (p3 && w == 3 && p >= 1) {  // L's block (3, p - 1), final since panel p - 1: raised with rbf[p - 1]
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = (tid & 63) + 64 * u;
+                st_sc1(&p3[(p - 1) * 256 + i], (T)P[(48 + (i >> 4)) * TLD + 16 * (p - 1) + (i & 15)]);
+            }
+        }
         // 2. rows below the block, one 16-row block per wave on f64 MFMA
         //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
         const int l = tid & 63, m = l & 15, kq = l >> 4;
@@ -2623,7 +2642,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                                 int* __restrict__ ticket, int* __restrict__ status,
                                                 unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
                                                 int panels, T* __restrict__ pend, int* __restrict__ pendf,
-                                                int chain_mode, int* __restrict__ rbf) {
+                                                int chain_mode, int* __restrict__ rbf, T* __restrict__ pub3) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
     __shared__ T AT[64][TLD];  // the dataflow chain: S_{K,K-1}^T, then L_{K,K-1}^T in place
@@ -3068,8 +3087,49 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
 #pragma unroll
                 for (int q = 0; q < 4; ++q) ca[cb][q] = (double)acc[cb][q];
             const T* dk = Dinv + (K - 1) * 4096;
+            // BSM_BLK_PROG=2: column block 3 by the triangular form
+            // L[:, 3] = (S[:, 3] - sum_{c<3} L[:, c] L_{K-1}[3][c]^T) Di[3]^T: the
+            // sum runs while tile K - 1 still factors its last panel, and only
+            // Di[3] (published by its wave 0 at once) is waited for
+            const T* p3k = pub3 ? pub3 + (K - 1) * 1024 : nullptr;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
+                if (p3k && c == 3) {
+                    bsm_d4 t3;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) t3[q] = (double)PT[48 + m][16 * w + kq + 4 * q];
+#pragma unroll
+                    for (int k4 = 0; k4 < 12; ++k4) {
+                        const int k = 4 * k4 + kq, cp = k4 >> 2;
+                        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)ATl[k * TLD + 16 * w + m],
+                                                                  (double)Tb[cp * 256 + m * 16 + (k - 16 * cp)], t3,
+                                                                  0, 0, 0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) AT[48 + m][16 * w + kq + 4 * q] = (T)t3[q];
+                    if (tdbg) cw0 = clock64();
+                    wait_flag(&rbf[(K - 1) * 4 + 3]);
+                    if (tdbg) cw1 = clock64();
+                    Di[tid] = ld_sc1(&p3k[768 + tid]);  // Di[3][row][col] of tile K - 1
+                    __syncthreads();
+                    if (tdbg) cs1 = clock64();
+                    bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) {
+                        const int k = 4 * k4 + kq;
+                        oc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)ATl[(48 + k) * TLD + 16 * w + m],
+                                                                  (double)Di[m * 16 + k], oc, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = rb + 4 * q, cc = 48 + cm;
+                        const T o = (T)oc[q];
+                        if (in_band(K, K - 1, r, cc)) st_sc1(&CB[band_idx(K, K - 1, r, cc)], o);
+                        AT[cc][r] = o;
+                    }
+                    __syncthreads();
+                    if (tdbg) cs2 = clock64();
+                } else {
                 if (tdbg && c == 3) cw0 = clock64();
                 wait_flag(c < 3 ? &rbf[(K - 1) * 4 + c] : &flags[(K - 1) * DM]);
                 if (tdbg && c == 3) cw1 = clock64();
@@ -3079,11 +3139,13 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                     const int i = tid + 256 * u, s = i >> 4, j = i & 15;
                     v[u] = s < 16 * c + 16 ? ld_sc1(&dk[s * 64 + 16 * c + j]) : (T)0;
                 }
+                const T l3 = p3k && c < 3 ? ld_sc1(&p3k[c * 256 + tid]) : (T)0;  // L_{K-1}'s block (3, c)
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = tid + 256 * u, s = i >> 4, j = i & 15;
                     if (s < 16 * c + 16) QT[s][16 * c + j] = v[u];
                 }
+                if (p3k && c < 3) Tb[c * 256 + tid] = l3;
                 __syncthreads();
                 if (tdbg && c == 3) cs1 = clock64();
                 bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
@@ -3102,6 +3164,7 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 }
                 __syncthreads();
                 if (tdbg && c == 3) cs2 = clock64();
+                }
 #pragma unroll
                 for (int k4 = 0; k4 < 4; ++k4) {
                     const int k = 16 * c + 4 * k4 + kq;
@@ -3175,7 +3238,8 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
                                          (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg,
                                          rbf ? Dinv + K * 4096 : nullptr, rbf ? rbf + K * 4 : nullptr,
-                                         rbf && sub ? &flags[(K - 1) * DM + 1] : nullptr);
+                                         rbf && sub ? &flags[(K - 1) * DM + 1] : nullptr,
+                                         rbf && pub3 ? pub3 + K * 1024 : nullptr);
             } else {  // one-wave factor; the inverse below
                 if (w == 0)
                     blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
@@ -3798,6 +3862,13 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const char* pge = getenv("BSM_BLK_PROG");
     const char* pe0 = getenv("BSM_BLK_PANELS");
     const bool prog = !chain && (!pge || atoi(pge) != 0) && (!pe0 || atoi(pe0) == 1);
+    // BSM_BLK_PROG=2: tile K also publishes L_K's blocks (3, c < 3) with Linv's
+    // row blocks and Di[3] the moment its last pivot block is factored; tile
+    // K + 1 forms its last column block by the triangular form against Di[3]
+    // (a reassociation: not the bits of modes 0 / 1, within the tolerance)
+    const bool prog2 = prog && pge && atoi(pge) == 2;
+    DBuf pub3;
+    if (prog2) BSM_TRY(pub3.alloc((size_t)nb64 * 1024 * sizeof(T)));
     DBuf fl, pend;
     const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0) + (prog ? 4 * nb64 : 0));
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
@@ -3841,7 +3912,8 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const int panels = pe ? atoi(pe) : 1;
     kern<<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
                                                tdb.as<unsigned long long>(), panels, chain ? pend.as<T>() : nullptr,
-                                               pendf, chain_mode, prog ? rbf : nullptr);
+                                               pendf, chain_mode, prog ? rbf : nullptr,
+                                               prog2 ? pub3.as<T>() : nullptr);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());
@@ -3999,21 +4071,19 @@ static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const 
             band_backward_reg<T, SEG, NL, true><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
         };
         const BwCfg c = band_walk_cfg(b);
-        // BSM_BW_SEG=25|40|50 (A/B, 896 < b <= 1000): longer segments on fewer
-        // lanes, the same W = 1000 terms in the same order (fewer lane hops,
-        // more registers per lane)
+        // BSM_BW_SEG=20|25 (A/B, 896 < b <= 1000): other segment lengths over
+        // the same W = 1000 terms in the same order
         static const int bw_seg = getenv("BSM_BW_SEG") ? atoi(getenv("BSM_BW_SEG")) : 0;
-        if (c.seg == 20 && bw_seg == 25) go.template operator()<25, 40>();
-        else if (c.seg == 20 && bw_seg == 40) go.template operator()<40, 25>();
-        else if (c.seg == 20 && bw_seg == 50) go.template operator()<50, 20>();
-        else if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
+        if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
+        else if (c.seg == 40 && bw_seg == 25) go.template operator()<25, 40>();
+        else if (c.seg == 40 && bw_seg == 20) go.template operator()<20, 50>();
+        else if (c.seg == 40) go.template operator()<40, 25>();
         else if (c.seg == 1) go.template operator()<1, 64>();
         else if (c.seg == 2) go.template operator()<2, 64>();
         else if (c.seg == 4) go.template operator()<4, 64>();
         else if (c.seg == 8) go.template operator()<8, 64>();
         else if (c.seg == 12) go.template operator()<12, 64>();
         else if (c.seg == 16 && c.nl == 56) go.template operator()<16, 56>();
-        else if (c.seg == 20) go.template operator()<20, 50>();
         else if (c.seg == 16) go.template operator()<16, 64>();
         else go.template operator()<32, 64>();
     } else if (b <= 64)

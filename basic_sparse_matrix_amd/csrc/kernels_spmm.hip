@@ -346,13 +346,16 @@ __global__ __launch_bounds__(256) void spmm_k32_f64(int64_t rows, const int64_t*
 // a wave instruction still gathers four whole 256-B X rows, one per group.
 // U entries per group are in flight per iteration (clamped, unconditional
 // loads); the wave runs to the longest of its four rows.
-template <int U>
+// PROBE (measurement only, wrong results; BSM_SPMM_PROBE_MASK): every gather
+// reads X row (col & xmask), e.g. 0: the PMC calibration of the col / val
+// stream alone (the gathers all hit one line).
+template <int U, bool PROBE = false>
 __global__ __launch_bounds__(256) void spmm_k32_f64_rows4(int64_t rows, const int64_t* __restrict__ rp,
                                                           const int32_t* __restrict__ col,
                                                           const double* __restrict__ val,
                                                           const double2* __restrict__ X,
                                                           double2* __restrict__ Y,
-                                                          int32_t* __restrict__ row_nnz) {
+                                                          int32_t* __restrict__ row_nnz, uint32_t xmask = ~0u) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int g = lane >> 4, q = lane & 15;
     const int64_t row = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) * 4 + g;
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(256) void spmm_k32_f64_rows4(int64_t rows, const in
         }
         double2 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = X[(int64_t)c[u] * 16 + q];
+        for (int u = 0; u < U; ++u) x[u] = X[(int64_t)(PROBE ? (uint32_t)c[u] & xmask : (uint32_t)c[u]) * 16 + q];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double s0 = __dadd_rn(a0, __dmul_rn(v[u], x[u].x));
@@ -1009,7 +1012,11 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
             const bool short_rows = nnz <= SHORT_ROW_AVG * rows;
             if (variant == 5 || variant == 6 || (variant == 0 && short_rows)) {
                 const uint64_t nb4 = (rows + 15) / 16;
-                if (variant == 6)
+                static const char* pm = getenv("BSM_SPMM_PROBE_MASK");
+                if (pm)
+                    spmm_k32_f64_rows4<4, true><<<(unsigned)nb4, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz,
+                                                                              (uint32_t)strtoul(pm, nullptr, 10));
+                else if (variant == 6)
                     spmm_k32_f64_rows4<2><<<(unsigned)nb4, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);
                 else
                     spmm_k32_f64_rows4<4><<<(unsigned)nb4, 256, 0, s>>>(r, rp, col, vals, X2, Y2, row_nnz);

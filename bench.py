@@ -62,6 +62,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # faster than the L2 serves them.
 L2_GATHER_PEAK_GBS = 17_030.0  # 17.03 TB/s: "mode 2 ... 8191" line (0.987 ms for 6.57e7 entries)
 L2_GATHER_PEAK_SRC = "profiles/r03_gather_ceiling.log"
+# The Infinity-Cache-served rate of uniformly random 256-B X-row gathers (no
+# L2 re-use): the tiled loop at C4 with one panel (BSM_TILED_PSHIFT=24) and
+# every column folded into a 256 MB table (BSM_TILED_PROBE_MASK=2^20-1):
+# 2.56 TB in 358 ms (a 1 GB table: 357 ms, the same). C3's X is 256 MB and a
+# row meets ~0.2 other entries of its X rows per L2 lifetime, so its row kernel
+# is bound by this rate, not by the L2's.
+IC_GATHER_PEAK_GBS = 7_150.0
+IC_GATHER_PEAK_SRC = "profiles/r04_b_c4_ic_gather_probe.log"
+# k = 1 (C2, spmm_tiled_k1): the same kernel with every gather confined to one
+# L2-resident 2 MiB panel (BSM_TILED_K1_PROBE=262143): 59 us at C2, i.e. C2's
+# B_gather (216,000,008 B) at 3,661 GB/s. Each 8-B gather moves a 128-B line
+# into L1 that no other gather of the CU re-uses.
+K1_GATHER_PEAK_GBS = 3_661.0
+K1_GATHER_PEAK_SRC = "profiles/r02_f_c2_gather_probe.log"
 ROWLEN_CONST, ROWLEN_BINOMIAL = 0, 2  # bsm_synth.h row-length families
 SEED_A, SEED_X = 1000, 1001
 
@@ -76,6 +90,22 @@ def b_gather(rows, nnz, k, es=8):
     """SURVEY.md §8d traffic model: every nnz gathers its whole X row (no reuse
     beyond the caches): 8(N+1) + (4 + es) nnz + es nnz k + es N k."""
     return 8 * (rows + 1) + (4 + es) * nnz + es * nnz * k + es * rows * k
+
+
+def gather_ceiling(tiled, k, x_bytes):
+    """The gather ceiling that bounds this schedule (measured, per config):
+    the tiled k = 32 copy re-reads X panels from L2; a row kernel on an X
+    beyond L2 (C3: 256 MB) is served by the Infinity Cache; the tiled k = 1
+    copy (C2) moves a 128-B line per 8-B gather."""
+    if tiled and k == 1:
+        return {"bound": "l2_line_gather_k1", "peak": K1_GATHER_PEAK_GBS, "peak_source": K1_GATHER_PEAK_SRC,
+                "peak_model": "the same kernel, every gather in one L2-resident 2 MiB panel (BSM_TILED_K1_PROBE)"}
+    if not tiled and x_bytes > (32 << 20):
+        return {"bound": "ic_gather", "peak": IC_GATHER_PEAK_GBS, "peak_source": IC_GATHER_PEAK_SRC,
+                "peak_model": "uniformly random 256-B row gathers served by the Infinity Cache (256 MB table, no "
+                              "L2 re-use)"}
+    return {"bound": "l2_gather", "peak": L2_GATHER_PEAK_GBS, "peak_source": L2_GATHER_PEAK_SRC,
+            "peak_model": "the same inner loop on a static L2-resident X table"}
 
 
 def kernel_label(rows, nnz, k, panel_cols, tiled=False):
@@ -602,8 +632,13 @@ def main():
                 "rows": rows, "n_cols": n_cols, "nnz": nnz_total, "rhs_cols": k,
                 "parallelism": f"row-block x{world}, {chunks} round(s) of {world} nnz-balanced pieces",
                 "comm": comm,
-                "schedule": f"row-block x column-panel copy (spmm_tiled_k{k})" if tiled else
-                            ("column panels" if panel_cols else "one pass"),
+                "schedule": f"row-block x column-panel copy (spmm_tiled_k{k}; Y rows in LDS)" if tiled else
+                            ("column panels" if panel_cols else
+                             "one pass, row per wave" + (" (spmm_k32_f64_rows4, 4 rows per wave): no LDS X panel, "
+                                                          "since at 10 nnz/row an X row meets ~0.2 other entries per "
+                                                          "L2 lifetime; the LDS row-block copy measured 0.63 ms "
+                                                          "against 0.42 (profiles/r04_b_c3_rows4_vs_tiled.log)"
+                                                          if k == 32 and nnz_total <= 24 * rows else "")),
                 "panel_cols": pinfo["panel_cols"], "passes": n_passes,
                 "plan_ms": plan,
                 "generate_ms": round(gen_ms, 1),
@@ -637,17 +672,14 @@ def main():
                                   if key in pmc} if pmc else None,
                 "bytes_per_launch_alg": b_launch,
             },
-            "roofline_gather": {
-                "bound": "l2_gather",
-                "model": "B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row); peak = the "
-                         "measured L2-served gather rate of the same inner loop on a static L2-resident X table",
-                "achieved": round(achieved_gather, 2),
-                "peak": L2_GATHER_PEAK_GBS,
-                "peak_source": L2_GATHER_PEAK_SRC,
-                "unit": "GB/s",
-                "frac": round(achieved_gather / L2_GATHER_PEAK_GBS, 5),
-                "bytes_per_launch_gather": b_gather(my_rows, my_nnz, k, es),
-            },
+            "roofline_gather": dict(
+                gather_ceiling(tiled, k, n_cols * k * es),
+                model="B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row)",
+                achieved=round(achieved_gather, 2),
+                unit="GB/s",
+                frac=round(achieved_gather / gather_ceiling(tiled, k, n_cols * k * es)["peak"], 5),
+                bytes_per_launch_gather=b_gather(my_rows, my_nnz, k, es),
+            ),
             "end_to_end_ms": e2e,
             "cpu_baseline": cpu,
         }

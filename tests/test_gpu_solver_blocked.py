@@ -170,3 +170,31 @@ def test_blocked_progressive_publication_same_bits(orc, monkeypatch, dtype, g):
     for j in range(2):
         assert np.array_equal(xs["prog"][j].view(np.uint8), xs["whole"][j].view(np.uint8)), j
         assert np.array_equal(xs["prog"][j].view(np.uint8), xs["chain"][j].view(np.uint8)), j
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("g,k", [(9, 1), (40, 2), (70, 1), (130, 2), (250, 1)])
+def test_blocked_prog2_triangular_last_block(orc, monkeypatch, dtype, g, k):
+    """BSM_BLK_PROG=2: tile K + 1 forms its sub-diagonal tile's last column
+    block by the triangular form against Di[3] (published by tile K's wave 0
+    as soon as its last pivot block is factored) instead of Linv_K's last row
+    block. A reassociation: within the blocked path's tolerance of the band
+    oracle (the reference order) and of mode 1."""
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    v = v.astype(dtype)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    b = orc.gen_x_cols(1007, n, k, dtype=dtype)
+    ex = orc.solve(n, rp, ci, v, b, band=True)
+    xs = {}
+    for mode in ("1", "2"):
+        monkeypatch.setenv("BSM_BLK_PROG", mode)
+        x = solve(A, Dense.from_columns(b), order="blocked")
+        xs[mode] = [np.asarray(x.get_col(j)).copy() for j in range(k)]
+    for j in range(k):
+        if dtype == np.float64:
+            assert rel_err(xs["2"][j], ex[j]) < TOL[dtype], j
+            assert rel_err(xs["2"][j], xs["1"][j]) < TOL[dtype], j
+        else:
+            ref64 = orc.solve(n, rp, ci, v.astype(np.float64), [c.astype(np.float64) for c in b], band=True)[j]
+            assert rel_err(xs["2"][j], ref64) < TOL[dtype], j
