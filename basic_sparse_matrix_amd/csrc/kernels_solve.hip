@@ -917,6 +917,234 @@ __global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_
 }
 
 // ---------------------------------------------------------------------------
+// band_chol5 (round 4): band_chol4's tile events with FOUR rows per wave (4
+// waves, 256 threads, one wave per SIMD). A row-block spends most of each tile
+// in U, where every wave reads the staged column tile from LDS for its own
+// row (band_chol4: 16 waves x 16 steps x (M - m) slots of 512-B reads, 15.2k
+// cycles per tile at C5, LDS-bound, profiles/r01_ac_chol4_trace.log); here one
+// read of a column value feeds the wave's four rows, a quarter of the LDS
+// traffic. The row-blocks complete one per (T + U) of a tile (each row-block
+// walks its ~b/16 tiles in order behind the row-block above), so U is on the
+// factor's critical rate. T solves the four rows' chains interleaved. Per
+// element the same operations in the same order as band_chol4 and the
+// reference (ascending k, no FMA, (1/L[k][k]) * (A - sum)): the same bits.
+// ---------------------------------------------------------------------------
+template <typename T, int M, int RP>  // RP rows per wave: 16 / RP waves
+__global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
+                                                    T* __restrict__ R, int* __restrict__ fprog,
+                                                    int* __restrict__ status, int* __restrict__ ticket,
+                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
+    using A = Arith<T>;
+    constexpr int CS = 64 + 64 * M;
+    constexpr int C5_NT = 64 * (16 / RP);
+    __shared__ T colK[C4_TB][CS];
+    __shared__ T dTl[C4_TB][64];
+    __shared__ T rT[C4_TB];
+    __shared__ T aK[C4_TB][C4_TB];
+    __shared__ T hist[C4_TB][C4_TB + 1];
+    __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
+    __shared__ T xl[16];
+    __shared__ long long tph[16];
+    const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
+    for (int q = tid; q < C4_TB * 64; q += C5_NT) colK[q >> 6][q & 63] = A::zero();
+    const int ib = (int)b;
+    auto poll_all = [&](int jlo, int jhi, int need) {  // wave 0: fprog[J] >= need for J in [jlo, jhi)
+        bool ok = true;
+        for (int base = jlo; base < jhi; base += 64) {  // more than 64 row-blocks: several lanes' worth
+            const int J = base + c;
+            bool okj = J >= jhi;
+            long long spins = 0;
+            while (true) {
+                if (!okj) okj = __hip_atomic_load(&fprog[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+                if (__all(okj)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT ||
+                    ((spins & 1023) == 0 &&
+                     (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
+                    if (c == 0) atomicOr(status, ST_TIMEOUT);
+                    ok = false;
+                    break;
+                }
+            }
+            if (!ok) break;
+        }
+    };
+    __shared__ int s_tk;
+    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
+        const int i0 = (int)(I * C4_TB);
+        const int K0 = (i0 - ib > 0 ? i0 - ib : 0) / C4_TB, jb = C4_TB * K0;
+        const int r0 = RP * w;  // this wave's rows: i0 + r0 .. i0 + r0 + 3
+        long long tlast = 0;
+        const bool tr0 = trace && tid == 0;
+        if (tr0) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) tph[q] = 0;
+            tlast = clock64();
+        }
+        auto mark = [&](bool last, int ph) {
+            if (tr0) {
+                const long long t = clock64();
+                if (last) tph[6 + ph] += t - tlast;
+                else tph[ph] += t - tlast;
+                tlast = t;
+            }
+        };
+        T acc[RP][M];
+#pragma unroll
+        for (int q = 0; q < RP; ++q)
+#pragma unroll
+            for (int m = 0; m < M; ++m) acc[q][m] = A::zero();
+        T accT[RP], aT[RP];
+#pragma unroll
+        for (int q = 0; q < RP; ++q) {
+            const int rw = r0 + q;
+            accT[q] = A::zero();
+            aT[q] = (c < C4_TB && c <= rw && rw - c <= ib && i0 + rw < n) ? CB[(int64_t)(i0 + c) * ld + (rw - c)]
+                                                                         : A::zero();
+        }
+        auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
+#pragma unroll 1
+            for (int e = 0; e < 4; ++e) {
+                const int K = K0 + 4 * m + e;
+                if (K >= (int)I) return;
+                const int k0 = C4_TB * K, lb = 16 * e;
+                const bool lastK = K == (int)I - 1;
+                // ---------------- T: this row-block's tile K
+                if (w == 0) poll_all(K, K + 1, K + 1);
+                mark(lastK, 0);
+                __syncthreads();
+#pragma unroll
+                for (int u4 = 0; u4 < C4_TB * 64 / C5_NT; ++u4) {  // the diagonal tile of K, per lane of the slot
+                    const int el = tid + C5_NT * u4, t = el >> 6, cc = el & 63, u = cc - lb - t;
+                    T v = A::zero();
+                    if (u >= 1 && t + u <= 15 && u <= ib) v = ld_sc1(CB + (int64_t)(k0 + t) * ld + u);
+                    dTl[t][cc] = v;
+                }
+                for (int el = tid; el < C4_TB * C4_TB; el += C5_NT) {
+                    const int rr = el >> 4, t = el & 15, d = i0 + rr - k0 - t;
+                    T v = A::zero();
+                    if (d <= ib && i0 + rr < n) v = CB[(int64_t)(k0 + t) * ld + d];
+                    aK[rr][t] = v;
+                }
+                if (tid < C4_TB) rT[tid] = ld_sc1(&R[k0 + tid]);
+                __syncthreads();
+                mark(lastK, 1);
+                T myR = rT[c & 15], myA[RP];
+#pragma unroll
+                for (int q = 0; q < RP; ++q) myA[q] = aK[r0 + q][c & 15];
+                T xv[RP];
+#pragma unroll
+                for (int q = 0; q < RP; ++q) xv[q] = A::zero();
+#pragma unroll
+                for (int t = 0; t < C4_TB; ++t) {
+                    asm volatile("" : "+v"(myR));
+                    const T dv = dTl[t][c];
+                    const T rt = readlane_t(myR, t);
+#pragma unroll
+                    for (int q = 0; q < RP; ++q) {
+                        asm volatile("" : "+v"(myA[q]));
+                        const T sq = readlane_t(acc[q][m], lb + t);
+                        const T x = A::mul(rt, A::sub(readlane_t(myA[q], t), sq));
+                        acc[q][m] = A::add(acc[q][m], A::mul(x, dv));
+                        if (c == t) xv[q] = x;
+                    }
+                }
+                if (c < C4_TB) {
+#pragma unroll
+                    for (int q = 0; q < RP; ++q) {
+                        const int rw = r0 + q;
+                        hist[c][rw] = xv[q];
+                        const int d = i0 + rw - k0 - c;
+                        if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + c) * ld + d], xv[q]);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                mark(lastK, 2);
+                __syncthreads();
+                if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lastK) {  // no rows in between: the diagonal-block sums of this tile
+                    mark(true, 4);
+                    if (c < C4_TB) {
+                        T hc[C4_TB];
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t) hc[t] = hist[t][c];
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t)
+#pragma unroll
+                            for (int q = 0; q < RP; ++q)
+                                accT[q] = A::add(accT[q], A::mul(readlane_t(xv[q], t), hc[t]));
+                    }
+                    mark(true, 5);
+                    return;
+                }
+                // ---------------- U: column tile K of the rows between, once they have it
+                mark(lastK, 3);
+                if (w == 0) poll_all(K + 1, (int)I, K + 1);
+                __syncthreads();
+                const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
+                for (int rr = tid; rr < cnt; rr += C5_NT) {
+                    const T* base = CB + (int64_t)k0 * ld + C4_TB + rr;
+                    T v[C4_TB];
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
+                }
+                __syncthreads();
+                mark(lastK, 4);
+#pragma unroll 1
+                for (int t = 0; t < C4_TB; ++t) {
+                    T x[RP];
+#pragma unroll
+                    for (int q = 0; q < RP; ++q) x[q] = hist[t][r0 + q];
+                    const T* col = &colK[t][64 + c - lb - C4_TB];  // col[64 (mm - m)]: column jb + c + 64 mm
+#pragma unroll
+                    for (int mm = m; mm < M; ++mm)
+                        if (jb + 64 * mm < i0) {
+                            const T cv = col[64 * (mm - m)];
+#pragma unroll
+                            for (int q = 0; q < RP; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(x[q], cv));
+                        }
+                    if (c < C4_TB) {
+                        const T hv = hist[t][c];
+#pragma unroll
+                        for (int q = 0; q < RP; ++q) accT[q] = A::add(accT[q], A::mul(x[q], hv));
+                    }
+                }
+                mark(lastK, 5);
+            }
+        };
+        [&]<int... ms>(std::integer_sequence<int, ms...>) __attribute__((always_inline)) {
+            (window(std::integral_constant<int, ms>{}), ...);
+        }(std::make_integer_sequence<int, M>{});
+        // ---------------- the 16 x 16 diagonal block (wave 0)
+        if (c < TR) {
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                dacc[r0 + q][c] = accT[q];
+                dA[r0 + q][c] = aT[q];
+            }
+        }
+        __syncthreads();
+        mark(false, 12);
+        if (tid < 64) {
+            diag_factor16<T>(dacc, dA, xl, i0, n, b, ld, CB, R, status, c);
+            mark(false, 13);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mark(false, 14);
+            if (tr0) {
+#pragma unroll
+                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
+                atomicAdd(&trace[15], 1ull);
+                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // forward substitution on the band (lib.rs:28-46): y_i = (b_i - sum_{j<i}
 // L_ij y_j) / L_ii, sum in ascending j. One workgroup per RHS column; blocks
 // of 256 rows: the "far" terms (j < block start) are summed first, one thread
@@ -2359,15 +2587,13 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];  // Di[p][row][col]
 #pragma unroll
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
-            if (p3 && p == 3) {
-                // BSM_BLK_PROG=2: Di[3] out at once, with its own flag (rbf[3]):
-                // the next tile's last column block needs only it (and L's
-                // blocks (3, c) < 3, published with Linv's row blocks)
-                if ((tid & 63) < 16) {
+            if (p3 && p == 3 && (tid & 63) < 16) {
+                // BSM_BLK_PROG=2: Di[3] out at once (its flag rbf[3] at the
+                // loop's end, beside rbf[2], before Linv's last row block is
+                // assembled): the next tile's last column block needs only it
+                // and L's blocks (3, c < 3), which go out with Linv's row blocks
 #pragma unroll
-                    for (int q2 = 0; q2 < 16; ++q2) st_sc1(&p3[768 + q2 * 16 + r], x[q2]);
-                }
-                blk_publish_flag(rbf, 3, tid & 63);
+                for (int q2 = 0; q2 < 16; ++q2) st_sc1(&p3[768 + q2 * 16 + r], x[q2]);
             }
         }
         // pflag: the caller's global stores (the sub-diagonal tile) drain on
@@ -2429,8 +2655,10 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
         }
     }
     // Linv's last row block and diagonal block
-    if (w < 3) blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
-    else {
+    if (w < 3) {
+        if (p3 && w == 0) blk_publish_flag(rbf, 3, tid & 63);  // Di[3], stored after the last pivots
+        blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
+    } else {
         if (dpub) blk_publish_flag(rbf, 2, tid & 63);
         blk_linv_diag<T>(Q, Di, 3, tid & 63);
     }
@@ -3092,19 +3320,10 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             // sum runs while tile K - 1 still factors its last panel, and only
             // Di[3] (published by its wave 0 at once) is waited for
             const T* p3k = pub3 ? pub3 + (K - 1) * 1024 : nullptr;
+            bsm_d4 t3 = {0.0, 0.0, 0.0, 0.0};  // prog 2: S[:, 3] - sum_{c < 3} L[:, c] L_{K-1}[3][c]^T, as c forms
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 if (p3k && c == 3) {
-                    bsm_d4 t3;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) t3[q] = (double)PT[48 + m][16 * w + kq + 4 * q];
-#pragma unroll
-                    for (int k4 = 0; k4 < 12; ++k4) {
-                        const int k = 4 * k4 + kq, cp = k4 >> 2;
-                        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)ATl[k * TLD + 16 * w + m],
-                                                                  (double)Tb[cp * 256 + m * 16 + (k - 16 * cp)], t3,
-                                                                  0, 0, 0);
-                    }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) AT[48 + m][16 * w + kq + 4 * q] = (T)t3[q];
                     if (tdbg) cw0 = clock64();
@@ -3147,6 +3366,10 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 }
                 if (p3k && c < 3) Tb[c * 256 + tid] = l3;
                 __syncthreads();
+                if (p3k && c == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) t3[q] = (double)PT[48 + m][16 * w + kq + 4 * q];
+                }
                 if (tdbg && c == 3) cs1 = clock64();
                 bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -3164,6 +3387,14 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 }
                 __syncthreads();
                 if (tdbg && c == 3) cs2 = clock64();
+                if (p3k && c < 3) {
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) {
+                        const int k = 4 * k4 + kq;
+                        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)ATl[(16 * c + k) * TLD + 16 * w + m],
+                                                                  (double)Tb[c * 256 + m * 16 + k], t3, 0, 0, 0);
+                    }
+                }
                 }
 #pragma unroll
                 for (int k4 = 0; k4 < 4; ++k4) {
@@ -3422,6 +3653,27 @@ int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     return BSM_OK;
 }
 
+template <typename T, int M, int RP>
+int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
+    constexpr int C5_NT = 64 * (16 / RP);
+    const int64_t n_tiles = (bd.n + C4_TB - 1) / C4_TB;
+    int dev = 0, cus = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    int per_cu = 0;
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol5<T, M, RP>, C5_NT, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol5 does not fit a CU");
+    band_chol4_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
+    BSM_HIP_TRY(hipGetLastError());
+    int64_t grid = (int64_t)cus * per_cu;
+    if (grid > n_tiles) grid = n_tiles;
+    if (grid < 1) grid = 1;
+    band_chol5<T, M, RP><<<(unsigned)grid, C5_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
+                                                     status + 1, n_tiles, trace);
+    BSM_HIP_TRY(hipGetLastError());
+    return BSM_OK;
+}
+
 // A into the band layout CB (zeros elsewhere); bw_max: the widest band accepted
 template <typename T>
 int band_setup(const bsm_csr* a, Band& bd, hipStream_t s, int64_t bw_max) {
@@ -3472,8 +3724,24 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     const bool fits32 = (int64_t)a->rows * (bw + 1) + band_pad(bw + 1) < ((int64_t)1 << 31);
     const bool v1 = (cv && atoi(cv) == 1) || bw > 64 * 16 || !fits32;
     // default band_chol4 (tile events); BSM_CHOL_VARIANT = 0 band_chol3, 1 band_chol (A/B)
-    const bool v4 = (!cv || atoi(cv) == 4) && bw + C4_TB - 1 <= 64 * 16;
-    if (v4) {
+    const bool v4 = (!cv || atoi(cv) == 4 || atoi(cv) == 5) && bw + C4_TB - 1 <= 64 * 16;
+    // BSM_CHOL_VARIANT=5: band_chol5 (four rows per wave; A/B)
+    const bool v5 = v4 && cv && atoi(cv) == 5;
+    if (v5) {
+        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
+        const int64_t w4 = bw + C4_TB - 1;
+        // BSM_CHOL_RPW: rows per wave (2: eight waves, 4 (default): four)
+        const char* rpe = getenv("BSM_CHOL_RPW");
+        auto go = [&]<int RP>() {
+            if (w4 <= 64) rc = launch_chol5<T, 1, RP>(bd, prog.as<int>(), status, s, tr);
+            else if (w4 <= 128) rc = launch_chol5<T, 2, RP>(bd, prog.as<int>(), status, s, tr);
+            else if (w4 <= 256) rc = launch_chol5<T, 4, RP>(bd, prog.as<int>(), status, s, tr);
+            else if (w4 <= 512) rc = launch_chol5<T, 8, RP>(bd, prog.as<int>(), status, s, tr);
+            else rc = launch_chol5<T, 16, RP>(bd, prog.as<int>(), status, s, tr);
+        };
+        if (rpe && atoi(rpe) == 2) go.template operator()<2>();
+        else go.template operator()<4>();
+    } else if (v4) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
         if (w4 <= 64) rc = launch_chol4<T, 1>(bd, prog.as<int>(), status, s, tr);

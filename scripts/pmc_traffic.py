@@ -10,9 +10,10 @@ only: it reports 1/2 of their bytes. The kernels also read their index /
 value stream with 4-B and 8-B lanes, which the guide leaves uncalibrated. So
 the stream is calibrated here on the kernel itself:
 
-* --probe: a FETCH_SIZE pass of the same run with BSM_TILED_PROBE_MASK=0,
-  where every gather reads X row 0 (an L2 hit), so the counter sees the
-  stream alone (wrong results: measurement only);
+* --probe: a FETCH_SIZE pass of the same run with the kernel's probe mask at
+  0 (BSM_TILED_PROBE_MASK, BSM_TILED_K1_PROBE or BSM_SPMM_PROBE_MASK), where
+  every gather reads X row 0 (an L2 hit), so the counter sees the stream
+  alone (wrong results: measurement only);
 * --stream-bytes: the stream's true size (the tiled copy's bytes; it has no
   reuse, so every byte goes to memory once).
 
@@ -81,9 +82,12 @@ def main():
             "stream_bytes": a.stream_bytes,
             "stream_factor": round(a.stream_bytes / (probe_kb * 1024.0), 4),
             "gather_bytes": gather_b,
-            "correction": "stream calibrated on the kernel (BSM_TILED_PROBE_MASK=0 pass: the stream alone; "
-                          "stream_factor = true stream bytes / (probe FETCH_SIZE x 1024)); gathers 16-B/lane: "
-                          "2 x (FETCH_SIZE - probe) x 1024 (MI355X_MICROARCH.md:298); WRITE_SIZE exact",
+            "correction": "stream calibrated on the kernel (a probe pass with every gather on X row 0: "
+                          "BSM_TILED_PROBE_MASK=0 (k = 32 copy), BSM_TILED_K1_PROBE=0 (k = 1 copy), "
+                          "BSM_SPMM_PROBE_MASK=0 (row kernel); the stream alone; stream_factor = true stream bytes "
+                          "/ (probe FETCH_SIZE x 1024)); gathers: 2 x (FETCH_SIZE - probe) x 1024 "
+                          "(MI355X_MICROARCH.md:298 for 16-B lanes; the 8-B lanes of k = 1 by the stream's own "
+                          "factor, ~1.9); WRITE_SIZE exact",
             "fetch_bytes": a.stream_bytes + gather_b,
         })
     else:

@@ -103,7 +103,7 @@ def csr_arrays(dense):
     return rp, nzc.astype(np.uint64), dense[nzr, nzc]
 
 
-@pytest.mark.parametrize("chol_variant", ["0", "1", "4"])  # band_chol3 / band_chol / band_chol4
+@pytest.mark.parametrize("chol_variant", ["0", "1", "4", "5"])  # band_chol3 / band_chol / band_chol4 / band_chol5
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("n,density", [(1, 1.0), (7, 0.5), (33, 0.2), (64, 0.05), (150, 0.1), (300, 0.02)])
 def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, chol_variant):
@@ -170,8 +170,9 @@ def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
     v = v.astype(dtype)
     expect = orc.cholesky(n, n, rp, ci, v, band=True)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
-    for variant in ("0", "1", "4"):
-        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
+    for variant in ("0", "1", "4", "5", "5r2"):
+        monkeypatch.setenv("BSM_CHOL_VARIANT", variant[0])
+        monkeypatch.setenv("BSM_CHOL_RPW", "2" if variant == "5r2" else "4")
         assert_csr_exact(A.cholesky_decomp(), *expect)
 
 
@@ -185,13 +186,14 @@ def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
     rp, ci, v = orc.poisson2d(g)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
     out = {}
-    for variant in ("0", "4"):
+    for variant in ("0", "4", "5"):
         monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
         L = A.cholesky_decomp()
         out[variant] = (np.asarray(L.row_index), np.asarray(L.col_index), bits(np.asarray(L.v)))
         del L
-    for a, b in zip(out["0"], out["4"]):
+    for a, b, c in zip(out["0"], out["4"], out["5"]):
         assert np.array_equal(a, b)
+        assert np.array_equal(a, c)  # band_chol5 (four rows per wave)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
