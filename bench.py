@@ -452,6 +452,11 @@ def main():
                     help="rounds of the row partition (pieces = chunks x N; 0: 1 at N=1 or with the tiled copy, "
                          "4 otherwise)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend under a launcher (nccl = RCCL)")
+    ap.add_argument("--exchange", default="rccl", choices=("rccl", "gloo"),
+                    help="how the ranks' Y slots are assembled: rccl = the library's in-place all-gathers; gloo = "
+                         "external rank contexts (bsm_multi_create_external) and distributed.exchange_slots over "
+                         "the launcher's group on the host (several ranks on one GPU: a logic check of the N > 1 "
+                         "path, not a measurement)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 recomputes Y on its own GPU by another schedule and checks the assembled Y bit for "
                          "bit (whole matrix up to 2e9 nnz, else the rows around every piece bound)")
@@ -469,6 +474,9 @@ def main():
         return
 
     launched = "WORLD_SIZE" in os.environ  # torch.distributed.run sets it, also at N = 1
+    external = args.exchange == "gloo"
+    if external and not launched:
+        ap.error("--exchange gloo needs a launcher (torch.distributed.run)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -479,7 +487,7 @@ def main():
     dev = torch.device("cuda", ordinal)
     backend = None
     if launched:
-        backend = args.backend
+        backend = "gloo" if external else args.backend
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -504,7 +512,9 @@ def main():
 
     # the library's RCCL context: the id travels over torch.distributed
     t0 = time.perf_counter()
-    if launched:
+    if external:
+        ctx = MultiGpu.external(world, rank, ordinal)
+    elif launched:
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx = MultiGpu.for_rank(obj[0], world, rank, ordinal)
@@ -522,10 +532,11 @@ def main():
     # the rows' nnz (the generator's row lengths): constant-length configs by count
     my_nnz = my_rows * nnz_r if nnz_r else None
     x = torch.empty((n_cols, k), dtype=torch_dt, device=dev)
-    if rank == 0:
+    if rank == 0 or external:  # external ranks have no communicator: each makes the replica itself
         x.copy_(gen_dense(SEED_X, 0, n_cols, k, dtype=np_dt, device=dev))
     torch.cuda.synchronize()
-    ctx.broadcast([x.data_ptr()], x.numel() * es, root=0)  # X replicated over RCCL (untimed setup)
+    if not external:
+        ctx.broadcast([x.data_ptr()], x.numel() * es, root=0)  # X replicated over RCCL (untimed setup)
     log(f"rank {rank}: pieces {my_pieces} of {m.pieces} ({chunks} round(s)), nnz {nnz_total:,} in total, generated in "
         f"{gen_ms:.0f} ms; RCCL context {comm_init_ms:.0f} ms")
     # the schedule's per-matrix preparation (outside the timed region, like the
@@ -543,8 +554,18 @@ def main():
                      for a, b in my_pieces)
 
     xp = [x.data_ptr()]
-    for _ in range(args.warmup):
+
+    def step():
         m.step(xp)
+        if external:  # the slots over the host group, then the compaction
+            from basic_sparse_matrix_amd.distributed import exchange_slots
+
+            m.sync()
+            exchange_slots(m, world, rank, chunks)
+            m.compact()
+
+    for _ in range(args.warmup):
+        step()
     torch.cuda.synchronize()
     m.reset_times()
     if launched:
@@ -552,7 +573,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        m.step(xp)
+        step()
     torch.cuda.synchronize()
     if launched:
         dist.barrier()
@@ -564,7 +585,8 @@ def main():
     comp_ms = [t["compaction"] for t in times]
     log(f"rank {rank}: SpMM ms per timed step: {[round(t, 2) for t in kern_ms]}")
     if launched:
-        t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, float(np.mean(kern_ms))], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmax = float(t[0]), float(t[1])
     else:
@@ -608,8 +630,10 @@ def main():
                 traffic_src = os.path.relpath(pmc_json, ROOT)
             else:
                 pmc = None
-        comm = (f"library RCCL all-gather (bsm_mcsr_step; {world} rank(s)"
-                + (f", context id over torch.distributed {backend})" if launched else ", ncclCommInitAll)"))
+        comm = ((f"external rank contexts, Y slots exchanged over torch.distributed {backend} on the host "
+                 f"({world} ranks; a logic check, not a measurement)") if external else
+                (f"library RCCL all-gather (bsm_mcsr_step; {world} rank(s)"
+                 + (f", context id over torch.distributed {backend})" if launched else ", ncclCommInitAll)")))
         line = {
             "metric": "CSR x dense SpMM effective GB/s (B_alg / step time); nnz/s",
             "value": round(value, 2),

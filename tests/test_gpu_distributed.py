@@ -110,3 +110,25 @@ def test_external_ranks_generate_schedules(tmp_path, world, rows, n_cols, kind, 
             assert r["plan"]["tiled_pieces"] == chunks, r  # the copy really ran on every piece
         else:
             assert r["plan"]["tiled_pieces"] == 0, r
+
+
+@pytest.mark.parametrize("config,chunks", [("c3", 1), ("c3", 3)])
+def test_bench_two_ranks_one_gpu_gloo_exchange(config, chunks):
+    """bench.py's N > 1 path (the rank's pieces, my_rows, the barriers, the
+    max over ranks, --verify of the assembled Y against one GPU, the JSON
+    line) with two ranks on the one GPU: external contexts, Y slots over gloo
+    (--exchange gloo). A logic check of what the driver's N = 2..8 runs do
+    with RCCL, not a measurement."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    root = os.path.dirname(HERE)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2",
+           "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-e2e", "--verify",
+           "--chunks", str(chunks), "--exchange", "gloo"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["verified_vs_single_gpu"] is True
+    assert line["verified_rows"] == 1_000_000
+    assert "external" in line["config"]["comm"]
