@@ -716,6 +716,11 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
     const size_t es = dtype_size(m->dtype);
     const size_t slot_b = m->pad * k * es;
     const bool allow_tiled = m->schedule != 2;
+    // one rank: the all-gathers have nothing to move (every slot is this
+    // rank's own), so the step skips them and their stream hops;
+    // BSM_MULTI_SOLO_RCCL=1 runs them anyway (tests of the RCCL calls at G = 1)
+    const char* sre = getenv("BSM_MULTI_SOLO_RCCL");
+    const bool solo = ctx->world == 1 && !ctx->external && !(sre && atoi(sre) == 1);
     // events of this step (timed steps are read after the fact: no host sync)
     for (int i = 0; i < ctx->n_local; ++i) {
         Local& L = m->loc[i];
@@ -741,15 +746,17 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
                                            static_cast<char*>(L.y) + slot * slot_b, L.nz + slot * m->pad,
                                            ctx->compute[i]));
             }
-            BSM_HIP_TRY(hipEventRecord(L.round_ev[c], ctx->compute[i]));
-            BSM_HIP_TRY(hipStreamWaitEvent(ctx->comm[i], L.round_ev[c], 0));
+            if (!solo) {
+                BSM_HIP_TRY(hipEventRecord(L.round_ev[c], ctx->compute[i]));
+                BSM_HIP_TRY(hipStreamWaitEvent(ctx->comm[i], L.round_ev[c], 0));
+            }
             if (c + 1 == m->chunks)
                 BSM_HIP_TRY(hipEventRecord(L.ev[L.steps * EV_PER_STEP + 1], ctx->compute[i]));
         }
         // round c of every rank lands at slots c*world .. c*world + world - 1
         // (an external context leaves that to the caller: bsm_mcsr_slot_read /
         // _write, then bsm_mcsr_compact)
-        if (ctx->external) continue;
+        if (ctx->external || solo) continue;
         BSM_NCCL_TRY(ncclGroupStart());
         for (int i = 0; i < ctx->n_local; ++i) {
             Local& L = m->loc[i];
@@ -775,8 +782,8 @@ int bsm_mcsr_step(bsm_mcsr* m, const void* const* x_dev) {
         DeviceGuard g(L.device);
         hipStream_t s = ctx->compute[i];
         hipEvent_t* E = &L.ev[L.steps * EV_PER_STEP];
-        BSM_HIP_TRY(hipEventRecord(E[2], ctx->comm[i]));
-        BSM_HIP_TRY(hipStreamWaitEvent(s, E[2], 0));
+        BSM_HIP_TRY(hipEventRecord(E[2], solo ? s : ctx->comm[i]));
+        if (!solo) BSM_HIP_TRY(hipStreamWaitEvent(s, E[2], 0));
         BSM_HIP_TRY(hipEventRecord(E[3], s));
         if (L.compacts && !ctx->external) BSM_TRY(compact_local(m, L, s));
         BSM_HIP_TRY(hipEventRecord(E[4], s));

@@ -630,8 +630,13 @@ def main():
                 traffic_src = os.path.relpath(pmc_json, ROOT)
             else:
                 pmc = None
+        solo_rccl = os.environ.get("BSM_MULTI_SOLO_RCCL") == "1"
         comm = ((f"external rank contexts, Y slots exchanged over torch.distributed {backend} on the host "
                  f"({world} ranks; a logic check, not a measurement)") if external else
+                ("one rank: no collective (the library skips the all-gathers, which have nothing to move at one "
+                 "rank; BSM_MULTI_SOLO_RCCL=1 runs them)" + (f"; context id over torch.distributed {backend}"
+                                                             if launched else ""))
+                if world == 1 and not solo_rccl else
                 (f"library RCCL all-gather (bsm_mcsr_step; {world} rank(s)"
                  + (f", context id over torch.distributed {backend})" if launched else ", ncclCommInitAll)")))
         line = {

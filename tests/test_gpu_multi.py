@@ -47,6 +47,13 @@ def assert_same_csr(got, want):
     assert np.array_equal(bits(v), bits(np.asarray(ev, dtype=np.asarray(v).dtype))), "values differ"
 
 
+@pytest.fixture(autouse=True)
+def _rccl_at_one_rank(monkeypatch):
+    """At one rank the step skips the all-gathers (nothing to move); these
+    tests run them anyway, so the RCCL calls execute on the GPU."""
+    monkeypatch.setenv("BSM_MULTI_SOLO_RCCL", "1")
+
+
 @pytest.fixture(scope="module")
 def ctx():
     c = MultiGpu(1)
@@ -219,7 +226,7 @@ def test_bench_under_torchrun_nccl(chunks):
     """bench.py --gpus 1 as a fresh torch.distributed.run job, backend nccl:
     the library's RCCL context from a shipped id, its all-gathers, torch's
     RCCL barrier / all-reduce, and --verify (bit-identical to one GPU)."""
-    env = dict(os.environ)
+    env = dict(os.environ, BSM_MULTI_SOLO_RCCL="1")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "1",
@@ -309,3 +316,19 @@ def test_external_context_world1_and_refusals(orc):
         m.slot_read(m.pieces, 1)  # past the last slot
     del m
     c.close()
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_one_rank_skips_allgathers_same_bits(ctx, orc, monkeypatch, chunks):
+    """One rank: the default step skips the degenerate all-gathers and their
+    stream hops; the output is the same as with them (BSM_MULTI_SOLO_RCCL=1)."""
+    rows, cols, k = 3000, 2000, 32
+    rp, ci, v = orc.gen_csr(1000, rows, cols, 1, 0, 40)
+    x_cols = orc.gen_x_cols(1001, cols, k)
+    m = MultiCsr.upload(ctx, rows, cols, rp, ci, v, chunks=chunks)
+    monkeypatch.setenv("BSM_MULTI_SOLO_RCCL", "0")
+    skipped = m.mul_dense_cols(x_cols, cols).download()
+    monkeypatch.setenv("BSM_MULTI_SOLO_RCCL", "1")
+    with_rccl = m.mul_dense_cols(x_cols, cols).download()
+    assert_same_csr(skipped, with_rccl)
+    assert_same_csr(skipped, orc.mul_dense(rows, cols, rp, ci, v, x_cols))
