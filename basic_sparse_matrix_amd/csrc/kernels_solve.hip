@@ -36,6 +36,12 @@
 
 #include "bsm_internal.hpp"
 
+// band_chol5's diagonal block: 0 diag_factor16, 1 diag_factor16x<SM = 1>
+// (default), 2 diag_factor16x<SM = 2> + stores by the whole workgroup (A/B builds)
+#ifndef BSM_C5_DIAG
+#define BSM_C5_DIAG 1
+#endif
+
 namespace bsm {
 namespace {
 
@@ -183,6 +189,155 @@ __device__ __forceinline__ void diag_factor16(const T (*dacc)[17], const T (*dA)
     [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
         (step(std::integral_constant<int, ts>{}), ...);
     }(std::make_integer_sequence<int, NB>{});
+}
+
+// √ of a pivot the caller has checked positive and finite: IEEE sqrt
+// correctly rounded (f32: formed in f64, rounded once, as pow_half). A pivot
+// that fails the check flags ST_NOT_PD and its factor is discarded, so the
+// -inf / -0 cases of pow_half need no handling here.
+__device__ __forceinline__ double sqrt_pos(double x) { return __dsqrt_rn(x); }
+__device__ __forceinline__ float sqrt_pos(float x) { return __double2float_rn(__dsqrt_rn((double)x)); }
+
+// band_chol5's chain hop (row-block J's diagonal block and 1/L to row-block
+// J + 1's last tile) as 8-byte {tag = J + 1, 32-bit half} granules written
+// sc1: the data is the flag (the guide's R2 hand-off), so the consumer's first
+// complete sweep IS its load, with no drain before a flag, no flag round trip
+// and no barrier. Slot J % MB_SLOTS; word ((t * 16 + u) * 2 + half) holds
+// L[16J + t + u][16J + t] for u >= 1 and 1/L[16J + t][16J + t] at u = 0.
+// The slots are zeroed per call (tag 0 never matches; J + 1 - MB_SLOTS, the
+// slot's previous tag, neither).
+constexpr int MB_SLOTS = 64;
+constexpr int MB_SLOT_WORDS = 16 * 16 * 2;
+template <typename T> __device__ __forceinline__ void mb_put(unsigned long long* g, unsigned tag, T v) {
+    const unsigned long long tg = (unsigned long long)tag << 32;
+    if constexpr (sizeof(T) == 8) {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        __hip_atomic_store(g, tg | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 1, tg | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(g, tg | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// one granule read: the value, and whether its tag(s) match
+template <typename T> __device__ __forceinline__ T mb_get(const unsigned long long* g, unsigned tag, bool& ok) {
+    if constexpr (sizeof(T) == 8) {
+        const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
+        return __builtin_bit_cast(T, (hi << 32) | (lo & 0xffffffffull));
+    } else {
+        const unsigned long long x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = (unsigned)(x >> 32) == tag;
+        return __builtin_bit_cast(T, (unsigned)x);
+    }
+}
+
+// diag_factor16 with the per-step side work taken off the pivot chain: the
+// pivot check is one class test per step folded into a flag (one atomic at
+// the end), 1/L[t][t] is kept by lane t (one select), and L's column t goes
+// to registers. Then, by SM:
+//   SM = 1: wave 0 stores the block and R after the 16 steps;
+//   SM = 2: the block and R go to LDS (Ls[r][t], Rs[t]) for the whole
+//           workgroup to store (diag_store16) behind a barrier.
+// IL: each step's updates of the columns past the next pivot's are issued in
+// the following step, beside its sqrt -> reciprocal chain (measured slower:
+// 8.7k against 8.1k cycles per block without, against 9.1k for diag_factor16;
+// scripts/micro/diag_factor.hip). hook() runs after step 3 (band_chol5: the
+// factor wave's drain and arrival for the last tile's progress flag).
+// Same operations per element in the same order: the same bits as diag_factor16.
+struct NoHook {
+    __device__ void operator()() const {}
+};
+template <typename T, int SM, bool IL = false, typename Hook = NoHook>
+__device__ __forceinline__ void diag_factor16x(const T (*dacc)[17], const T (*dA)[17], T (*Ls)[17], T* Rs, int i0,
+                                               int64_t n, int64_t b, int64_t ld, T* CB, T* R, int* status, int c,
+                                               unsigned long long* mb = nullptr, unsigned mb_tag = 0,
+                                               Hook hook = {}) {
+    using A = Arith<T>;
+    constexpr int NB = 16;
+    asm volatile("" : "+v"(c));
+    const int r = c & (NB - 1);
+    const bool live = i0 + r < n;
+    T q[NB], a[NB], xs[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        q[j] = live ? dacc[r][j] : A::zero();
+        a[j] = live ? dA[r][j] : (r == j ? (T)1 : A::zero());
+    }
+    T myrt = A::zero();
+    bool pd = true;
+    auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
+        const T v = A::sub(a[t], q[t]);
+        const T vv = rowbcast<t>(v);
+        pd = pd && __builtin_isfinite(vv) && vv > A::zero();
+        const T piv = sqrt_pos(vv);
+        const T rt = div_rn((T)1, piv);
+        const T x = r == t ? piv : A::mul(rt, v);  // L[i0 + r][i0 + t] for r >= t
+        xs[t] = x;
+        myrt = c == t ? rt : myrt;
+        if constexpr (IL) {
+            // step t - 1's updates of the columns after t + 1, placed beside this
+            // step's pivot chain (one scheduling region: they fill its latency),
+            // then this step's update of column t + 1 (the next pivot's)
+            if constexpr (t >= 1) {
+                const T xp = xs[t - 1];
+                [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+                    ((q[t + 1 + js] = A::add(q[t + 1 + js], A::mul(xp, rowbcast<t + 1 + js>(xp)))), ...);
+                }(std::make_integer_sequence<int, NB - 1 - t>{});
+            }
+            if constexpr (t + 1 < NB) q[t + 1] = A::add(q[t + 1], A::mul(x, rowbcast<t + 1>(x)));
+        } else {
+            [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
+                ((q[t + 1 + js] = A::add(q[t + 1 + js], A::mul(x, rowbcast<t + 1 + js>(x)))), ...);
+            }(std::make_integer_sequence<int, NB - 1 - t>{});
+        }
+#pragma unroll
+        for (int j = t + 1; j < NB; ++j) asm volatile("" : "+v"(q[j]));
+        if constexpr (t == 3) hook();  // a quarter in: the caller's earlier stores have drained by now
+    };
+    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+        (step(std::integral_constant<int, ts>{}), ...);
+    }(std::make_integer_sequence<int, NB>{});
+    if (c == 0 && !pd) atomicOr(status, ST_NOT_PD);
+    if constexpr (SM == 1) {
+        if (mb && c < NB) {  // the chain hop first (mailbox granules), then the band
+#pragma unroll
+            for (int t = 0; t < NB; ++t)
+                if (t < r) mb_put(mb + (t * 16 + (r - t)) * 2, mb_tag, xs[t]);
+            mb_put(mb + (r * 16) * 2, mb_tag, myrt);
+        }
+        if (c < NB && live) {
+            T* p = CB + (int64_t)i0 * ld + r;  // L[i0 + r][i0 + t] = CB[(i0 + t) ld + r - t]
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                if (r >= t && r - t <= b) st_sc1(p, xs[t]);
+                p += ld - 1;
+            }
+            st_sc1(&R[i0 + r], myrt);
+        }
+    } else {
+        if (c < NB) {
+#pragma unroll
+            for (int t = 0; t < NB; ++t) Ls[r][t] = xs[t];
+            Rs[r] = myrt;
+        }
+    }
+}
+
+// The stores of diag_factor16x<T, 2>'s block, by NT threads (after a barrier
+// behind the factor): L[i0 + r][i0 + t] for r >= t, r - t <= b, and R.
+template <typename T, int NT>
+__device__ __forceinline__ void diag_store16(const T (*Ls)[17], const T* Rs, int i0, int64_t n, int64_t b,
+                                             int64_t ld, T* CB, T* R, int tid) {
+    for (int e = tid; e < 16 * 16 + 16; e += NT) {
+        if (e < 256) {
+            const int t = e >> 4, d = e & 15, r = t + d;  // column t, offset d: coalesced along the band
+            if (r < 16 && d <= b && i0 + r < n) st_sc1(&CB[(int64_t)(i0 + t) * ld + d], Ls[r][t]);
+        } else {
+            const int r = e - 256;
+            if (i0 + r < n) st_sc1(&R[i0 + r], Rs[r]);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -933,20 +1088,23 @@ template <typename T, int M, int RP>  // RP rows per wave: 16 / RP waves
 __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                     T* __restrict__ R, int* __restrict__ fprog,
                                                     int* __restrict__ status, int* __restrict__ ticket,
-                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
+                                                    int64_t n_tiles, unsigned long long* __restrict__ trace,
+                                                    unsigned long long* __restrict__ mbox) {
     using A = Arith<T>;
     constexpr int CS = 64 + 64 * M;
     constexpr int C5_NT = 64 * (16 / RP);
     __shared__ T colK[C4_TB][CS];
-    __shared__ T dTl[C4_TB][64];
-    __shared__ T rT[C4_TB];
-    __shared__ T aK[C4_TB][C4_TB];
     __shared__ T hist[C4_TB][C4_TB + 1];
     __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
     __shared__ T xl[16];
     __shared__ long long tph[16];
+    __shared__ int s_arr;
+#if BSM_C5_DIAG != 1
+    mbox = nullptr;  // only diag_factor16x<T, 1> fills the mailbox
+#endif
     const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
     for (int q = tid; q < C4_TB * 64; q += C5_NT) colK[q >> 6][q & 63] = A::zero();
+    if (tid == 0) s_arr = 0;
     const int ib = (int)b;
     auto poll_all = [&](int jlo, int jhi, int need) {  // wave 0: fprog[J] >= need for J in [jlo, jhi)
         bool ok = true;
@@ -1010,59 +1168,104 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 const int k0 = C4_TB * K, lb = 16 * e;
                 const bool lastK = K == (int)I - 1;
                 // ---------------- T: this row-block's tile K
-                if (w == 0) poll_all(K, K + 1, K + 1);
-                mark(lastK, 0);
-                __syncthreads();
+                // the rows' own A values for the tile's columns (nobody else writes
+                // them): loaded before the wait, straight into the lanes (lane c:
+                // column k0 + (c & 15))
+                T myA[RP];
 #pragma unroll
-                for (int u4 = 0; u4 < C4_TB * 64 / C5_NT; ++u4) {  // the diagonal tile of K, per lane of the slot
-                    const int el = tid + C5_NT * u4, t = el >> 6, cc = el & 63, u = cc - lb - t;
-                    T v = A::zero();
-                    if (u >= 1 && t + u <= 15 && u <= ib) v = ld_sc1(CB + (int64_t)(k0 + t) * ld + u);
-                    dTl[t][cc] = v;
+                for (int q = 0; q < RP; ++q) {
+                    const int rw = r0 + q, cl = c & 15, d = i0 + rw - k0 - cl;
+                    const bool ok = d <= ib && i0 + rw < n;
+                    const T v = ld_sc1(CB + (((int64_t)(k0 + cl) * ld + d) & -(int64_t)ok));
+                    myA[q] = ok ? v : A::zero();
                 }
-                for (int el = tid; el < C4_TB * C4_TB; el += C5_NT) {
-                    const int rr = el >> 4, t = el & 15, d = i0 + rr - k0 - t;
-                    T v = A::zero();
-                    if (d <= ib && i0 + rr < n) v = CB[(int64_t)(k0 + t) * ld + d];
-                    aK[rr][t] = v;
+                // row-block K's diagonal tile and 1/L, per lane, straight into
+                // registers (no LDS staging, no second barrier): lane c takes
+                // L[k0 + t + u][k0 + t], u = c - lb - t, for every t
+                T dvr[C4_TB], myR;
+                if (mbox && lastK) {
+                    // the chain hop: row-block I - 1's mailbox slot, swept by
+                    // every wave until all its granules carry tag I (the barrier
+                    // first: hist is still being read by U of the previous tile)
+                    __syncthreads();
+                    mark(true, 0);
+                    const unsigned long long* slot = mbox + (int64_t)(K & (MB_SLOTS - 1)) * MB_SLOT_WORDS;
+                    long long spins = 0;
+                    while (true) {
+                        bool all = true, g;
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t) {
+                            const int u = c - lb - t;
+                            const bool ok = u >= 1 && t + u <= 15 && u <= ib;
+                            const T v = mb_get<T>(slot + (ok ? (t * 16 + u) * 2 : 0), (unsigned)I, g);
+                            dvr[t] = ok ? v : A::zero();
+                            all &= g || !ok;
+                        }
+                        myR = mb_get<T>(slot + ((c & 15) * 16) * 2, (unsigned)I, g);
+                        all &= g;
+                        if (__all(all)) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > SPIN_LIMIT ||
+                            ((spins & 1023) == 0 &&
+                             (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
+                            if (c == 0) atomicOr(status, ST_TIMEOUT);
+                            break;
+                        }
+                    }
+                } else {
+                    if (w == 0) poll_all(K, K + 1, K + 1);
+                    mark(lastK, 0);
+                    __syncthreads();
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) {
+                        const int u = c - lb - t;
+                        const bool ok = u >= 1 && t + u <= 15 && u <= ib;
+                        const T v = ld_sc1(CB + (((int64_t)(k0 + t) * ld + u) & -(int64_t)ok));
+                        dvr[t] = ok ? v : A::zero();
+                    }
+                    myR = ld_sc1(&R[k0 + (c & 15)]);
                 }
-                if (tid < C4_TB) rT[tid] = ld_sc1(&R[k0 + tid]);
-                __syncthreads();
                 mark(lastK, 1);
-                T myR = rT[c & 15], myA[RP];
-#pragma unroll
-                for (int q = 0; q < RP; ++q) myA[q] = aK[r0 + q][c & 15];
+                // The tile's 16 columns are lanes lb .. lb + 15 of slot m: one DPP row
+                // (row e). Step t takes lane lb + t's accumulator, 1/L and A by
+                // row_newbcast (VALU, no SGPR round trip on the chain); every row of
+                // lanes gets its own lane t, so x is right in row e only and is
+                // zeroed elsewhere (dv is 0 there too: no term reaches other columns)
+                const bool inrow = (c >> 4) == e;
                 T xv[RP];
 #pragma unroll
                 for (int q = 0; q < RP; ++q) xv[q] = A::zero();
+                [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
+                    (([&] {
+                         constexpr int t = ts;
+                         const T dv = dvr[t];
+                         const T rt = rowbcast<t>(myR);
 #pragma unroll
-                for (int t = 0; t < C4_TB; ++t) {
-                    asm volatile("" : "+v"(myR));
-                    const T dv = dTl[t][c];
-                    const T rt = readlane_t(myR, t);
-#pragma unroll
-                    for (int q = 0; q < RP; ++q) {
-                        asm volatile("" : "+v"(myA[q]));
-                        const T sq = readlane_t(acc[q][m], lb + t);
-                        const T x = A::mul(rt, A::sub(readlane_t(myA[q], t), sq));
-                        acc[q][m] = A::add(acc[q][m], A::mul(x, dv));
-                        if (c == t) xv[q] = x;
-                    }
-                }
-                if (c < C4_TB) {
+                         for (int q = 0; q < RP; ++q) {
+                             const T sq = rowbcast<t>(acc[q][m]);
+                             const T x0 = A::mul(rt, A::sub(rowbcast<t>(myA[q]), sq));
+                             const T x = inrow ? x0 : A::zero();
+                             acc[q][m] = A::add(acc[q][m], A::mul(x, dv));
+                             if (c == lb + t) xv[q] = x;
+                         }
+                     }()),
+                     ...);
+                }(std::make_integer_sequence<int, C4_TB>{});
+                if (inrow) {
+                    const int cl = c & 15;
 #pragma unroll
                     for (int q = 0; q < RP; ++q) {
                         const int rw = r0 + q;
-                        hist[c][rw] = xv[q];
-                        const int d = i0 + rw - k0 - c;
-                        if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + c) * ld + d], xv[q]);
+                        hist[cl][rw] = xv[q];
+                        const int d = i0 + rw - k0 - cl;
+                        if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
                     }
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                mark(lastK, 2);
-                __syncthreads();
-                if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (lastK) {  // no rows in between: the diagonal-block sums of this tile
+                    // (the stores drain behind them: this tile's flag goes up at
+                    // the diagonal block's staging barrier, after the window)
+                    mark(true, 2);
+                    __syncthreads();
                     mark(true, 4);
                     if (c < C4_TB) {
                         T hc[C4_TB];
@@ -1072,13 +1275,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                         for (int t = 0; t < C4_TB; ++t)
 #pragma unroll
                             for (int q = 0; q < RP; ++q)
-                                accT[q] = A::add(accT[q], A::mul(readlane_t(xv[q], t), hc[t]));
+                                accT[q] = A::add(accT[q], A::mul(readlane_t(xv[q], lb + t), hc[t]));
                     }
                     mark(true, 5);
                     return;
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                mark(false, 2);
+                __syncthreads();
+                if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // ---------------- U: column tile K of the rows between, once they have it
-                mark(lastK, 3);
+                mark(false, 3);
                 if (w == 0) poll_all(K + 1, (int)I, K + 1);
                 __syncthreads();
                 const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
@@ -1092,24 +1299,42 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 }
                 __syncthreads();
                 mark(lastK, 4);
-#pragma unroll 1
-                for (int t = 0; t < C4_TB; ++t) {
-                    T x[RP];
+                // software-pipelined: step t + 1's LDS reads (x, the column
+                // values, the diagonal-block value) go out before step t's
+                // multiply-adds, so the LDS latency overlaps the VALU work
+                struct UB {
+                    T cv[M], x[RP], hv;
+                };
+                auto u_load = [&](int t, UB& ub) __attribute__((always_inline)) {
 #pragma unroll
-                    for (int q = 0; q < RP; ++q) x[q] = hist[t][r0 + q];
+                    for (int q = 0; q < RP; ++q) ub.x[q] = hist[t][r0 + q];
                     const T* col = &colK[t][64 + c - lb - C4_TB];  // col[64 (mm - m)]: column jb + c + 64 mm
+#pragma unroll
+                    for (int mm = m; mm < M; ++mm) ub.cv[mm] = col[64 * (mm - m)];
+                    ub.hv = hist[t][c & 15];
+                };
+                auto u_add = [&](const UB& ub) __attribute__((always_inline)) {
 #pragma unroll
                     for (int mm = m; mm < M; ++mm)
                         if (jb + 64 * mm < i0) {
-                            const T cv = col[64 * (mm - m)];
 #pragma unroll
-                            for (int q = 0; q < RP; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(x[q], cv));
+                            for (int q = 0; q < RP; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(ub.x[q], ub.cv[mm]));
                         }
                     if (c < C4_TB) {
-                        const T hv = hist[t][c];
 #pragma unroll
-                        for (int q = 0; q < RP; ++q) accT[q] = A::add(accT[q], A::mul(x[q], hv));
+                        for (int q = 0; q < RP; ++q) accT[q] = A::add(accT[q], A::mul(ub.x[q], ub.hv));
                     }
+                };
+                UB ua, ubb;
+                u_load(0, ua);
+#pragma unroll 1
+                for (int t = 0; t < C4_TB; t += 2) {
+                    u_load(t + 1, ubb);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u_add(ua);
+                    if (t + 2 < C4_TB) u_load(t + 2, ua);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u_add(ubb);
                 }
                 mark(lastK, 5);
             }
@@ -1125,8 +1350,62 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 dA[r0 + q][c] = aT[q];
             }
         }
-        __syncthreads();
+#if BSM_C5_DIAG == 1
+        __syncthreads();  // dacc / dA visible; the last tile's stores drain behind the factor
         mark(false, 12);
+        // The last tile's progress flag (fprog[I] = I, which the next row-blocks'
+        // U of tile I - 1 waits for) without a drain on the chain: every wave
+        // waits for its own stores, then arrives at an LDS counter, and the last
+        // to arrive raises the flag (MI355X_MICROARCH.md "Valid forms": per-wave
+        // arrival in LDS); the factor wave arrives from inside the factor, when
+        // its stores have long drained. An atomic max: the completion value
+        // I + 1 may already be there.
+        auto arrive = [&]() __attribute__((always_inline)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 1) {
+                s_arr = 0;
+                __hip_atomic_fetch_max(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        };
+        if (tid < 64) {
+            diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c,
+                                 mbox ? mbox + (I & (MB_SLOTS - 1)) * MB_SLOT_WORDS : nullptr, (unsigned)I + 1, arrive);
+            mark(false, 13);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mark(false, 14);
+            if (tr0) {
+#pragma unroll
+                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
+                atomicAdd(&trace[15], 1ull);
+                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
+            }
+        } else {
+            arrive();
+        }
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tile's stores
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(false, 12);
+#endif
+#if BSM_C5_DIAG == 2
+        // the block to LDS (over dacc / xl, read before), stored by every thread
+        if (tid < 64) diag_factor16x<T, 2>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
+        mark(false, 13);
+        __syncthreads();
+        diag_store16<T, C5_NT>(dacc, xl, i0, n, b, ld, CB, R, tid);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mark(false, 14);
+        if (tr0) {
+#pragma unroll
+            for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
+            atomicAdd(&trace[15], 1ull);
+            atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
+        }
+#elif BSM_C5_DIAG == 0
         if (tid < 64) {
             diag_factor16<T>(dacc, dA, xl, i0, n, b, ld, CB, R, status, c);
             mark(false, 13);
@@ -1140,6 +1419,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
             }
         }
+#endif
         __syncthreads();
     }
 }
@@ -3654,7 +3934,8 @@ int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
 }
 
 template <typename T, int M, int RP>
-int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
+int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace,
+                 unsigned long long* mbox) {
     constexpr int C5_NT = 64 * (16 / RP);
     const int64_t n_tiles = (bd.n + C4_TB - 1) / C4_TB;
     int dev = 0, cus = 0;
@@ -3669,7 +3950,7 @@ int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol5<T, M, RP><<<(unsigned)grid, C5_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
-                                                     status + 1, n_tiles, trace);
+                                                         status + 1, n_tiles, trace, mbox);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -3707,8 +3988,11 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     const int64_t bw = bd.b, need = bw + TR;
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
     DBuf prog;
-    BSM_TRY(prog.alloc((n_tiles + 1) * sizeof(int) + 16));
-    BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, (n_tiles + 1) * sizeof(int) + 16, s));
+    // progress flags, status, ticket; then band_chol5's mailbox slots (zeroed with them)
+    const size_t mb_off = ((n_tiles + 1) * sizeof(int) + 16 + 255) & ~(size_t)255;
+    const size_t prog_bytes = mb_off + (size_t)MB_SLOTS * MB_SLOT_WORDS * sizeof(unsigned long long);
+    BSM_TRY(prog.alloc(prog_bytes));
+    BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, prog_bytes, s));
     int* status = prog.as<int>() + n_tiles;
     // optional diagnostic trace: per-tile-row clocks + blocking-poll counts
     DBuf trace_buf;
@@ -3730,17 +4014,16 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     if (v5) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;
-        // BSM_CHOL_RPW: rows per wave (2: eight waves, 4 (default): four)
-        const char* rpe = getenv("BSM_CHOL_RPW");
-        auto go = [&]<int RP>() {
-            if (w4 <= 64) rc = launch_chol5<T, 1, RP>(bd, prog.as<int>(), status, s, tr);
-            else if (w4 <= 128) rc = launch_chol5<T, 2, RP>(bd, prog.as<int>(), status, s, tr);
-            else if (w4 <= 256) rc = launch_chol5<T, 4, RP>(bd, prog.as<int>(), status, s, tr);
-            else if (w4 <= 512) rc = launch_chol5<T, 8, RP>(bd, prog.as<int>(), status, s, tr);
-            else rc = launch_chol5<T, 16, RP>(bd, prog.as<int>(), status, s, tr);
-        };
-        if (rpe && atoi(rpe) == 2) go.template operator()<2>();
-        else go.template operator()<4>();
+        // BSM_C5_MBOX=0: the last tile waits on the progress flag and loads the
+        // band instead of the mailbox (A/B)
+        const char* mbe = getenv("BSM_C5_MBOX");
+        unsigned long long* mb =
+            (mbe && atoi(mbe) == 0) ? nullptr : reinterpret_cast<unsigned long long*>(static_cast<char*>(prog.p) + mb_off);
+        if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr, mb);
+        else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr, mb);
+        else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr, mb);
+        else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr, mb);
+        else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr, mb);
     } else if (v4) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15

@@ -162,7 +162,7 @@ def test_csr_triangular_solves_vs_oracle(orc, dtype):
 @pytest.mark.parametrize("g", [5, 17, 40, 63, 100])
 def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
     """Every Cholesky kernel (BSM_CHOL_VARIANT 0 = band_chol3, 1 = band_chol,
-    4 = band_chol4) gives the band oracle's factor bit for bit, including
+    4 = band_chol4, 5 = band_chol5) gives the band oracle's factor bit for bit, including
     bandwidths that are not a multiple of the 16-row tiles and last
     row-blocks that are cut short."""
     n = g * g
@@ -170,9 +170,8 @@ def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
     v = v.astype(dtype)
     expect = orc.cholesky(n, n, rp, ci, v, band=True)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
-    for variant in ("0", "1", "4", "5", "5r2"):
-        monkeypatch.setenv("BSM_CHOL_VARIANT", variant[0])
-        monkeypatch.setenv("BSM_CHOL_RPW", "2" if variant == "5r2" else "4")
+    for variant in ("0", "1", "4", "5"):
+        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
         assert_csr_exact(A.cholesky_decomp(), *expect)
 
 
@@ -193,7 +192,7 @@ def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
         del L
     for a, b, c in zip(out["0"], out["4"], out["5"]):
         assert np.array_equal(a, b)
-        assert np.array_equal(a, c)  # band_chol5 (four rows per wave)
+        assert np.array_equal(a, c)  # band_chol5 (two rows per wave)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
