@@ -36,12 +36,6 @@
 
 #include "bsm_internal.hpp"
 
-// band_chol5's diagonal block: 0 diag_factor16, 1 diag_factor16x<SM = 1>
-// (default), 2 diag_factor16x<SM = 2> + stores by the whole workgroup (A/B builds)
-#ifndef BSM_C5_DIAG
-#define BSM_C5_DIAG 1
-#endif
-
 namespace bsm {
 namespace {
 
@@ -198,40 +192,6 @@ __device__ __forceinline__ void diag_factor16(const T (*dacc)[17], const T (*dA)
 __device__ __forceinline__ double sqrt_pos(double x) { return __dsqrt_rn(x); }
 __device__ __forceinline__ float sqrt_pos(float x) { return __double2float_rn(__dsqrt_rn((double)x)); }
 
-// band_chol5's chain hop (row-block J's diagonal block and 1/L to row-block
-// J + 1's last tile) as 8-byte {tag = J + 1, 32-bit half} granules written
-// sc1: the data is the flag (the guide's R2 hand-off), so the consumer's first
-// complete sweep IS its load, with no drain before a flag, no flag round trip
-// and no barrier. Slot J % MB_SLOTS; word ((t * 16 + u) * 2 + half) holds
-// L[16J + t + u][16J + t] for u >= 1 and 1/L[16J + t][16J + t] at u = 0.
-// The slots are zeroed per call (tag 0 never matches; J + 1 - MB_SLOTS, the
-// slot's previous tag, neither).
-constexpr int MB_SLOTS = 64;
-constexpr int MB_SLOT_WORDS = 16 * 16 * 2;
-template <typename T> __device__ __forceinline__ void mb_put(unsigned long long* g, unsigned tag, T v) {
-    const unsigned long long tg = (unsigned long long)tag << 32;
-    if constexpr (sizeof(T) == 8) {
-        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-        __hip_atomic_store(g, tg | (u & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(g + 1, tg | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        __hip_atomic_store(g, tg | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-// one granule read: the value, and whether its tag(s) match
-template <typename T> __device__ __forceinline__ T mb_get(const unsigned long long* g, unsigned tag, bool& ok) {
-    if constexpr (sizeof(T) == 8) {
-        const unsigned long long lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = (unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag;
-        return __builtin_bit_cast(T, (hi << 32) | (lo & 0xffffffffull));
-    } else {
-        const unsigned long long x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = (unsigned)(x >> 32) == tag;
-        return __builtin_bit_cast(T, (unsigned)x);
-    }
-}
-
 // diag_factor16 with the per-step side work taken off the pivot chain: the
 // pivot check is one class test per step folded into a flag (one atomic at
 // the end), 1/L[t][t] is kept by lane t (one select), and L's column t goes
@@ -242,17 +202,11 @@ template <typename T> __device__ __forceinline__ T mb_get(const unsigned long lo
 // IL: each step's updates of the columns past the next pivot's are issued in
 // the following step, beside its sqrt -> reciprocal chain (measured slower:
 // 8.7k against 8.1k cycles per block without, against 9.1k for diag_factor16;
-// scripts/micro/diag_factor.hip). hook() runs after step 3 (band_chol5: the
-// factor wave's drain and arrival for the last tile's progress flag).
+// scripts/micro/diag_factor.hip).
 // Same operations per element in the same order: the same bits as diag_factor16.
-struct NoHook {
-    __device__ void operator()() const {}
-};
-template <typename T, int SM, bool IL = false, typename Hook = NoHook>
+template <typename T, int SM, bool IL = false>
 __device__ __forceinline__ void diag_factor16x(const T (*dacc)[17], const T (*dA)[17], T (*Ls)[17], T* Rs, int i0,
-                                               int64_t n, int64_t b, int64_t ld, T* CB, T* R, int* status, int c,
-                                               unsigned long long* mb = nullptr, unsigned mb_tag = 0,
-                                               Hook hook = {}) {
+                                               int64_t n, int64_t b, int64_t ld, T* CB, T* R, int* status, int c) {
     using A = Arith<T>;
     constexpr int NB = 16;
     asm volatile("" : "+v"(c));
@@ -293,19 +247,12 @@ __device__ __forceinline__ void diag_factor16x(const T (*dacc)[17], const T (*dA
         }
 #pragma unroll
         for (int j = t + 1; j < NB; ++j) asm volatile("" : "+v"(q[j]));
-        if constexpr (t == 3) hook();  // a quarter in: the caller's earlier stores have drained by now
     };
     [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
         (step(std::integral_constant<int, ts>{}), ...);
     }(std::make_integer_sequence<int, NB>{});
     if (c == 0 && !pd) atomicOr(status, ST_NOT_PD);
     if constexpr (SM == 1) {
-        if (mb && c < NB) {  // the chain hop first (mailbox granules), then the band
-#pragma unroll
-            for (int t = 0; t < NB; ++t)
-                if (t < r) mb_put(mb + (t * 16 + (r - t)) * 2, mb_tag, xs[t]);
-            mb_put(mb + (r * 16) * 2, mb_tag, myrt);
-        }
         if (c < NB && live) {
             T* p = CB + (int64_t)i0 * ld + r;  // L[i0 + r][i0 + t] = CB[(i0 + t) ld + r - t]
 #pragma unroll
@@ -1072,24 +1019,32 @@ __global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_
 }
 
 // ---------------------------------------------------------------------------
-// band_chol5 (round 4): band_chol4's tile events with FOUR rows per wave (4
-// waves, 256 threads, one wave per SIMD). A row-block spends most of each tile
-// in U, where every wave reads the staged column tile from LDS for its own
-// row (band_chol4: 16 waves x 16 steps x (M - m) slots of 512-B reads, 15.2k
-// cycles per tile at C5, LDS-bound, profiles/r01_ac_chol4_trace.log); here one
-// read of a column value feeds the wave's four rows, a quarter of the LDS
-// traffic. The row-blocks complete one per (T + U) of a tile (each row-block
-// walks its ~b/16 tiles in order behind the row-block above), so U is on the
-// factor's critical rate. T solves the four rows' chains interleaved. Per
-// element the same operations in the same order as band_chol4 and the
+// band_chol5 (round 4; the default for b <= 1009): band_chol4's tile events
+// with TWO rows per wave (8 waves, 512 threads), tuned for the completion
+// chain. Row-block I completes one diagonal block after row-block I - 1, so
+// its last tile's T, the diagonal sums and the 16 x 16 factor set the rate
+// (a row-block's other tiles run behind completed row-blocks, off the chain):
+//  * T reads row-block K's diagonal tile, 1/L and its own A values straight
+//    into registers (no LDS staging, one barrier), and the 16 chain steps take
+//    lane t's accumulator, 1/L and A by DPP row_newbcast (VALU only);
+//  * U (16 column steps over the staged column tile) is software-pipelined:
+//    step t + 1's LDS reads go out before step t's multiply-adds;
+//  * the last tile's stores drain behind the diagonal sums and the factor:
+//    its progress flag is raised by whichever wave arrives last at an LDS
+//    counter after its own drain (the factor wave from inside the factor);
+//  * the factor is diag_factor16x (pivot check folded into a flag, stores
+//    after the 16 steps: 8.1k instead of 9.1k cycles per block alone).
+// Per element the same operations in the same order as band_chol4 and the
 // reference (ascending k, no FMA, (1/L[k][k]) * (A - sum)): the same bits.
+// (RP = 4 -- 4 waves, 442 VGPRs -- gave wrong bits from row-block 14 of the
+// 500^2 case, deterministically, while RP = 2 and band_chol4 agree with the
+// oracle; it is not instantiated.)
 // ---------------------------------------------------------------------------
 template <typename T, int M, int RP>  // RP rows per wave: 16 / RP waves
 __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                     T* __restrict__ R, int* __restrict__ fprog,
                                                     int* __restrict__ status, int* __restrict__ ticket,
-                                                    int64_t n_tiles, unsigned long long* __restrict__ trace,
-                                                    unsigned long long* __restrict__ mbox) {
+                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
     using A = Arith<T>;
     constexpr int CS = 64 + 64 * M;
     constexpr int C5_NT = 64 * (16 / RP);
@@ -1098,13 +1053,10 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
     __shared__ T xl[16];
     __shared__ long long tph[16];
-    __shared__ int s_arr;
-#if BSM_C5_DIAG != 1
-    mbox = nullptr;  // only diag_factor16x<T, 1> fills the mailbox
-#endif
+    __shared__ int s_arr;  // waves past the last tile's stores (after the windows)
+    if (threadIdx.x == 0) s_arr = 0;
     const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
     for (int q = tid; q < C4_TB * 64; q += C5_NT) colK[q >> 6][q & 63] = A::zero();
-    if (tid == 0) s_arr = 0;
     const int ib = (int)b;
     auto poll_all = [&](int jlo, int jhi, int need) {  // wave 0: fprog[J] >= need for J in [jlo, jhi)
         bool ok = true;
@@ -1152,13 +1104,18 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         for (int q = 0; q < RP; ++q)
 #pragma unroll
             for (int m = 0; m < M; ++m) acc[q][m] = A::zero();
-        T accT[RP], aT[RP];
+        // the diagonal block's A values go to LDS now (dA is free since the
+        // last row-block's factor): their load is waited for here, not behind
+        // the last tile's stores
+        T accT[RP];
 #pragma unroll
         for (int q = 0; q < RP; ++q) {
             const int rw = r0 + q;
             accT[q] = A::zero();
-            aT[q] = (c < C4_TB && c <= rw && rw - c <= ib && i0 + rw < n) ? CB[(int64_t)(i0 + c) * ld + (rw - c)]
-                                                                         : A::zero();
+            const T aT = (c < C4_TB && c <= rw && rw - c <= ib && i0 + rw < n)
+                             ? ld_sc1(CB + (int64_t)(i0 + c) * ld + (rw - c))
+                             : A::zero();
+            if (c < TR) dA[rw][c] = aT;
         }
         auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
 #pragma unroll 1
@@ -1183,48 +1140,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 // registers (no LDS staging, no second barrier): lane c takes
                 // L[k0 + t + u][k0 + t], u = c - lb - t, for every t
                 T dvr[C4_TB], myR;
-                if (mbox && lastK) {
-                    // the chain hop: row-block I - 1's mailbox slot, swept by
-                    // every wave until all its granules carry tag I (the barrier
-                    // first: hist is still being read by U of the previous tile)
-                    __syncthreads();
-                    mark(true, 0);
-                    const unsigned long long* slot = mbox + (int64_t)(K & (MB_SLOTS - 1)) * MB_SLOT_WORDS;
-                    long long spins = 0;
-                    while (true) {
-                        bool all = true, g;
+                if (w == 0) poll_all(K, K + 1, K + 1);
+                mark(lastK, 0);
+                __syncthreads();
 #pragma unroll
-                        for (int t = 0; t < C4_TB; ++t) {
-                            const int u = c - lb - t;
-                            const bool ok = u >= 1 && t + u <= 15 && u <= ib;
-                            const T v = mb_get<T>(slot + (ok ? (t * 16 + u) * 2 : 0), (unsigned)I, g);
-                            dvr[t] = ok ? v : A::zero();
-                            all &= g || !ok;
-                        }
-                        myR = mb_get<T>(slot + ((c & 15) * 16) * 2, (unsigned)I, g);
-                        all &= g;
-                        if (__all(all)) break;
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spins > SPIN_LIMIT ||
-                            ((spins & 1023) == 0 &&
-                             (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
-                            if (c == 0) atomicOr(status, ST_TIMEOUT);
-                            break;
-                        }
-                    }
-                } else {
-                    if (w == 0) poll_all(K, K + 1, K + 1);
-                    mark(lastK, 0);
-                    __syncthreads();
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) {
-                        const int u = c - lb - t;
-                        const bool ok = u >= 1 && t + u <= 15 && u <= ib;
-                        const T v = ld_sc1(CB + (((int64_t)(k0 + t) * ld + u) & -(int64_t)ok));
-                        dvr[t] = ok ? v : A::zero();
-                    }
-                    myR = ld_sc1(&R[k0 + (c & 15)]);
+                for (int t = 0; t < C4_TB; ++t) {
+                    const int u = c - lb - t;
+                    const bool ok = u >= 1 && t + u <= 15 && u <= ib;
+                    const T v = ld_sc1(CB + (((int64_t)(k0 + t) * ld + u) & -(int64_t)ok));
+                    dvr[t] = ok ? v : A::zero();
                 }
+                myR = ld_sc1(&R[k0 + (c & 15)]);
                 mark(lastK, 1);
                 // The tile's 16 columns are lanes lb .. lb + 15 of slot m: one DPP row
                 // (row e). Step t takes lane lb + t's accumulator, 1/L and A by
@@ -1251,19 +1177,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                      }()),
                      ...);
                 }(std::make_integer_sequence<int, C4_TB>{});
-                if (inrow) {
+                if (inrow) {  // (the last tile's band stores wait until the factor runs: below)
                     const int cl = c & 15;
 #pragma unroll
                     for (int q = 0; q < RP; ++q) {
                         const int rw = r0 + q;
                         hist[cl][rw] = xv[q];
                         const int d = i0 + rw - k0 - cl;
-                        if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
+                        if (!lastK && d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
                     }
                 }
                 if (lastK) {  // no rows in between: the diagonal-block sums of this tile
-                    // (the stores drain behind them: this tile's flag goes up at
-                    // the diagonal block's staging barrier, after the window)
                     mark(true, 2);
                     __syncthreads();
                     mark(true, 4);
@@ -1343,83 +1267,49 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
             (window(std::integral_constant<int, ms>{}), ...);
         }(std::make_integer_sequence<int, M>{});
         // ---------------- the 16 x 16 diagonal block (wave 0)
-        if (c < TR) {
+        // (the LDS addresses from an opaque copy of the thread index: hoisted,
+        // they were spilled, and the reload's vmcnt(0) waited for the last
+        // tile's write-through stores: 3.6k cycles on the chain)
+        int tix = tid;
+        asm volatile("" : "+v"(tix));
+        if ((tix & 63) < TR) {
 #pragma unroll
-            for (int q = 0; q < RP; ++q) {
-                dacc[r0 + q][c] = accT[q];
-                dA[r0 + q][c] = aT[q];
-            }
+            for (int q = 0; q < RP; ++q) dacc[RP * (tix >> 6) + q][tix & 63] = accT[q];
         }
-#if BSM_C5_DIAG == 1
-        __syncthreads();  // dacc / dA visible; the last tile's stores drain behind the factor
+        __syncthreads();  // dacc visible
         mark(false, 12);
-        // The last tile's progress flag (fprog[I] = I, which the next row-blocks'
-        // U of tile I - 1 waits for) without a drain on the chain: every wave
-        // waits for its own stores, then arrives at an LDS counter, and the last
-        // to arrive raises the flag (MI355X_MICROARCH.md "Valid forms": per-wave
-        // arrival in LDS); the factor wave arrives from inside the factor, when
-        // its stores have long drained. An atomic max: the completion value
-        // I + 1 may already be there.
-        auto arrive = [&]() __attribute__((always_inline)) {
+        if (tid < 64) {
+            diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
+            mark(false, 13);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 1) {
+            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mark(false, 14);
+            if (tr0) {
+#pragma unroll
+                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
+                atomicAdd(&trace[15], 1ull);
+                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
+            }
+        } else if (K0 < (int)I) {
+            // While wave 0 factors, the other waves store the last tile's L
+            // (from hist) and raise its progress flag (fprog[I] = I, which the
+            // next row-blocks' U of tile I - 1 waits for): no store was in
+            // flight before the barrier, so no wait there drained one. Each
+            // wave waits for its own stores and arrives at an LDS counter; the
+            // last to arrive raises the flag (MI355X_MICROARCH.md "Valid
+            // forms": per-wave arrival). An atomic max: the completion value
+            // I + 1 may already be there.
+            const int k0 = i0 - C4_TB;
+            for (int e = tid - 64; e < C4_TB * C4_TB; e += C5_NT - 64) {
+                const int t = e >> 4, rw = e & 15, d = i0 + rw - k0 - t;
+                if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + t) * ld + d], hist[t][rw]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 2) {
                 s_arr = 0;
                 __hip_atomic_fetch_max(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-        };
-        if (tid < 64) {
-            diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c,
-                                 mbox ? mbox + (I & (MB_SLOTS - 1)) * MB_SLOT_WORDS : nullptr, (unsigned)I + 1, arrive);
-            mark(false, 13);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mark(false, 14);
-            if (tr0) {
-#pragma unroll
-                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
-                atomicAdd(&trace[15], 1ull);
-                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
-            }
-        } else {
-            arrive();
         }
-#else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tile's stores
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mark(false, 12);
-#endif
-#if BSM_C5_DIAG == 2
-        // the block to LDS (over dacc / xl, read before), stored by every thread
-        if (tid < 64) diag_factor16x<T, 2>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
-        mark(false, 13);
-        __syncthreads();
-        diag_store16<T, C5_NT>(dacc, xl, i0, n, b, ld, CB, R, tid);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        mark(false, 14);
-        if (tr0) {
-#pragma unroll
-            for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
-            atomicAdd(&trace[15], 1ull);
-            atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
-        }
-#elif BSM_C5_DIAG == 0
-        if (tid < 64) {
-            diag_factor16<T>(dacc, dA, xl, i0, n, b, ld, CB, R, status, c);
-            mark(false, 13);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mark(false, 14);
-            if (tr0) {
-#pragma unroll
-                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
-                atomicAdd(&trace[15], 1ull);
-                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
-            }
-        }
-#endif
         __syncthreads();
     }
 }
@@ -3934,8 +3824,7 @@ int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
 }
 
 template <typename T, int M, int RP>
-int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace,
-                 unsigned long long* mbox) {
+int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
     constexpr int C5_NT = 64 * (16 / RP);
     const int64_t n_tiles = (bd.n + C4_TB - 1) / C4_TB;
     int dev = 0, cus = 0;
@@ -3950,7 +3839,7 @@ int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
     band_chol5<T, M, RP><<<(unsigned)grid, C5_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
-                                                         status + 1, n_tiles, trace, mbox);
+                                                         status + 1, n_tiles, trace);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -3988,11 +3877,8 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     const int64_t bw = bd.b, need = bw + TR;
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
     DBuf prog;
-    // progress flags, status, ticket; then band_chol5's mailbox slots (zeroed with them)
-    const size_t mb_off = ((n_tiles + 1) * sizeof(int) + 16 + 255) & ~(size_t)255;
-    const size_t prog_bytes = mb_off + (size_t)MB_SLOTS * MB_SLOT_WORDS * sizeof(unsigned long long);
-    BSM_TRY(prog.alloc(prog_bytes));
-    BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, prog_bytes, s));
+    BSM_TRY(prog.alloc((n_tiles + 1) * sizeof(int) + 16));
+    BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, (n_tiles + 1) * sizeof(int) + 16, s));
     int* status = prog.as<int>() + n_tiles;
     // optional diagnostic trace: per-tile-row clocks + blocking-poll counts
     DBuf trace_buf;
@@ -4007,23 +3893,18 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     // band_chol3 indexes the band with 32-bit offsets
     const bool fits32 = (int64_t)a->rows * (bw + 1) + band_pad(bw + 1) < ((int64_t)1 << 31);
     const bool v1 = (cv && atoi(cv) == 1) || bw > 64 * 16 || !fits32;
-    // default band_chol4 (tile events); BSM_CHOL_VARIANT = 0 band_chol3, 1 band_chol (A/B)
+    // default band_chol5 (tile events, two rows per wave); BSM_CHOL_VARIANT = 4 band_chol4, 0 band_chol3, 1 band_chol (A/B)
     const bool v4 = (!cv || atoi(cv) == 4 || atoi(cv) == 5) && bw + C4_TB - 1 <= 64 * 16;
-    // BSM_CHOL_VARIANT=5: band_chol5 (four rows per wave; A/B)
-    const bool v5 = v4 && cv && atoi(cv) == 5;
+    // default band_chol5 (two rows per wave); BSM_CHOL_VARIANT=4: band_chol4 (A/B)
+    const bool v5 = v4 && !(cv && atoi(cv) == 4);
     if (v5) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;
-        // BSM_C5_MBOX=0: the last tile waits on the progress flag and loads the
-        // band instead of the mailbox (A/B)
-        const char* mbe = getenv("BSM_C5_MBOX");
-        unsigned long long* mb =
-            (mbe && atoi(mbe) == 0) ? nullptr : reinterpret_cast<unsigned long long*>(static_cast<char*>(prog.p) + mb_off);
-        if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr, mb);
-        else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr, mb);
-        else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr, mb);
-        else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr, mb);
-        else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr, mb);
+        if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr);
+        else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr);
     } else if (v4) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15

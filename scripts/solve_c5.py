@@ -47,6 +47,12 @@ def system(g, dt):
     return rp, ci, v.astype(dt), b.astype(dt), x_true
 
 
+def band_kernel():
+    """The reference-order factor kernel the library picks (BSM_CHOL_VARIANT)."""
+    return {"4": "band_chol4", "0": "band_chol3", "1": "band_chol"}.get(os.environ.get("BSM_CHOL_VARIANT", ""),
+                                                                      "band_chol5")
+
+
 def leading_system(g, rows_g):
     """The leading principal block of the g x g system: the first rows_g grid
     rows (R = rows_g * g unknowns, band g). Its band Cholesky is the first R
@@ -143,7 +149,7 @@ def main():
             "wall_ms": round(1e3 * float(np.median(walls)), 2),
             "stages_ms": st,
             "device_ms_total": round(sum(st.values()), 2),
-            "factor": {"kernel": "band_chol4 (reference order)" if order == "reference" else "blk_chol (blocked)",
+            "factor": {"kernel": f"{band_kernel()} (reference order)" if order == "reference" else "blk_chol (blocked)",
                        "flops": flops, "ms": st.get("cholesky"),
                        "achieved_TFs": round(flops / (st["cholesky"] * 1e-3) / 1e12, 3) if st.get("cholesky") else None,
                        "peak_TFs": F64_PEAK_TFS,

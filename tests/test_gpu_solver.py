@@ -352,7 +352,7 @@ def test_short_rhs_column_panics():
     assert np.asarray(got.v).tolist() == [3.0, 2.0]
 
 
-@pytest.mark.parametrize("variant", ["4", "0", "1"])  # band_chol4 / band_chol3 / band_chol
+@pytest.mark.parametrize("variant", ["5", "4", "0", "1"])  # band_chol5 / band_chol4 / band_chol3 / band_chol
 def test_cholesky_finishes_beside_a_kernel_holding_cus(orc, monkeypatch, variant):
     """The persistent factor kernels take row-blocks by atomic ticket, so
     they finish (bit-exact) while other work holds part of the GPU: large f64
