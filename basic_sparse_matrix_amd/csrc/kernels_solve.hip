@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     constexpr int CS = 64 + 64 * M;
     constexpr int C5_NT = 64 * (16 / RP);
     __shared__ T colK[C4_TB][CS];
-    __shared__ T hist[C4_TB][C4_TB + 1];
+    __shared__ T hist2[2][C4_TB][C4_TB + 1];  // by tile parity: T(K + 1) may write while U(K) reads
     __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
     __shared__ T xl[16];
     __shared__ long long tph[16];
@@ -1117,6 +1117,60 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                              : A::zero();
             if (c < TR) dA[rw][c] = aT;
         }
+        // U over accumulator slots [LO, HI) for the column tile staged in colK
+        // (tile slot mK, lanes lbK..lbK+15) with the tile's x in hs; WT: also the
+        // diagonal-block sums. Software-pipelined: step t + 1's LDS reads (x,
+        // column values, diagonal-block value) go out before step t's
+        // multiply-adds. Each tile's U is split (look-ahead): the slot holding
+        // the next tile's columns right after the tile's T, so the next T can
+        // start, the other slots after that T. Per accumulator the tiles still
+        // come in ascending order (T touches only its own tile's slot), so the
+        // bits are unchanged; the split takes U's bulk off the dependency from
+        // one row-block's T(K) to the next one's T(K + 1) (~40k cycles per
+        // row-block before, with the whole U(K) on that path).
+        auto u_run = [&]<int LO, int HI, bool WT>(std::integral_constant<int, LO>, std::integral_constant<int, HI>,
+                                                  std::bool_constant<WT>, int mK, int lbK,
+                                                  T (*hs)[C4_TB + 1]) __attribute__((always_inline)) {
+            if constexpr (LO < HI) {
+                struct UB {
+                    T cv[HI - LO], x[RP], hv;
+                };
+                auto u_load = [&](int t, UB& ub) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int q = 0; q < RP; ++q) ub.x[q] = hs[t][r0 + q];
+                    const T* col = &colK[t][64 + c - lbK - C4_TB];  // col[64 (mm - mK)]: column jb + c + 64 mm
+#pragma unroll
+                    for (int mm = LO; mm < HI; ++mm) ub.cv[mm - LO] = col[64 * (mm - mK)];
+                    if constexpr (WT) ub.hv = hs[t][c & 15];
+                };
+                auto u_add = [&](const UB& ub) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int mm = LO; mm < HI; ++mm)
+                        if (jb + 64 * mm < i0) {
+#pragma unroll
+                            for (int q = 0; q < RP; ++q)
+                                acc[q][mm] = A::add(acc[q][mm], A::mul(ub.x[q], ub.cv[mm - LO]));
+                        }
+                    if constexpr (WT) {
+                        if (c < C4_TB) {
+#pragma unroll
+                            for (int q = 0; q < RP; ++q) accT[q] = A::add(accT[q], A::mul(ub.x[q], ub.hv));
+                        }
+                    }
+                };
+                UB ua, ubb;
+                u_load(0, ua);
+#pragma unroll 1
+                for (int t = 0; t < C4_TB; t += 2) {
+                    u_load(t + 1, ubb);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u_add(ua);
+                    if (t + 2 < C4_TB) u_load(t + 2, ua);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u_add(ubb);
+                }
+            }
+        };
         auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
 #pragma unroll 1
             for (int e = 0; e < 4; ++e) {
@@ -1140,9 +1194,15 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 // registers (no LDS staging, no second barrier): lane c takes
                 // L[k0 + t + u][k0 + t], u = c - lb - t, for every t
                 T dvr[C4_TB], myR;
+#ifdef BSM_C5_WAVEPOLL
+                poll_all(K, K + 1, K + 1);  // every wave for itself: no barrier
+                mark(lastK, 0);
+#else
                 if (w == 0) poll_all(K, K + 1, K + 1);
                 mark(lastK, 0);
                 __syncthreads();
+#endif
+                auto& hist = hist2[K & 1];
 #pragma unroll
                 for (int t = 0; t < C4_TB; ++t) {
                     const int u = c - lb - t;
@@ -1208,9 +1268,19 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 mark(false, 2);
                 __syncthreads();
                 if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // ---------------- U: column tile K of the rows between, once they have it
+                // ---------------- the rest of U(K - 1): the slots after tile K's,
+                // which T(K) did not need (look-ahead: see u_run below)
                 mark(false, 3);
-                if (w == 0) poll_all(K + 1, (int)I, K + 1);
+                if (K > K0) {
+                    if (e) u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
+                                 std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1]);
+                    else if constexpr (m >= 1)
+                        u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
+                              std::false_type{}, m - 1, 48, hist2[(K - 1) & 1]);
+                }
+                mark(false, 5);
+                // ---------------- U(K): column tile K of the rows between, once they have it
+                if (w == 0) poll_all(K + 1, (int)I, K + 1);  // (K + 1 <= I - 1)
                 __syncthreads();
                 const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
                 for (int rr = tid; rr < cnt; rr += C5_NT) {
@@ -1222,43 +1292,15 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
                 }
                 __syncthreads();
-                mark(lastK, 4);
-                // software-pipelined: step t + 1's LDS reads (x, the column
-                // values, the diagonal-block value) go out before step t's
-                // multiply-adds, so the LDS latency overlaps the VALU work
-                struct UB {
-                    T cv[M], x[RP], hv;
-                };
-                auto u_load = [&](int t, UB& ub) __attribute__((always_inline)) {
-#pragma unroll
-                    for (int q = 0; q < RP; ++q) ub.x[q] = hist[t][r0 + q];
-                    const T* col = &colK[t][64 + c - lb - C4_TB];  // col[64 (mm - m)]: column jb + c + 64 mm
-#pragma unroll
-                    for (int mm = m; mm < M; ++mm) ub.cv[mm] = col[64 * (mm - m)];
-                    ub.hv = hist[t][c & 15];
-                };
-                auto u_add = [&](const UB& ub) __attribute__((always_inline)) {
-#pragma unroll
-                    for (int mm = m; mm < M; ++mm)
-                        if (jb + 64 * mm < i0) {
-#pragma unroll
-                            for (int q = 0; q < RP; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(ub.x[q], ub.cv[mm]));
-                        }
-                    if (c < C4_TB) {
-#pragma unroll
-                        for (int q = 0; q < RP; ++q) accT[q] = A::add(accT[q], A::mul(ub.x[q], ub.hv));
-                    }
-                };
-                UB ua, ubb;
-                u_load(0, ua);
-#pragma unroll 1
-                for (int t = 0; t < C4_TB; t += 2) {
-                    u_load(t + 1, ubb);
-                    __builtin_amdgcn_sched_barrier(0);
-                    u_add(ua);
-                    if (t + 2 < C4_TB) u_load(t + 2, ua);
-                    __builtin_amdgcn_sched_barrier(0);
-                    u_add(ubb);
+                mark(false, 4);
+                // now only the slot holding tile K + 1 (and the diagonal-block
+                // sums); the other slots after the next T
+                if (e < 3) {
+                    u_run(std::integral_constant<int, m>{}, std::integral_constant<int, m + 1>{}, std::true_type{}, m,
+                          lb, hist);
+                } else if constexpr (m + 1 < M) {
+                    u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, m + 2>{},
+                          std::true_type{}, m, lb, hist);
                 }
                 mark(lastK, 5);
             }
@@ -1302,7 +1344,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
             const int k0 = i0 - C4_TB;
             for (int e = tid - 64; e < C4_TB * C4_TB; e += C5_NT - 64) {
                 const int t = e >> 4, rw = e & 15, d = i0 + rw - k0 - t;
-                if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + t) * ld + d], hist[t][rw]);
+                if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + t) * ld + d], hist2[(I - 1) & 1][t][rw]);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 2) {
