@@ -1278,6 +1278,9 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                         u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
                               std::false_type{}, m - 1, 48, hist2[(K - 1) & 1]);
                 }
+#ifdef BSM_C5_PROBE_REST  // sensitivity probe (A/B builds only): ~8k cycles more per non-last tile
+                __builtin_amdgcn_s_sleep(127);
+#endif
                 mark(false, 5);
                 // ---------------- U(K): column tile K of the rows between, once they have it
                 if (w == 0) poll_all(K + 1, (int)I, K + 1);  // (K + 1 <= I - 1)
@@ -1322,6 +1325,9 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         mark(false, 12);
         if (tid < 64) {
             diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
+#ifdef BSM_C5_PROBE_CHAIN  // sensitivity probe (A/B builds only): ~8k cycles more on the completion chain
+            __builtin_amdgcn_s_sleep(127);
+#endif
             mark(false, 13);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
