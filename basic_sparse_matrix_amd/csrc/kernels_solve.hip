@@ -3948,11 +3948,19 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     if (v5) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;
+#ifdef BSM_C5_RP4  // four rows per wave (A/B build only)
+        if (w4 <= 64) rc = launch_chol5<T, 1, 4>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 128) rc = launch_chol5<T, 2, 4>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 256) rc = launch_chol5<T, 4, 4>(bd, prog.as<int>(), status, s, tr);
+        else if (w4 <= 512) rc = launch_chol5<T, 8, 4>(bd, prog.as<int>(), status, s, tr);
+        else rc = launch_chol5<T, 16, 4>(bd, prog.as<int>(), status, s, tr);
+#else
         if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr);
         else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr);
+#endif
     } else if (v4) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
