@@ -1128,9 +1128,10 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         // bits are unchanged; the split takes U's bulk off the dependency from
         // one row-block's T(K) to the next one's T(K + 1) (~40k cycles per
         // row-block before, with the whole U(K) on that path).
-        auto u_run = [&]<int LO, int HI, bool WT>(std::integral_constant<int, LO>, std::integral_constant<int, HI>,
-                                                  std::bool_constant<WT>, int mK, int lbK,
-                                                  T (*hs)[C4_TB + 1]) __attribute__((always_inline)) {
+        auto no_hook = []() {};
+        auto u_run = [&]<int LO, int HI, bool WT, typename Hook = decltype(no_hook)>(
+                         std::integral_constant<int, LO>, std::integral_constant<int, HI>, std::bool_constant<WT>,
+                         int mK, int lbK, T (*hs)[C4_TB + 1], Hook hook = {}) __attribute__((always_inline)) {
             if constexpr (LO < HI) {
                 struct UB {
                     T cv[HI - LO], x[RP], hv;
@@ -1168,6 +1169,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     if (t + 2 < C4_TB) u_load(t + 2, ua);
                     __builtin_amdgcn_sched_barrier(0);
                     u_add(ubb);
+                    if (t == 4) hook();  // (band_chol5's late flag: the stores before have drained)
                 }
             }
         };
@@ -1264,20 +1266,41 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     mark(true, 5);
                     return;
                 }
+#ifdef BSM_C5_LATEPUB
+                // T(K)'s flag without a drain or a barrier in this row-block's
+                // path: each wave waits for its own stores a few steps into the
+                // rest of U(K - 1) (they have drained by then) and arrives at the
+                // LDS counter; the last to arrive raises fprog[I] = K + 1
+                mark(false, 2);
+                bool arrived = false;
+                auto arrive_t = [&]() __attribute__((always_inline)) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 1) {
+                        s_arr = 0;
+                        __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    arrived = true;
+                };
+#else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 mark(false, 2);
                 __syncthreads();
                 if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                auto arrive_t = []() {};
+#endif
                 // ---------------- the rest of U(K - 1): the slots after tile K's,
                 // which T(K) did not need (look-ahead: see u_run below)
                 mark(false, 3);
                 if (K > K0) {
                     if (e) u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
-                                 std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1]);
+                                 std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1], arrive_t);
                     else if constexpr (m >= 1)
                         u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
-                              std::false_type{}, m - 1, 48, hist2[(K - 1) & 1]);
+                              std::false_type{}, m - 1, 48, hist2[(K - 1) & 1], arrive_t);
                 }
+#ifdef BSM_C5_LATEPUB
+                if (!arrived) arrive_t();
+#endif
 #ifdef BSM_C5_PROBE_REST  // sensitivity probe (A/B builds only): ~8k cycles more per non-last tile
                 __builtin_amdgcn_s_sleep(127);
 #endif
@@ -3948,19 +3971,11 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     if (v5) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;
-#ifdef BSM_C5_RP4  // four rows per wave (A/B build only)
-        if (w4 <= 64) rc = launch_chol5<T, 1, 4>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 128) rc = launch_chol5<T, 2, 4>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 256) rc = launch_chol5<T, 4, 4>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 512) rc = launch_chol5<T, 8, 4>(bd, prog.as<int>(), status, s, tr);
-        else rc = launch_chol5<T, 16, 4>(bd, prog.as<int>(), status, s, tr);
-#else
         if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr);
         else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr);
-#endif
     } else if (v4) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
