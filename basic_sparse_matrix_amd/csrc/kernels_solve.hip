@@ -4708,7 +4708,7 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
         g_blk_phase = "band setup";
         Band bd;
         DBuf dinv;
-        // BSM_BLK_CHOL=0: the reference-order factor (band_chol4) under the blocked solves (A/B)
+        // BSM_BLK_CHOL=0: the reference-order factor (band_factor: band_chol5 by default) under the blocked solves (A/B)
         const char* bc_env = getenv("BSM_BLK_CHOL");
         if (bc_env && atoi(bc_env) == 0) BSM_TRY(band_factor<T>(a, bd, s));
         else BSM_TRY(band_factor_blocked<T>(a, bd, dinv, s));

@@ -176,8 +176,8 @@ def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
 
 
 def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
-    """250,000 unknowns, bandwidth 500: band_chol4 and band_chol3 factors are
-    identical bit for bit (both are pinned to the oracle at smaller sizes)."""
+    """250,000 unknowns, bandwidth 500: band_chol3, band_chol4 and band_chol5 factors are
+    identical bit for bit (all are pinned to the oracle at smaller sizes)."""
     from oracle import pyoracle as orc
 
     g = 500

@@ -109,7 +109,7 @@ def test_blocked_random_spd_vs_oracle(orc):
 
 
 # blocked factor with the one-wave diagonal factor / with the panel diagonal factor /
-# the reference-order band_chol4 under the blocked solves (A/B)
+# the reference-order band factor (band_chol5) under the blocked solves (A/B)
 @pytest.mark.parametrize("blk_chol,panels", [("1", "3"), ("1", "0"), ("1", "1"), ("0", "0")])
 def test_blocked_poisson_250_f64_vs_reference_order(orc, monkeypatch, blk_chol, panels):
     """62,500 unknowns, bandwidth 250: blocked vs reference order on the GPU."""
