@@ -1053,6 +1053,13 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
     __shared__ T xl[16];
     __shared__ long long tph[16];
+#ifdef BSM_C5_EARLY_LAST
+    // A/B: the last tile's band stores and flag right after its T chain (drain
+    // + barrier + flag, as for the other tiles), instead of behind the factor
+    constexpr bool EARLY_LAST = true;
+#else
+    constexpr bool EARLY_LAST = false;
+#endif
     __shared__ int s_arr;  // waves past the last tile's stores (after the windows)
     if (threadIdx.x == 0) s_arr = 0;
     const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
@@ -1246,12 +1253,16 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                         const int rw = r0 + q;
                         hist[cl][rw] = xv[q];
                         const int d = i0 + rw - k0 - cl;
-                        if (!lastK && d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
+                        if (!(lastK && !EARLY_LAST) && d <= ib && i0 + rw < n)
+                            st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
                     }
                 }
                 if (lastK) {  // no rows in between: the diagonal-block sums of this tile
                     mark(true, 2);
+                    if constexpr (EARLY_LAST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
+                    if (EARLY_LAST && tid == 0)
+                        __hip_atomic_store(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     mark(true, 4);
                     if (c < C4_TB) {
                         T hc[C4_TB];
@@ -1361,7 +1372,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 atomicAdd(&trace[15], 1ull);
                 atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
             }
-        } else if (K0 < (int)I) {
+        } else if (!EARLY_LAST && K0 < (int)I) {
             // While wave 0 factors, the other waves store the last tile's L
             // (from hist) and raise its progress flag (fprog[I] = I, which the
             // next row-blocks' U of tile I - 1 waits for): no store was in
