@@ -1320,6 +1320,27 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 if (w == 0) poll_all(K + 1, (int)I, K + 1);  // (K + 1 <= I - 1)
                 __syncthreads();
                 const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
+#ifdef BSM_C5_STAGE2
+                // two rows per thread per pass: 32 loads in flight before the LDS writes
+                for (int rr = tid; rr < cnt; rr += 2 * C5_NT) {
+                    const int r2 = rr + C5_NT;
+                    const bool ok2 = r2 < cnt;
+                    const T* base = CB + (int64_t)k0 * ld + C4_TB + rr;
+                    const T* base2 = CB + (int64_t)k0 * ld + C4_TB + (ok2 ? r2 : rr);
+                    T v[C4_TB], v2[C4_TB];
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) {
+                        v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
+                        v2[t] = ld_sc1(base2 + (int64_t)t * (ld - 1));
+                    }
+#pragma unroll
+                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
+                    if (ok2) {
+#pragma unroll
+                        for (int t = 0; t < C4_TB; ++t) colK[t][64 + r2] = C4_TB + r2 - t <= ib ? v2[t] : A::zero();
+                    }
+                }
+#else
                 for (int rr = tid; rr < cnt; rr += C5_NT) {
                     const T* base = CB + (int64_t)k0 * ld + C4_TB + rr;
                     T v[C4_TB];
@@ -1328,6 +1349,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
 #pragma unroll
                     for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
                 }
+#endif
                 __syncthreads();
                 mark(false, 4);
                 // now only the slot holding tile K + 1 (and the diagonal-block
