@@ -1135,6 +1135,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         // bits are unchanged; the split takes U's bulk off the dependency from
         // one row-block's T(K) to the next one's T(K + 1) (~40k cycles per
         // row-block before, with the whole U(K) on that path).
+        // column tile K's rows k0 + 16 + rr, rr in [lo, hi), into colK
+        auto stage_rows = [&](int k0s, int lo, int hi) __attribute__((always_inline)) {
+            for (int rr = lo + tid; rr < hi; rr += C5_NT) {
+                const T* base = CB + (int64_t)k0s * ld + C4_TB + rr;
+                T v[C4_TB];
+#pragma unroll
+                for (int t = 0; t < C4_TB; ++t) v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
+#pragma unroll
+                for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
+            }
+        };
         auto no_hook = []() {};
         auto u_run = [&]<int LO, int HI, bool WT, typename Hook = decltype(no_hook)>(
                          std::integral_constant<int, LO>, std::integral_constant<int, HI>, std::bool_constant<WT>,
@@ -1303,6 +1314,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 // which T(K) did not need (look-ahead: see u_run below)
                 mark(false, 3);
                 if (K > K0) {
+#ifdef BSM_C5_SPLITSTAGE
+                    // its column tile's rows past the first 64 (row-blocks K + 4
+                    // on, whose T(K - 1) the first part did not wait for)
+                    const int kp = k0 - C4_TB, cntp = i0 - kp - C4_TB;
+                    if (cntp > 64) {
+                        if (w == 0) poll_all(K + 4, (int)I, K);
+                        __syncthreads();
+                        stage_rows(kp, 64, cntp);
+                        __syncthreads();
+                    }
+#endif
                     if (e) u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
                                  std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1], arrive_t);
                     else if constexpr (m >= 1)
@@ -1317,38 +1339,17 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
 #endif
                 mark(false, 5);
                 // ---------------- U(K): column tile K of the rows between, once they have it
+                const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
+#ifdef BSM_C5_SPLITSTAGE
+                // only the rows the next slot reads (row-blocks K + 1 .. K + 4);
+                // the others are polled and staged before the rest of U(K)
+                if (w == 0) poll_all(K + 1, (K + 5 < (int)I ? K + 5 : (int)I), K + 1);
+                __syncthreads();
+                stage_rows(k0, 0, cnt < 64 ? cnt : 64);
+#else
                 if (w == 0) poll_all(K + 1, (int)I, K + 1);  // (K + 1 <= I - 1)
                 __syncthreads();
-                const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
-#ifdef BSM_C5_STAGE2
-                // two rows per thread per pass: 32 loads in flight before the LDS writes
-                for (int rr = tid; rr < cnt; rr += 2 * C5_NT) {
-                    const int r2 = rr + C5_NT;
-                    const bool ok2 = r2 < cnt;
-                    const T* base = CB + (int64_t)k0 * ld + C4_TB + rr;
-                    const T* base2 = CB + (int64_t)k0 * ld + C4_TB + (ok2 ? r2 : rr);
-                    T v[C4_TB], v2[C4_TB];
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) {
-                        v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
-                        v2[t] = ld_sc1(base2 + (int64_t)t * (ld - 1));
-                    }
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
-                    if (ok2) {
-#pragma unroll
-                        for (int t = 0; t < C4_TB; ++t) colK[t][64 + r2] = C4_TB + r2 - t <= ib ? v2[t] : A::zero();
-                    }
-                }
-#else
-                for (int rr = tid; rr < cnt; rr += C5_NT) {
-                    const T* base = CB + (int64_t)k0 * ld + C4_TB + rr;
-                    T v[C4_TB];
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
-                }
+                stage_rows(k0, 0, cnt);
 #endif
                 __syncthreads();
                 mark(false, 4);
