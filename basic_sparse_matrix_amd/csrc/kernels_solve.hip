@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
         const int i0 = (int)(I * C4_TB);
         const int K0 = (i0 - ib > 0 ? i0 - ib : 0) / C4_TB, jb = C4_TB * K0;
-        const int r0 = RP * w;  // this wave's rows: i0 + r0 .. i0 + r0 + 3
+        const int r0 = RP * w;  // this wave's rows: i0 + r0 .. i0 + r0 + RP - 1
         long long tlast = 0;
         const bool tr0 = trace && tid == 0;
         if (tr0) {
@@ -1275,6 +1275,13 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     if (EARLY_LAST && tid == 0)
                         __hip_atomic_store(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     mark(true, 4);
+                    // the rows' own x come from hist (an LDS broadcast), NOT by
+                    // v_readlane of xv from lane lb + t: inside this lane-divergent
+                    // branch (exec = lanes 0-15) lanes 16-63 of xv are dead to the
+                    // compiler, and an exec-masked copy of xv (the RP = 4 build,
+                    // 442 registers) left lane lb + t stale: the diagonal sums of
+                    // row-blocks whose last tile sits at e >= 1 missed that tile
+                    // (round 5, scripts/chol_rp4_debug.py; DESIGN.md §4.5b')
                     if (c < C4_TB) {
                         T hc[C4_TB];
 #pragma unroll
@@ -1283,7 +1290,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                         for (int t = 0; t < C4_TB; ++t)
 #pragma unroll
                             for (int q = 0; q < RP; ++q)
-                                accT[q] = A::add(accT[q], A::mul(readlane_t(xv[q], lb + t), hc[t]));
+                                accT[q] = A::add(accT[q], A::mul(hist[t][r0 + q], hc[t]));
                     }
                     mark(true, 5);
                     return;
@@ -1380,6 +1387,16 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         }
         __syncthreads();  // dacc visible
         mark(false, 12);
+        // Completion (fprog[I] = I + 1) is raised by whichever of the 16 / RP
+        // waves arrives LAST at s_arr after its own drain: wave 0 (the factor)
+        // adds C5_W0, a store wave adds 1. Wave 0 publishing on its own drain
+        // could let a consumer's U(I - 1) (it waits for fprog[I] >= I) read
+        // the last tile's rows before the store waves' stores have landed
+        // (ADVICE r4). The last store wave raises fprog[I] = I if wave 0 is
+        // still factoring. Atomic max: the two values may land in either order.
+        constexpr int C5_NSW = C5_NT / 64 - 1;  // store waves
+        constexpr int C5_W0 = 0x100;
+        const bool store_waves = !EARLY_LAST && K0 < (int)I;
         if (tid < 64) {
             diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
 #ifdef BSM_C5_PROBE_CHAIN  // sensitivity probe (A/B builds only): ~8k cycles more on the completion chain
@@ -1387,7 +1404,12 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
 #endif
             mark(false, 13);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c == 0) {
+                if (!store_waves || (atomicAdd(&s_arr, C5_W0) & 0xff) == C5_NSW) {
+                    if (store_waves) s_arr = 0;
+                    __hip_atomic_fetch_max(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             mark(false, 14);
             if (tr0) {
 #pragma unroll
@@ -1395,24 +1417,27 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 atomicAdd(&trace[15], 1ull);
                 atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));
             }
-        } else if (!EARLY_LAST && K0 < (int)I) {
+        } else if (store_waves) {
             // While wave 0 factors, the other waves store the last tile's L
             // (from hist) and raise its progress flag (fprog[I] = I, which the
             // next row-blocks' U of tile I - 1 waits for): no store was in
             // flight before the barrier, so no wait there drained one. Each
-            // wave waits for its own stores and arrives at an LDS counter; the
-            // last to arrive raises the flag (MI355X_MICROARCH.md "Valid
-            // forms": per-wave arrival). An atomic max: the completion value
-            // I + 1 may already be there.
+            // wave waits for its own stores and arrives at s_arr; the last
+            // store wave raises the flag, or completion if wave 0 has already
+            // arrived (MI355X_MICROARCH.md "Valid forms": per-wave arrival).
             const int k0 = i0 - C4_TB;
             for (int e = tid - 64; e < C4_TB * C4_TB; e += C5_NT - 64) {
                 const int t = e >> 4, rw = e & 15, d = i0 + rw - k0 - t;
                 if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + t) * ld + d], hist2[(I - 1) & 1][t][rw]);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 2) {
-                s_arr = 0;
-                __hip_atomic_fetch_max(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c == 0) {
+                const int old = atomicAdd(&s_arr, 1);
+                if ((old & 0xff) == C5_NSW - 1) {  // the last store wave
+                    if (old >= C5_W0) s_arr = 0;   // wave 0 is done too: complete
+                    __hip_atomic_fetch_max(&fprog[I], old >= C5_W0 ? (int)I + 1 : (int)I, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
         __syncthreads();
@@ -4005,6 +4030,11 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     if (v5) {
         BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
         const int64_t w4 = bw + C4_TB - 1;
+#ifdef BSM_C5_RP4  // A/B build: four rows per wave (BSM_CHOL_RPW=4), M = 16 only
+        if (w4 > 512 && getenv("BSM_CHOL_RPW") && atoi(getenv("BSM_CHOL_RPW")) == 4)
+            rc = launch_chol5<T, 16, 4>(bd, prog.as<int>(), status, s, tr);
+        else
+#endif
         if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
         else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
