@@ -15,14 +15,14 @@
 // (b = max over rows of i - first_col(i)). Column k of L is contiguous, which
 // is what the right-looking update and the backward solve (rows of L^T) read.
 //
-// band_chol: persistent kernel, one 1024-thread workgroup per CU. Tile-row I
-// (32 rows) is swept column by column (right-looking): at column k the owner
-// threads finalise L[i][k] for the 32 rows, then every (i, j > k) accumulator
-// of the tile-row adds L[i][k] * L[j][k]. The accumulators (32 rows x b+32
-// columns) live in registers. Tile-row I needs column k of the rows above it,
-// i.e. of tile-rows < I: it waits on tile-row I-1's progress counter, which
-// is published every few columns (write-through sc1 stores + counter, the
-// hand-off of MI355X_MICROARCH.md "Valid forms", table row 1).
+// Kernels, one per stage and order (the measured variants they replaced
+// are in DESIGN.md §4.5-§4.6 and in git history):
+//   reference order (bit-exact): band_chol5 -> band_forward2 -> band_backward_reg;
+//   general exact path (non-SPD, unsorted, b > 1073; n <= 16384): chol_general;
+//   blocked (reassociated, within BASELINE's 1e-6 on f64): blk_chol ->
+//   blk_prep -> blk_trsv (forward, backward).
+// Hand-offs between workgroups use write-through (sc1) stores, a drain and a
+// relaxed agent flag (MI355X_MICROARCH.md "Valid forms", table row 1).
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -40,7 +40,6 @@ namespace bsm {
 namespace {
 
 constexpr int TR = 16;              // rows per tile-row
-constexpr int CH_THREADS = 1024;    // 16 rows x 64 column lanes
 constexpr long long SPIN_LIMIT = 1ll << 25;
 
 enum { ST_NOT_PD = 1, ST_TIMEOUT = 2, ST_EMPTY_ROW = 4, ST_COL_OOB = 8 };
@@ -110,10 +109,8 @@ __device__ __forceinline__ double div_by(double a, double b, double y) {
 }
 __device__ __forceinline__ float div_by(float a, float b, float) { return div_rn(a, b); }
 
-constexpr int BH_RING = 4096;        // x ring (power of two > b)
-// zero elements after the band: whole-segment reads of the last rows
-// (band_backward_hop) and band_chol3's unclamped staging of columns up to
-// 32 past the last one
+// zero elements after the band: the backward solve's fixed-length walks of
+// the last rows read them
 __host__ __device__ inline int64_t band_pad(int64_t ld) { return 32 * ld + 4096; }
 
 __device__ __forceinline__ double readlane_t(double v, int l) {
@@ -138,51 +135,6 @@ template <int J> __device__ __forceinline__ double rowbcast(double v) {
 }
 template <int J> __device__ __forceinline__ float rowbcast(float v) {
     return __int_as_float(rowbcast_i<J>(__float_as_int(v)));
-}
-
-// Factor the 16 x 16 diagonal block of row-block i0 (wave 0; lane r < 16 is
-// row i0 + r): q[j] = the row's accumulated sum for column i0 + j (dacc[r][j]),
-// a[j] = A[i0 + r][i0 + j] (dA[r][j]). All 16 columns unrolled, straight-line:
-// lane r keeps its row in registers, the pivot comes from lane t and L[j][t]
-// for the updates from lane j (v_readlane). Per element the reference's order
-// (sparse.rs:689-708): sum in ascending k, sqrt pivot, (1/L[t][t]) * (A - sum).
-// Stores L and R = 1 / L[t][t] write-through; the caller drains and publishes.
-template <typename T>
-__device__ __forceinline__ void diag_factor16(const T (*dacc)[17], const T (*dA)[17], T* xl, int i0, int64_t n,
-                                              int64_t b, int64_t ld, T* CB, T* R, int* status, int c) {
-    using A = Arith<T>;
-    constexpr int NB = 16;
-    // opaque lane index: otherwise the per-step masks and store offsets (functions of the lane
-    // and b only) are hoisted out of the caller's loop and kept, in spilled registers, for good
-    asm volatile("" : "+v"(c));
-    const int r = c & (NB - 1);
-    const bool live = i0 + r < n;
-    T q[NB], a[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        q[j] = live ? dacc[r][j] : A::zero();
-        a[j] = live ? dA[r][j] : (r == j ? (T)1 : A::zero());
-    }
-    auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
-        const T v = A::sub(a[t], q[t]);
-        const T piv = pow_half(rowbcast<t>(v));
-        const T rt = div_rn((T)1, piv);
-        const T x = r == t ? piv : A::mul(rt, v);  // L[i0 + r][i0 + t] for r >= t
-        if (c == 0 && i0 + t < n && (!(piv > A::zero()) || isinf(piv))) atomicOr(status, ST_NOT_PD);
-        if (c < NB && r >= t && live && r - t <= b) st_sc1(&CB[(int64_t)(i0 + t) * ld + (r - t)], x);
-        if (c == t && live) st_sc1(&R[i0 + t], rt);
-        // L[j][t] of the other rows by DPP row broadcast (q[t + 1] first: the next pivot's)
-        [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
-            ((q[t + 1 + js] = A::add(q[t + 1 + js], A::mul(x, rowbcast<t + 1 + js>(x)))), ...);
-        }(std::make_integer_sequence<int, NB - 1 - t>{});
-        // materialise the sums now: left to itself the compiler sinks every add to
-        // the step that reads it, keeping all x alive and putting t adds on the chain
-#pragma unroll
-        for (int j = t + 1; j < NB; ++j) asm volatile("" : "+v"(q[j]));
-    };
-    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-        (step(std::integral_constant<int, ts>{}), ...);
-    }(std::make_integer_sequence<int, NB>{});
 }
 
 // √ of a pivot the caller has checked positive and finite: IEEE sqrt
@@ -321,724 +273,46 @@ __global__ __launch_bounds__(256) void band_fill(const int64_t* __restrict__ rp,
     }
 }
 
-// ---------------------------------------------------------------------------
-// band_chol: see file header. 1024 threads:
-//   every thread: row r = t >> 6 of the tile-row, column lane c = t & 63,
-//     accumulators for j = jb + c + 64 m (m < M);
-//   all threads: prefetch, CH_PF columns ahead, the column values
-//     L[k+d][k] of the rows above the tile-row (into colL), the 16 A values
-//     A[i][k] of the tile-row and the pivot L[k][k] (into LDS double
-//     buffers), plus the predecessor's progress counter, so neither a data
-//     load nor a flag poll sits on a step's critical path. Every thread
-//     issues exactly four unconditional (clamped) loads per step, so the
-//     compiler can count its s_waitcnt vmcnt(N) across the ring;
-//   wave 0, lanes 0..15: store the tile-row's column k after each step.
-//     Its VMEM stream per step is 4 loads then 1 store, so "the store of
-//     step k - CH_PUB is done" is s_waitcnt vmcnt(5 * CH_PUB) -- a delayed
-//     publication that never waits on a fresh load or store.
-// A tile-row needs column k of the rows above it (tile-rows < I): it waits
-// on tile-row I-1's progress counter (columns done), published every
-// CH_PUB columns by wave 0 with the write-through (sc1) hand-off of
-// MI355X_MICROARCH.md "Valid forms", row 1.
-// ---------------------------------------------------------------------------
-constexpr int CH_PF = 4;   // prefetch distance (columns)
-constexpr int CH_PUB = 4;  // publication period (columns); lag = CH_PF + CH_PUB
+constexpr int C4_TB = 16;  // rows per row-block / columns per tile
 
-constexpr int TRACE_TILES = 4096;  // diagnostic trace (BSM_CHOL_TRACE=1): first tile-rows
-
-template <typename T, int M>
-__global__ __launch_bounds__(CH_THREADS) void band_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
-                                                         int* __restrict__ progress, int* __restrict__ status,
-                                                         int* __restrict__ ticket, int64_t n_tiles,
-                                                         unsigned long long* __restrict__ trace) {
-    using A = Arith<T>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    T* colL = reinterpret_cast<T*>(smem_raw);  // [b + 1]: L[k + d][k] of column k
-    __shared__ T rowval[TR];                   // L[i][k] of the tile-row's rows at this step
-    __shared__ T aval[2][TR];                  // A[i][k] of those rows (double buffer by k & 1)
-    __shared__ T pval[2];                      // L[k][k] for k < i0 (double buffer)
-    __shared__ T s_pivot;
-    const int tid = threadIdx.x;
-    const int r = tid >> 6, c = tid & 63;
-    const int pf = tid;  // prefetch lane
-    constexpr int PFN = CH_THREADS;
-    __shared__ int s_tk;
-    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
-        const int64_t i0 = I * TR;
-        const int64_t i = i0 + r;  // this thread's row
-        const int64_t jb = i0 - b > 0 ? i0 - b : 0;
-        const int64_t kend = i0 + TR < n ? i0 + TR : n;
-        T acc[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) acc[m] = A::zero();
-        int64_t seen = -1;  // last progress of tile-row I-1 this thread observed
-        // prefetch ring: every thread issues exactly three
-        // UNCONDITIONAL loads per column (clamped, always in-bounds addresses)
-        // so the compiler's s_waitcnt before a ring slot is used can count
-        // (a conditional load makes it fall back to vmcnt(0)): two column
-        // values L[kc+d][kc] and one "extra": A[i0+pf][kc] for pf < TR, the
-        // pivot L[kc][kc] for pf == TR, a dummy otherwise. Validity is decided
-        // when a slot is staged into LDS.
-        T pc0[CH_PF], pc1[CH_PF], px[CH_PF];
-        int pp[CH_PF];  // progress[I-1] as loaded CH_PF steps earlier
-#pragma unroll
-        for (int q = 0; q < CH_PF; ++q) { pc0[q] = A::zero(); pc1[q] = A::zero(); px[q] = A::zero(); pp[q] = -1; }
-        int* prev_progress = &progress[I > 0 ? I - 1 : 0];
-        // blocking poll (rare: the prefetched counter normally suffices)
-        auto wait_progress = [&](int64_t need) {
-            long long spins = 0;
-            if (trace && tid == 0 && seen < need) atomicAdd(&trace[3 * TRACE_TILES], 1ull);
-            while (seen < need) {
-                seen = __hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (seen >= need) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > SPIN_LIMIT ||
-                    ((spins & 1023) == 0 &&
-                     (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
-                    atomicOr(status, ST_TIMEOUT);
-                    seen = INT32_MAX;
-                    break;
-                }
-            }
-            if (trace && tid == 0 && spins) atomicAdd(&trace[3 * TRACE_TILES + 1], (unsigned long long)spins);
-        };
-        const int64_t last = n * ld - 1;  // clamp target
-        auto clampi = [&](int64_t x) { return x < 0 ? 0 : (x > last ? last : x); };
-        auto issue = [&](int q, int64_t kc) {
-            const int64_t base = kc * ld;
-            const int64_t d0 = 1 + pf, d1 = 1 + pf + PFN;
-            pc0[q] = ld_sc1(&CB[clampi(base + d0)]);
-            pc1[q] = ld_sc1(&CB[clampi(base + d1)]);
-            const int64_t xo = pf < TR ? base + (i0 + pf - kc) : (pf == TR ? base : base + d0);
-            px[q] = ld_sc1(&CB[clampi(xo)]);
-            pp[q] = __hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        auto stage_cols = [&](int q, int64_t kc) {
-            const int64_t d0 = 1 + pf, d1 = 1 + pf + PFN;
-            const int64_t dmax = (i0 - 1 - kc < b) ? i0 - 1 - kc : b;  // rows kc+1 .. i0-1 above us
-            if (d0 <= dmax) colL[d0] = pc0[q];
-            if (d1 <= dmax) colL[d1] = pc1[q];
-        };
-        auto stage_ap = [&](int q, int64_t kc) {
-            if (pf < TR) {
-                const int64_t ia = i0 + pf;
-                aval[kc & 1][pf] = (ia < n && ia >= kc && ia - kc <= b) ? px[q] : A::zero();
-            } else if (pf == TR) {
-                pval[kc & 1] = kc < i0 ? px[q] : A::zero();
-            }
-        };
-        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I] = wall_clock64();
-        // prologue: columns jb .. jb+CH_PF-1 must be final above us
-        if (I > 0) wait_progress(jb + CH_PF < i0 ? jb + CH_PF : i0);
-        __syncthreads();
-        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 1] = wall_clock64();
-#pragma unroll
-        for (int q = 0; q < CH_PF; ++q) issue(q, jb + q);
-        stage_ap(0, jb);
-        __syncthreads();
-        // The k loop is unrolled by CH_PF so every ring slot index is a
-        // compile-time constant (a register ring that is shifted instead
-        // would force a wait on every in-flight load), and the unrolled body
-        // runs unconditionally -- up to CH_PF-1 idle steps past kend, which
-        // do nothing -- so the compiler can count its s_waitcnt vmcnt(N).
-        for (int64_t k0 = jb; k0 < kend; k0 += CH_PF) {
-#pragma unroll
-            for (int q = 0; q < CH_PF; ++q) {
-                const int64_t k = k0 + q;
-                {
-                    const int64_t kk = k - jb;
-                    const int mk = (int)(kk >> 6), ck = (int)(kk & 63);
-                    // (b) finalise column k (diagonal first when row k is ours)
-                    T piv;
-                    if (k >= i0) {
-                        if (i == k && i < n && c == ck) {
-                            T sacc = A::zero();
-#pragma unroll
-                            for (int m = 0; m < M; ++m) if (m == mk) sacc = acc[m];
-                            const T l = pow_half(A::sub(aval[k & 1][r], sacc));
-                            if (!(l > A::zero()) || isinf(l)) atomicOr(status, ST_NOT_PD);
-                            s_pivot = l;
-                        }
-                        __syncthreads();
-                        piv = s_pivot;
-                    } else {
-                        piv = pval[k & 1];
-                    }
-                    if (c == ck) {
-                        T lik = A::zero();
-                        if (i < n && i >= k && i - k <= b) {
-                            if (i == k) {
-                                lik = piv;
-                            } else {
-                                T sacc = A::zero();
-#pragma unroll
-                                for (int m = 0; m < M; ++m) if (m == mk) sacc = acc[m];
-                                lik = A::mul(div_rn((T)1, piv), A::sub(aval[k & 1][r], sacc));
-                                colL[i - k] = lik;
-                            }
-                        }
-                        rowval[r] = lik;
-                    }
-                    // (c) prefetch waves: stage column k from ring slot q; make
-                    // sure column k + CH_PF is final above us before reloading q
-                    stage_cols(q, k);
-                    if (I > 0) {
-                        const int64_t need = (k + CH_PF + 1 < i0) ? k + CH_PF + 1 : i0;
-                        if (pp[q] > seen) seen = pp[q];
-                        if (seen < need) wait_progress(need);
-                    }
-                    __syncthreads();  // B: column k staged; rowval final; slot q free
-                    issue(q, k + CH_PF);
-                    stage_ap((q + 1) % CH_PF, k + 1);
-                    // (e) wave 0 stores column k of the tile-row; delayed publication
-                    if (tid < 64) {
-                        if (tid < TR) {
-                            const int64_t is = i0 + tid;
-                            if (is < n && is >= k && is - k <= b) st_sc1(&CB[k * ld + (is - k)], rowval[tid]);
-                        }
-                        if (k + 1 == kend) {
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            if (tid == 0)
-                                __hip_atomic_store(&progress[I], (int)kend, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        } else if (k + 1 < kend && (kk + 1) % CH_PUB == 0 && kk + 1 > CH_PUB) {
-                            // wave 0 issues 4 loads + 1 store per step: all but the
-                            // 5*CH_PUB youngest ops done => stores of columns <= k - CH_PUB done
-                            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * CH_PUB) : "memory");
-                            if (tid == 0)
-                                __hip_atomic_store(&progress[I], (int)(k + 1 - CH_PUB), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    }
-                    // (d) right-looking update of this thread's accumulators
-                    const T lk = rowval[r];
-                    if (lk != A::zero()) {
-                        const int dbase = (int)(jb - k) + c;
-                        const int di = (int)(i - k), bb = (int)b;
-#pragma unroll
-                        for (int m = 0; m < M; ++m) {
-                            const int d = dbase + 64 * m;
-                            if (d >= 1 && d <= bb && d <= di) acc[m] = A::add(acc[m], A::mul(lk, colL[d]));
-                        }
-                    }
-                    __syncthreads();  // colL / rowval / aval[k & 1] are reused at step k + 1
-                }
-            }
-        }
-        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 2] = wall_clock64();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// band_chol3: the same factorisation with one workgroup barrier per C3S
-// columns instead of two or three per column. 512 threads = 8 waves, one
-// workgroup per CU (2 waves per SIMD, up to 256 VGPRs each).
-//   * Wave w owns rows ia = i0 + 2w and ib = ia + 1 of tile-row I. Their
-//     accumulators for the columns left of the tile (j < i0) sit in M
-//     register slots per row, lane c holding j = jb + c + 64 m; the k loop
-//     runs window by window (64 columns per slot, one instantiation per
-//     window), so the slot of column k is a compile-time index. Per column
-//     k the wave forms L[i][k] = (1/L[k][k]) * (A[i][k] - acc) in every
-//     lane, takes lane (k - jb) & 63's value with v_readlane and adds
-//     L[i][k] * L[j][k] to every later slot, one LDS read of L[j][k] serving
-//     both rows. No other wave is involved: a column step has no barrier.
-//   * The accumulators of the tile's own columns (j in [i0, i0+16), lanes
-//     0..15) are kept apart and updated once per batch from the tile's own
-//     L values of the batch (an LDS history), in ascending k.
-//   * Column k of the rows above the tile and 1/L[k][k] (array R, written
-//     once per column by the tile-row that owns row k) are staged into LDS
-//     C3S columns at a time from a register ring loaded C3LA batches ahead:
-//     unconditional sc1 loads, so every s_waitcnt vmcnt is a count.
-//   * The 16x16 diagonal block is factored by wave 0 alone at the end of the
-//     tile-row (registers + LDS), which then publishes the tile-row's
-//     progress. During the sweep, progress is published per batch, one
-//     batch behind: every wave's stores drained by a counted wait, the
-//     barrier, then one lane's sc1 flag store (MI355X_MICROARCH.md "Valid
-//     forms", row 1).
-// Operation order per element is the reference's (sparse.rs:689-708), so
-// the result is bit-identical to band_chol and to the oracle.
-// ---------------------------------------------------------------------------
-constexpr int C3S = 4;  // columns per staging batch (one barrier per batch)
-
-// RW rows per wave: 16 / RW waves, 1024 / RW threads
-template <typename T, int M, int RW>
-__global__ __launch_bounds__(1024 / RW) void band_chol3(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
-                                                         T* __restrict__ R, int* __restrict__ progress,
-                                                         int* __restrict__ status, int* __restrict__ ticket,
-                                                         int64_t n_tiles, unsigned long long* __restrict__ trace) {
-    using A = Arith<T>;
-    constexpr int NT = 1024 / RW;           // threads
-    constexpr int SPAN = 64 * M;            // staged d = 1 .. SPAN of each column
-    constexpr int CSTR = 64 * (M + 1) + 8;  // staged column k: [64 + d] = CB[k * ld + d], d in [-63, SPAN]
-    constexpr int PFN = (C3S * SPAN + NT - 1) / NT;
-    __shared__ T colbuf[2][C3S][CSTR];
-    __shared__ T rbuf[2][C3S];
-    __shared__ T hist[2][C3S][TR];
-    __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
-    __shared__ T lcol[64];
-    const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
-    // staged element e = tid + NT q of a batch: column e / SPAN, d = e % SPAN + 1,
-    // at offset off[q] from the batch's first column (int: n * ld + pad < 2^31)
-    int off[PFN];
-#pragma unroll
-    for (int q = 0; q < PFN; ++q) {
-        const int e = tid + NT * q;
-        off[q] = e < C3S * SPAN ? (e / SPAN) * (int)ld + e % SPAN + 1 : 0;
-    }
-    __shared__ int s_tk;
-    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
-        const int i0 = (int)(I * TR);
-        const int jb = i0 - (int)b > 0 ? i0 - (int)b : 0;
-        const int nb = (i0 - jb + C3S - 1) / C3S;  // batches of the sweep
-        int* prev = &progress[I > 0 ? I - 1 : 0];
-        int seen = I > 0 ? -1 : INT32_MAX;
-        auto poll = [&](int need) {  // wave 0 only; blocking, bounded
-            long long spins = 0;
-            if (trace && c == 0 && seen < need) atomicAdd(&trace[3 * TRACE_TILES], 1ull);
-            while (seen < need) {
-                seen = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (seen >= need) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > SPIN_LIMIT ||
-                    ((spins & 1023) == 0 &&
-                     (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
-                    atomicOr(status, ST_TIMEOUT);
-                    seen = INT32_MAX;
-                    break;
-                }
-            }
-            if (trace && c == 0 && spins) atomicAdd(&trace[3 * TRACE_TILES + 1], (unsigned long long)spins);
-        };
-        auto batch_end = [&](int p) { return jb + C3S * (p + 1) < i0 ? jb + C3S * (p + 1) : i0; };
-        T acc[RW][M], aT[RW], accT[RW];
-#pragma unroll
-        for (int q = 0; q < RW; ++q) {
-            const int rr = RW * w + q;  // A[i0 + rr][i0 + c] for the diagonal block (read at the end)
-            const bool ok = c < TR && c <= rr && rr - c <= (int)b && i0 + rr < n;
-            aT[q] = ok ? CB[(int64_t)(i0 + c) * ld + (rr - c)] : A::zero();
-            accT[q] = A::zero();
-#pragma unroll
-            for (int m = 0; m < M; ++m) acc[q][m] = A::zero();
-        }
-        // one register batch in flight: loaded at boundary p - 1 for batch p + 1
-        T pf[PFN + 1];
-        auto issue = [&](int kb) {
-            const T* base = CB + (int64_t)kb * ld;
-#pragma unroll
-            for (int q = 0; q < PFN; ++q) pf[q] = ld_sc1(base + off[q]);
-            pf[PFN] = ld_sc1(&R[kb + (tid & (C3S - 1))]);
-        };
-        auto stage = [&](int buf) {
-#pragma unroll
-            for (int q = 0; q < PFN; ++q) {
-                const int e = tid + NT * q;
-                if (C3S * SPAN % NT == 0 || e < C3S * SPAN) colbuf[buf][e / SPAN][64 + e % SPAN + 1] = pf[q];
-            }
-            rbuf[buf][tid & (C3S - 1)] = pf[PFN];  // every thread (same values): no branch, no vmcnt(0)
-        };
-        int pv = -1;  // progress[I-1] as loaded at the last boundary
-        // diagnostic phase clocks (BSM_CHOL_TRACE): steps, boundary up to the
-        // poll, poll, barrier, after the barrier -- summed by thread 0
-        const bool tr0 = trace && tid == 0 && I < TRACE_TILES;
-        long long tph[5] = {0, 0, 0, 0, 0}, tlast = 0;
-        auto mark = [&](int ph) {
-            if (tr0) {
-                const long long t = clock64();
-                tph[ph] += t - tlast;
-                tlast = t;
-            }
-        };
-        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I] = wall_clock64();
-        if (tid < 64 && I > 0) poll(batch_end(1));
-        __syncthreads();
-        if (trace && tid == 0 && I < TRACE_TILES) trace[3 * I + 1] = wall_clock64();
-        issue(jb);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stage(0);
-        if (tid < 64) pv = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        issue(jb + C3S);
-        __syncthreads();
-        if (tr0) tlast = clock64();
-        // one instantiation per window m (64 columns = 8 batches): the slot index
-        // and the update range m..M-1 are compile-time
-        auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
-            for (int pw = 0; pw < 64 / C3S; ++pw) {
-                const int p = (64 / C3S) * m + pw;  // batch
-                if (p >= nb) return;
-                const int kb = jb + C3S * p, cur = p & 1;
-                // ---- C3S column steps, no barrier
-                for (int s = 0; s < C3S; ++s) {
-                    const int k = kb + s;
-                    if (k < i0) {
-                        const int ck = C3S * pw + s;
-                        // every LDS read of the step first (none depends on this step's L values)
-                        const T rk = rbuf[cur][s];
-                        const T* colk = &colbuf[cur][s][64 + (jb - k) + c];  // colk[64 mm] = L[jb + c + 64 mm][k]
-                        T lv[M];
-#pragma unroll
-                        for (int mm = m; mm < M; ++mm) lv[mm] = colk[64 * mm];
-                        T av[RW];
-#pragma unroll
-                        for (int q = 0; q < RW; ++q) {  // A[i0 + rr][k], staged at d = i0 + rr - k (not yet overwritten)
-                            const int d = i0 + RW * w + q - k;
-                            const T a = colbuf[cur][s][64 + (d < SPAN ? d : SPAN)];
-                            av[q] = d <= (int)b ? a : A::zero();
-                        }
-                        T x[RW];
-#pragma unroll
-                        for (int q = 0; q < RW; ++q) {
-                            x[q] = readlane_t(A::mul(rk, A::sub(av[q], acc[q][m])), ck);
-                            if (c == ck) hist[cur][s][RW * w + q] = x[q];
-                        }
-#pragma unroll
-                        for (int mm = m; mm < M; ++mm)
-#pragma unroll
-                            for (int q = 0; q < RW; ++q) acc[q][mm] = A::add(acc[q][mm], A::mul(x[q], lv[mm]));
-                    }
-                }
-                mark(0);
-                // ---- batch boundary
-                {  // store the batch's values: lane l -> row RW w + l / 32 (RW = 2), column kb + l % 8
-                    const int hs = c & (C3S - 1);
-                    const int rr = RW * w + (RW == 2 ? (c >> 5) : 0);
-                    const int i = i0 + rr, k = kb + hs;
-                    const T xv = hist[cur][hs][rr];
-                    const bool ok = i < n && k < i0 && i - k <= (int)b;
-                    st_sc1(ok ? &CB[(int64_t)k * ld + (i - k)] : &R[n + c], xv);
-                }
-                // everything but that store is done: the previous batch's stores,
-                // the next batch's columns, the last progress load
-                asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                stage(cur ^ 1);
-                mark(1);
-                if (tid < 64 && I > 0) {
-                    const int need = batch_end(p + 2);
-                    if (pv > seen) seen = pv;
-                    if (seen < need) poll(need);
-                }
-                mark(2);
-                __syncthreads();
-                mark(3);
-                if (tid == 0)  // columns < kb are final for this tile-row
-                    __hip_atomic_store(&progress[I], kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (c < TR) {  // tile-column accumulators, ascending k (reads first, then the chain)
-                    T hc[C3S], hr[C3S][RW];
-#pragma unroll
-                    for (int s = 0; s < C3S; ++s) {
-                        hc[s] = hist[cur][s][c];
-#pragma unroll
-                        for (int q = 0; q < RW; ++q) hr[s][q] = hist[cur][s][RW * w + q];
-                    }
-#pragma unroll
-                    for (int s = 0; s < C3S; ++s)
-                        if (kb + s < i0)
-#pragma unroll
-                            for (int q = 0; q < RW; ++q) accT[q] = A::add(accT[q], A::mul(hr[s][q], hc[s]));
-                }
-                if (tid < 64) pv = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                issue(kb + 2 * C3S);
-                mark(4);
-            }
-        };
-        [&]<int... ms>(std::integer_sequence<int, ms...>) __attribute__((always_inline)) {
-            (window(std::integral_constant<int, ms>{}), ...);
-        }(std::make_integer_sequence<int, M>{});
-        // ---- diagonal block: wave 0 factors the 16 x 16 block
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (c < TR) {
-#pragma unroll
-            for (int q = 0; q < RW; ++q) {
-                dacc[RW * w + q][c] = accT[q];
-                dA[RW * w + q][c] = aT[q];
-            }
-        }
-        __syncthreads();
-        if (tid < 64) {
-            // lane c owns the block elements (r, j) = ((c + 64 u) / 16, (c + 64 u) % 16), u < 4:
-            // q = their accumulators, av = their A values; column t at step t
-            T q[4], av[4];
-            int er[4], ej[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                er[u] = (c + 64 * u) >> 4;
-                ej[u] = (c + 64 * u) & 15;
-                const bool live = i0 + er[u] < n;
-                q[u] = live ? dacc[er[u]][ej[u]] : A::zero();
-                av[u] = live ? dA[er[u]][ej[u]] : (er[u] == ej[u] ? (T)1 : A::zero());
-            }
-#pragma unroll 1
-            for (int t = 0; t < TR; ++t) {
-                // the pivot: element (t, t) is owned by lane (16 t + t) & 63, slot (16 t + t) >> 6
-                const int pe = 17 * t;
-                T dd = A::zero();
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (u == (pe >> 6)) dd = A::sub(av[u], q[u]);
-                const T piv = readlane_t(pow_half(dd), pe & 63);
-                const T rt = div_rn((T)1, piv);
-                if (c == 0) {
-                    if (i0 + t < n && (!(piv > A::zero()) || isinf(piv))) atomicOr(status, ST_NOT_PD);
-                    if (i0 + t < n) st_sc1(&R[i0 + t], rt);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {  // column t: L[i0 + r][i0 + t], r >= t
-                    if (ej[u] == t && er[u] >= t) {
-                        const T x = er[u] == t ? piv : A::mul(rt, A::sub(av[u], q[u]));
-                        lcol[er[u]] = x;
-                        if (i0 + er[u] < n && er[u] - t <= b) st_sc1(&CB[(i0 + t) * ld + (er[u] - t)], x);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)  // acc[r][j] += L[r][t] * L[j][t] for t < j <= r
-                    if (ej[u] > t && er[u] >= ej[u]) q[u] = A::add(q[u], A::mul(lcol[er[u]], lcol[ej[u]]));
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0)
-                __hip_atomic_store(&progress[I], (int)(i0 + TR < n ? i0 + TR : n), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (tr0) {
-            trace[3 * I + 2] = wall_clock64();
-            for (int ph = 0; ph < 5; ++ph) atomicAdd(&trace[3 * TRACE_TILES + 2 + ph], (unsigned long long)tph[ph]);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// band_chol4: tile-event schedule. Row-block I = rows [16 I, 16 I + 16), one
-// 1024-thread workgroup per CU (wave w = row i0 + w); column
-// tile K = columns [16 K, 16 K + 16). Accumulators as in band_chol3 (lane c
-// of slot m holds column jb + c + 64 m, jb = 16 K0 aligned down), so tile K
-// sits in lanes 16 e .. 16 e + 15 of slot m with 16 (K - K0) = 64 m + 16 e.
-// Per off-diagonal tile K (ascending):
-//   T  (needs row-block K complete): stage the 16 x 16 diagonal tile of K and
-//      1/L[k][k]; each wave solves its row across the tile's 16 columns
-//      (x_t = R_t (A - acc_t), acc_{t'} += x_t L[t'][t] in-tile), stores them
-//      write-through and the workgroup publishes fprog[I] = K + 1 (tiles <= K
-//      final) -- the only work on the row-blocks' critical chain;
-//   U  (needs fprog[J] > K for the row-blocks J in (K, I) -- one vector poll):
-//      stage column tile K of the rows in between and add its 16 terms to
-//      every later accumulator, and
-//      to the diagonal-block accumulators from the other rows' x (LDS).
-// Then the 16 x 16 diagonal block (wave 0, diag_factor16) and fprog[I] = I+1.
-// Unlike band_chol3 (which advances column by column behind its predecessor
-// and pays a staging round + barrier per 4 columns on the chain), a
-// row-block's bulk updates run as soon as the tiles they need exist; only
-// T of the last tile + the diagonal block sit between two completions.
-// Operation order per element = the reference's (ascending k, no FMA).
-// ---------------------------------------------------------------------------
-constexpr int C4_TB = 16;
-constexpr int C4_NT = 1024;  // 16 waves, one row each
-
-__global__ __launch_bounds__(256) void band_chol4_init(int64_t n_tiles, int64_t b, int* __restrict__ fprog) {
+// fprog[J]: row-block J's progress (tiles final); tiles before the band are
+// structurally zero
+__global__ __launch_bounds__(256) void chol_prog_init(int64_t n_tiles, int64_t b, int* __restrict__ fprog) {
     const int64_t J = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (J >= n_tiles) return;
     const int64_t lo = C4_TB * J - b;
     fprog[J] = (int)((lo > 0 ? lo : 0) / C4_TB);  // tiles before the band: structurally zero
 }
 
-template <typename T, int M>
-__global__ __launch_bounds__(C4_NT) void band_chol4(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
-                                                    T* __restrict__ R, int* __restrict__ fprog,
-                                                    int* __restrict__ status, int* __restrict__ ticket,
-                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
-    using A = Arith<T>;
-    constexpr int CS = 64 + 64 * M;  // [64 zero pad][column tile K of rows k0+16 ...]
-    __shared__ T colK[C4_TB][CS];
-    __shared__ T dTl[C4_TB][64];          // [t][lane lb + t + u] = L[k0 + t + u][k0 + t], 1 <= u <= 15 - t; else 0
-    __shared__ T rT[C4_TB];               // 1 / L[k0 + t][k0 + t]
-    __shared__ T aK[C4_TB][C4_TB];        // aK[r][t] = A[i0 + r][k0 + t]
-    __shared__ T hist[C4_TB][C4_TB + 1];  // hist[t][r] = L[i0 + r][k0 + t]
-    __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
-    __shared__ T xl[16];
-    __shared__ long long tph[16];  // BSM_CHOL_TRACE phase clocks (thread 0)
-    const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
-    for (int q = tid; q < C4_TB * 64; q += C4_NT) colK[q >> 6][q & 63] = A::zero();
-    const int ib = (int)b;
-    auto poll_all = [&](int jlo, int jhi, int need) {  // wave 0: fprog[J] >= need for J in [jlo, jhi)
-        const int J = jlo + c;
-        bool ok = J >= jhi;
-        long long spins = 0;
-        while (true) {
-            if (!ok) ok = __hip_atomic_load(&fprog[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > SPIN_LIMIT ||
-                ((spins & 1023) == 0 &&
-                 (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_TIMEOUT))) {
-                if (c == 0) atomicOr(status, ST_TIMEOUT);
-                break;
-            }
-        }
-    };
-    __shared__ int s_tk;
-    for (int64_t I = next_ticket(ticket, &s_tk); I < n_tiles; I = next_ticket(ticket, &s_tk)) {
-        const int i0 = (int)(I * C4_TB);
-        const int K0 = (i0 - ib > 0 ? i0 - ib : 0) / C4_TB, jb = C4_TB * K0;
-        const bool live = i0 + w < n;
-        // diagnostic phase clocks (BSM_CHOL_TRACE), thread 0: [0..6) every off-diagonal tile but the
-        // last, [6..12) the last one (K = I - 1), [12..15) the diagonal block
-        long long tlast = 0;
-        const bool tr0 = trace && tid == 0;
-        if (tr0) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) tph[q] = 0;
-            tlast = clock64();
-        }
-        auto mark = [&](bool last, int ph) {  // ph: a constant
-            if (tr0) {
-                const long long t = clock64();
-                if (last) tph[6 + ph] += t - tlast;
-                else tph[ph] += t - tlast;
-                tlast = t;
-            }
-        };
-        T acc[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) acc[m] = A::zero();
-        T accT = A::zero();
-        const T aT = (c < C4_TB && c <= w && w - c <= ib && live) ? CB[(int64_t)(i0 + c) * ld + (w - c)] : A::zero();
-        auto window = [&]<int m>(std::integral_constant<int, m>) __attribute__((always_inline)) {
-#pragma unroll 1
-            for (int e = 0; e < 4; ++e) {
-                const int K = K0 + 4 * m + e;
-                if (K >= (int)I) return;
-                const int k0 = C4_TB * K, lb = 16 * e;
-                const bool lastK = K == (int)I - 1;
-                // ---------------- T: this row-block's tile K
-                if (w == 0) poll_all(K, K + 1, K + 1);
-                mark(lastK, 0);
-                __syncthreads();
-                {  // the diagonal tile of K, laid out per lane of the slot: one element per thread
-                    const int t = w, u = c - lb - t;
-                    T v = A::zero();
-                    if (u >= 1 && t + u <= 15 && u <= ib) v = ld_sc1(CB + (int64_t)(k0 + t) * ld + u);
-                    dTl[t][c] = v;
-                }
-                if (tid < 256) {
-                    const int rr = tid >> 4, t = tid & 15, d = i0 + rr - k0 - t;
-                    T v = A::zero();
-                    if (d <= ib && i0 + rr < n) v = CB[(int64_t)(k0 + t) * ld + d];
-                    aK[rr][t] = v;
-                } else if (tid < 256 + C4_TB) {
-                    rT[tid - 256] = ld_sc1(&R[k0 + tid - 256]);
-                }
-                __syncthreads();
-                mark(lastK, 1);
-                // lane t holds 1/L[k0+t][k0+t] and A[i][k0+t] (v_readlane), lane l its column's
-                // diagonal-tile values: nothing on the step chain waits for LDS
-                T myR = rT[c & 15], myA = aK[w][c & 15];
-                T xv = A::zero();
-#pragma unroll
-                for (int t = 0; t < C4_TB; ++t) {
-                    // keep the step's v_readlanes in the step (hoisted, they exhaust the SGPRs)
-                    asm volatile("" : "+v"(myR), "+v"(myA));
-                    const T dv = dTl[t][c];
-                    const T s = readlane_t(acc[m], lb + t);
-                    const T x = A::mul(readlane_t(myR, t), A::sub(readlane_t(myA, t), s));
-                    acc[m] = A::add(acc[m], A::mul(x, dv));
-                    if (c == t) xv = x;
-                }
-                if (c < C4_TB) {
-                    hist[c][w] = xv;
-                    const int d = i0 + w - k0 - c;
-                    if (d <= ib && live) st_sc1(&CB[(int64_t)(k0 + c) * ld + d], xv);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                mark(lastK, 2);
-                // publish F(I, K) at once: the row-blocks below wait on it in their U phase (a
-                // publication behind this row-block's own U wait would chain the hand-offs)
-                __syncthreads();
-                if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (lastK) {  // no rows in between: the diagonal-block sums of this tile
-                    mark(true, 4);
-                    if (c < C4_TB) {
-                        T hc[C4_TB];
-#pragma unroll
-                        for (int t = 0; t < C4_TB; ++t) hc[t] = hist[t][c];
-#pragma unroll
-                        for (int t = 0; t < C4_TB; ++t) accT = A::add(accT, A::mul(readlane_t(xv, t), hc[t]));
-                    }
-                    mark(true, 5);
-                    return;
-                }
-                // ---------------- U: column tile K of the rows between, once they have it
-                mark(lastK, 3);
-                if (w == 0) poll_all(K + 1, (int)I, K + 1);
-                __syncthreads();
-                const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
-                if (tid < cnt) {
-                    // element (t, row k0 + 16 + tid) at base + t (ld - 1); reads past the band
-                    // (d > b) stay inside the allocation (band_pad) and are replaced by 0
-                    const T* base = CB + (int64_t)k0 * ld + C4_TB + tid;
-                    T v[C4_TB];
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) v[t] = ld_sc1(base + (int64_t)t * (ld - 1));
-#pragma unroll
-                    for (int t = 0; t < C4_TB; ++t) colK[t][64 + tid] = C4_TB + tid - t <= ib ? v[t] : A::zero();
-                }
-                __syncthreads();
-                mark(lastK, 4);
-#pragma unroll 1
-                for (int t = 0; t < C4_TB; ++t) {
-                    const T x = hist[t][w];
-                    const T* col = &colK[t][64 + c - lb - C4_TB];  // col[64 (mm - m)]: column jb + c + 64 mm
-#pragma unroll
-                    for (int mm = m; mm < M; ++mm)
-                        if (jb + 64 * mm < i0) acc[mm] = A::add(acc[mm], A::mul(x, col[64 * (mm - m)]));
-                    if (c < C4_TB) accT = A::add(accT, A::mul(x, hist[t][c]));
-                }
-                mark(lastK, 5);
-            }
-        };
-        [&]<int... ms>(std::integer_sequence<int, ms...>) __attribute__((always_inline)) {
-            (window(std::integral_constant<int, ms>{}), ...);
-        }(std::make_integer_sequence<int, M>{});
-        // ---------------- the 16 x 16 diagonal block (wave 0)
-        if (c < TR) {
-            dacc[w][c] = accT;
-            dA[w][c] = aT;
-        }
-        __syncthreads();
-        mark(false, 12);
-        if (tid < 64) {
-            diag_factor16<T>(dacc, dA, xl, i0, n, b, ld, CB, R, status, c);
-            mark(false, 13);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (c == 0) __hip_atomic_store(&fprog[I], (int)I + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            mark(false, 14);
-            if (tr0) {
-#pragma unroll
-                for (int q = 0; q < 15; ++q) atomicAdd(&trace[q], (unsigned long long)tph[q]);
-                atomicAdd(&trace[15], 1ull);
-                atomicAdd(&trace[16], (unsigned long long)((int)I - K0 - 1));  // non-last tiles
-            }
-        }
-        __syncthreads();  // dacc / dA / LDS tiles reused by the next row-block
-    }
-}
-
 // ---------------------------------------------------------------------------
-// band_chol5 (round 4; the default for b <= 1009): band_chol4's tile events
-// with TWO rows per wave (8 waves, 512 threads), tuned for the completion
-// chain. Row-block I completes one diagonal block after row-block I - 1, so
-// its last tile's T, the diagonal sums and the 16 x 16 factor set the rate
-// (a row-block's other tiles run behind completed row-blocks, off the chain):
-//  * T reads row-block K's diagonal tile, 1/L and its own A values straight
-//    into registers (no LDS staging, one barrier), and the 16 chain steps take
-//    lane t's accumulator, 1/L and A by DPP row_newbcast (VALU only);
-//  * U (16 column steps over the staged column tile) is software-pipelined:
-//    step t + 1's LDS reads go out before step t's multiply-adds;
-//  * the last tile's stores drain behind the diagonal sums and the factor:
-//    its progress flag is raised by whichever wave arrives last at an LDS
-//    counter after its own drain (the factor wave from inside the factor);
-//  * the factor is diag_factor16x (pivot check folded into a flag, stores
-//    after the 16 steps: 8.1k instead of 9.1k cycles per block alone).
-// Per element the same operations in the same order as band_chol4 and the
-// reference (ascending k, no FMA, (1/L[k][k]) * (A - sum)): the same bits.
-// (RP = 4 -- 4 waves, 442 VGPRs -- gave wrong bits from row-block 14 of the
-// 500^2 case, deterministically, while RP = 2 and band_chol4 agree with the
-// oracle; it is not instantiated.)
+// band_chol5: the exact (reference-order) band Cholesky, b <= 1073.
+// Tile events. Row-block I = rows [16 I, 16 I + 16) is one workgroup of
+// 16 / RP waves (RP rows per wave; RP = 2 is instantiated), taken by ticket
+// in ascending order. Column tile K = columns [16 K, 16 K + 16). Row i's
+// accumulators for the columns left of its row-block sit in M register
+// slots (lane c of slot m: column jb + c + 64 m, jb = 16 K0 the band start
+// aligned down), so tile K is lanes 16 e .. 16 e + 15 of slot m, 16 (K - K0)
+// = 64 m + 16 e. Per off-diagonal tile K, in ascending order:
+//   T (needs row-block K complete, fprog[K] > K): the rows' x across the
+//     tile's 16 columns, x_t = (1/L[t][t]) (A - acc_t), acc_t' += x_t L[t'][t]:
+//     row-block K's diagonal tile, 1/L and the rows' own A values go straight
+//     into registers and the 16 chain steps take lane t's values by DPP
+//     row_newbcast (VALU only); write-through stores, drain, barrier,
+//     fprog[I] = K + 1;
+//   U (needs fprog[J] > K for the row-blocks J in (K, I), one vector poll):
+//     stage column tile K of those rows in LDS and add its 16 terms to every
+//     later accumulator (software-pipelined: step t + 1's LDS reads before
+//     step t's multiply-adds), and to the diagonal-block sums. Look-ahead: the
+//     slot holding tile K + 1 right after the staging, then T(K + 1), then the
+//     other slots (per accumulator the tiles still come in ascending order).
+// Then the 16 x 16 diagonal block (wave 0, diag_factor16x) while the other
+// waves store the last tile's L from LDS; completion (fprog[I] = I + 1) is
+// raised by the last wave to arrive after its own drain.
+// Per element the reference's operations in its order (ascending k, no FMA,
+// (1/L[k][k]) * (A - sum), sparse.rs:689-708): bit-identical to the oracle.
+// Measured variants (each dropped, DESIGN.md §4.5b'): four rows per wave,
+// the last tile stored before the factor, late T publication, per-wave polls,
+// split staging of U, two staging rows per thread.
 // ---------------------------------------------------------------------------
 template <typename T, int M, int RP>  // RP rows per wave: 16 / RP waves
 __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
@@ -1053,13 +327,6 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     __shared__ T dacc[TR][TR + 1], dA[TR][TR + 1];
     __shared__ T xl[16];
     __shared__ long long tph[16];
-#ifdef BSM_C5_EARLY_LAST
-    // A/B: the last tile's band stores and flag right after its T chain (drain
-    // + barrier + flag, as for the other tiles), instead of behind the factor
-    constexpr bool EARLY_LAST = true;
-#else
-    constexpr bool EARLY_LAST = false;
-#endif
     __shared__ int s_arr;  // waves past the last tile's stores (after the windows)
     if (threadIdx.x == 0) s_arr = 0;
     const int tid = threadIdx.x, w = tid >> 6, c = tid & 63;
@@ -1146,10 +413,9 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 for (int t = 0; t < C4_TB; ++t) colK[t][64 + rr] = C4_TB + rr - t <= ib ? v[t] : A::zero();
             }
         };
-        auto no_hook = []() {};
-        auto u_run = [&]<int LO, int HI, bool WT, typename Hook = decltype(no_hook)>(
-                         std::integral_constant<int, LO>, std::integral_constant<int, HI>, std::bool_constant<WT>,
-                         int mK, int lbK, T (*hs)[C4_TB + 1], Hook hook = {}) __attribute__((always_inline)) {
+        auto u_run = [&]<int LO, int HI, bool WT>(std::integral_constant<int, LO>, std::integral_constant<int, HI>,
+                                                  std::bool_constant<WT>, int mK, int lbK,
+                                                  T (*hs)[C4_TB + 1]) __attribute__((always_inline)) {
             if constexpr (LO < HI) {
                 struct UB {
                     T cv[HI - LO], x[RP], hv;
@@ -1187,7 +453,6 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     if (t + 2 < C4_TB) u_load(t + 2, ua);
                     __builtin_amdgcn_sched_barrier(0);
                     u_add(ubb);
-                    if (t == 4) hook();  // (band_chol5's late flag: the stores before have drained)
                 }
             }
         };
@@ -1214,14 +479,9 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                 // registers (no LDS staging, no second barrier): lane c takes
                 // L[k0 + t + u][k0 + t], u = c - lb - t, for every t
                 T dvr[C4_TB], myR;
-#ifdef BSM_C5_WAVEPOLL
-                poll_all(K, K + 1, K + 1);  // every wave for itself: no barrier
-                mark(lastK, 0);
-#else
                 if (w == 0) poll_all(K, K + 1, K + 1);
                 mark(lastK, 0);
                 __syncthreads();
-#endif
                 auto& hist = hist2[K & 1];
 #pragma unroll
                 for (int t = 0; t < C4_TB; ++t) {
@@ -1264,16 +524,13 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                         const int rw = r0 + q;
                         hist[cl][rw] = xv[q];
                         const int d = i0 + rw - k0 - cl;
-                        if (!(lastK && !EARLY_LAST) && d <= ib && i0 + rw < n)
+                        if (!lastK && d <= ib && i0 + rw < n)
                             st_sc1(&CB[(int64_t)(k0 + cl) * ld + d], xv[q]);
                     }
                 }
                 if (lastK) {  // no rows in between: the diagonal-block sums of this tile
                     mark(true, 2);
-                    if constexpr (EARLY_LAST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
-                    if (EARLY_LAST && tid == 0)
-                        __hip_atomic_store(&fprog[I], (int)I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     mark(true, 4);
                     // the rows' own x come from hist (an LDS broadcast), NOT by
                     // v_readlane of xv from lane lb + t: inside this lane-divergent
@@ -1295,69 +552,26 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
                     mark(true, 5);
                     return;
                 }
-#ifdef BSM_C5_LATEPUB
-                // T(K)'s flag without a drain or a barrier in this row-block's
-                // path: each wave waits for its own stores a few steps into the
-                // rest of U(K - 1) (they have drained by then) and arrives at the
-                // LDS counter; the last to arrive raises fprog[I] = K + 1
-                mark(false, 2);
-                bool arrived = false;
-                auto arrive_t = [&]() __attribute__((always_inline)) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (c == 0 && atomicAdd(&s_arr, 1) == C5_NT / 64 - 1) {
-                        s_arr = 0;
-                        __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    arrived = true;
-                };
-#else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 mark(false, 2);
                 __syncthreads();
                 if (tid == 0) __hip_atomic_store(&fprog[I], K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                auto arrive_t = []() {};
-#endif
                 // ---------------- the rest of U(K - 1): the slots after tile K's,
                 // which T(K) did not need (look-ahead: see u_run below)
                 mark(false, 3);
                 if (K > K0) {
-#ifdef BSM_C5_SPLITSTAGE
-                    // its column tile's rows past the first 64 (row-blocks K + 4
-                    // on, whose T(K - 1) the first part did not wait for)
-                    const int kp = k0 - C4_TB, cntp = i0 - kp - C4_TB;
-                    if (cntp > 64) {
-                        if (w == 0) poll_all(K + 4, (int)I, K);
-                        __syncthreads();
-                        stage_rows(kp, 64, cntp);
-                        __syncthreads();
-                    }
-#endif
                     if (e) u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
-                                 std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1], arrive_t);
+                                 std::false_type{}, m, lb - C4_TB, hist2[(K - 1) & 1]);
                     else if constexpr (m >= 1)
                         u_run(std::integral_constant<int, m + 1>{}, std::integral_constant<int, M>{},
-                              std::false_type{}, m - 1, 48, hist2[(K - 1) & 1], arrive_t);
+                              std::false_type{}, m - 1, 48, hist2[(K - 1) & 1]);
                 }
-#ifdef BSM_C5_LATEPUB
-                if (!arrived) arrive_t();
-#endif
-#ifdef BSM_C5_PROBE_REST  // sensitivity probe (A/B builds only): ~8k cycles more per non-last tile
-                __builtin_amdgcn_s_sleep(127);
-#endif
                 mark(false, 5);
                 // ---------------- U(K): column tile K of the rows between, once they have it
                 const int cnt = i0 - k0 - C4_TB;  // rows k0 + 16 .. i0 - 1
-#ifdef BSM_C5_SPLITSTAGE
-                // only the rows the next slot reads (row-blocks K + 1 .. K + 4);
-                // the others are polled and staged before the rest of U(K)
-                if (w == 0) poll_all(K + 1, (K + 5 < (int)I ? K + 5 : (int)I), K + 1);
-                __syncthreads();
-                stage_rows(k0, 0, cnt < 64 ? cnt : 64);
-#else
                 if (w == 0) poll_all(K + 1, (int)I, K + 1);  // (K + 1 <= I - 1)
                 __syncthreads();
                 stage_rows(k0, 0, cnt);
-#endif
                 __syncthreads();
                 mark(false, 4);
                 // now only the slot holding tile K + 1 (and the diagonal-block
@@ -1396,12 +610,9 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         // still factoring. Atomic max: the two values may land in either order.
         constexpr int C5_NSW = C5_NT / 64 - 1;  // store waves
         constexpr int C5_W0 = 0x100;
-        const bool store_waves = !EARLY_LAST && K0 < (int)I;
+        const bool store_waves = K0 < (int)I;
         if (tid < 64) {
             diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
-#ifdef BSM_C5_PROBE_CHAIN  // sensitivity probe (A/B builds only): ~8k cycles more on the completion chain
-            __builtin_amdgcn_s_sleep(127);
-#endif
             mark(false, 13);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (c == 0) {
@@ -1444,79 +655,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
     }
 }
 
-// ---------------------------------------------------------------------------
-// forward substitution on the band (lib.rs:28-46): y_i = (b_i - sum_{j<i}
-// L_ij y_j) / L_ii, sum in ascending j. One workgroup per RHS column; blocks
-// of 256 rows: the "far" terms (j < block start) are summed first, one thread
-// per row (loads batched ahead of the dependent adds), then the in-block
-// terms column by column with the band values prefetched FW_PF steps ahead
-// and one barrier per step (double-buffered y). y lives in an LDS ring.
-// ---------------------------------------------------------------------------
-constexpr int FW_BLOCK = 256;
-constexpr int FW_RING = 2048;  // >= b + FW_BLOCK
-constexpr int FW_PF = 16;
-
-template <typename T>
-__global__ __launch_bounds__(FW_BLOCK) void band_forward(int64_t n, int64_t b, int64_t ld,
-                                                         const T* __restrict__ CB, const T* __restrict__ B,
-                                                         T* __restrict__ Y) {
-    using A = Arith<T>;
-    __shared__ T ring[FW_RING];
-    __shared__ T s_y[2];
-    const int t = threadIdx.x;
-    const T* bc = B + (int64_t)blockIdx.x * n;
-    T* yc = Y + (int64_t)blockIdx.x * n;
-    for (int64_t i0 = 0; i0 < n; i0 += FW_BLOCK) {
-        const int64_t i = i0 + t;
-        const bool valid = i < n;
-        const T bi = valid ? bc[i] : A::zero();
-        const T lii = valid ? CB[i * ld] : A::zero();
-        T s = A::zero();
-        const int64_t j0 = (i - b > 0) ? i - b : 0;
-        if (valid) {
-            int64_t j = j0;
-            for (; j + 16 <= i0; j += 16) {
-                T lv[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) lv[u] = CB[(j + u) * ld + (i - j - u)];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) s = A::add(s, A::mul(lv[u], ring[(j + u) & (FW_RING - 1)]));
-            }
-            for (; j < i0; ++j) s = A::add(s, A::mul(CB[j * ld + (i - j)], ring[j & (FW_RING - 1)]));
-        }
-        const int64_t nb = (n - i0 < FW_BLOCK) ? n - i0 : FW_BLOCK;
-        // near-part band values L[i][i0 + tt] for tt = 0.. (prefetch ring of
-        // unconditional loads from clamped addresses; validity checked at use)
-        const int64_t last = n * ld - 1;
-        auto lnear = [&](int64_t tt) -> T {
-            const int64_t j = i0 + tt;
-            int64_t a = j * ld + (i - j);
-            a = a < 0 ? 0 : (a > last ? last : a);
-            return CB[a];
-        };
-        auto near_ok = [&](int64_t tt) { const int64_t j = i0 + tt; return valid && i > j && i - j <= b; };
-        T pre[FW_PF];
-#pragma unroll
-        for (int q = 0; q < FW_PF; ++q) pre[q] = lnear(q);
-        for (int64_t tt0 = 0; tt0 < nb; tt0 += FW_PF) {
-#pragma unroll
-            for (int q = 0; q < FW_PF; ++q) {
-                const int64_t tt = tt0 + q;  // runs past nb: idle steps
-                if (t == tt && valid) {
-                    const T y = div_rn(A::sub(bi, s), lii);
-                    ring[i & (FW_RING - 1)] = y;
-                    s_y[tt & 1] = y;
-                    yc[i] = y;
-                }
-                __syncthreads();
-                const T lij = pre[q];
-                pre[q] = lnear(tt + FW_PF);
-                if (tt < nb && t > tt && near_ok(tt)) s = A::add(s, A::mul(lij, s_y[tt & 1]));
-            }
-        }
-        __syncthreads();
-    }
-}
+constexpr int FW_BLOCK = 256;  // csr_forward's rows per block
 
 // ---------------------------------------------------------------------------
 // band_forward2: the forward solve with one 64-row block per wave and no
@@ -1803,152 +942,16 @@ __global__ __launch_bounds__(64 * NW) void band_forward2(int64_t n, int64_t b, i
 // backward substitution on the band (lib.rs:49-65) with L* = L^T: x_i =
 // (y_i - sum_{j>i} L_ji x_j) / L_ii, sum in ascending j. Ascending order makes
 // each row's sum START with the newest x, so the solve is one serial chain of
-// N*b dependent adds. Two wavefronts: wave 1 forms row i-1's products for
-// j >= i+1 (and stages L_ii, L_{i,i-1}... inputs) while lane 0 of wave 0 runs
-// row i's chain; one barrier per row.
-// ---------------------------------------------------------------------------
-constexpr int BW_RING = 2048;
-
-template <typename T>
-__global__ __launch_bounds__(128) void band_backward(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
-                                                     const T* __restrict__ Yin, T* __restrict__ X) {
-    using A = Arith<T>;
-    __shared__ T ring[BW_RING];
-    __shared__ T prod[2][BW_RING];  // prod[r & 1][d] = L[r+d][r] * x[r+d], d >= 2
-    __shared__ T meta[2][3];        // {L[r][r], L[r+1][r], y[r]} for row r (by r & 1)
-    const int tid = threadIdx.x, lane = tid & 63;
-    const bool producer = tid >= 64;
-    const T* yc = Yin + (int64_t)blockIdx.x * n;
-    T* xc = X + (int64_t)blockIdx.x * n;
-    // producer work for row r: products d >= 2 and the row's scalars
-    auto produce = [&](int64_t r) {
-        if (r < 0) return;
-        const int64_t dmax = (n - 1 - r < b) ? n - 1 - r : b;
-        const T* col = CB + r * ld;
-        for (int64_t d = 2 + lane; d <= dmax; d += 64)
-            prod[r & 1][d] = A::mul(col[d], ring[(r + d) & (BW_RING - 1)]);
-        if (lane == 0) {
-            meta[r & 1][0] = col[0];
-            meta[r & 1][1] = dmax >= 1 ? col[1] : A::zero();
-            meta[r & 1][2] = yc[r];
-        }
-    };
-    if (producer) produce(n - 1);
-    __syncthreads();
-    T x_next = A::zero();  // wave 0 lane 0: x[i + 1]
-    for (int64_t i = n - 1; i >= 0; --i) {
-        if (producer) {
-            produce(i - 1);  // needs x[i+1..]: final before this iteration
-        } else if (lane == 0) {
-            const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
-            T s = A::zero();
-            if (dmax >= 1) s = A::add(s, A::mul(meta[i & 1][1], x_next));
-            const T* p = prod[i & 1];
-            int64_t d = 2;
-            for (; d + 8 <= dmax + 1; d += 8) {
-                T v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = p[d + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) s = A::add(s, v[u]);
-            }
-            for (; d <= dmax; ++d) s = A::add(s, p[d]);
-            const T x = div_rn(A::sub(meta[i & 1][2], s), meta[i & 1][0]);
-            ring[i & (BW_RING - 1)] = x;
-            xc[i] = x;
-            x_next = x;
-        }
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// band_backward_hop: the same solve with the chain kept in registers. One
-// wavefront per RHS column. Row i's terms m = 1..dmax are split into 64
-// segments of SEG consecutive terms; lane l holds the products of segment l
-// in registers, and the running sum walks the lanes: lane l adds its SEG
-// products in order, then the sum moves to lane l+1 through an SGPR
-// (v_readlane). A dependent f64 add costs 8 cycles on gfx950, the same add
-// fed from LDS 13-19 (scripts/micro/*chain*), so the chain pays ~8 cycles
-// per term plus one lane hop per SEG terms. Per row, before the chain:
-// products from the x ring in LDS and the L column prefetched two rows
-// ahead. Padding terms are +0: the sum starts at +0 and can never become
-// -0, so adding +0 leaves it unchanged (bit-exact).
-// ---------------------------------------------------------------------------
-template <typename T, int SEG>
-__global__ __launch_bounds__(64) void band_backward_hop(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
-                                                        const T* __restrict__ Yin, T* __restrict__ X) {
-    using A = Arith<T>;
-    __shared__ T xr[BH_RING];
-    const int lane = threadIdx.x;
-    const T* yc = Yin + (int64_t)blockIdx.x * n;
-    T* xc = X + (int64_t)blockIdx.x * n;
-    const int m0 = SEG * lane + 1;  // first term of this lane's segment
-    // L[i+m][i] = CB[i*ld + m] for this lane's m, rows prefetched two ahead;
-    // CB is padded by BAND_PAD zeros, so row n-1's reads stay in bounds
-    T lvA[SEG], lvB[SEG];
-    auto load_row = [&](T (&lv)[SEG], int64_t r) {
-        const T* src = CB + (r < 0 ? 0 : r) * ld + m0;
-#pragma unroll
-        for (int u = 0; u < SEG; ++u) lv[u] = src[u];
-    };
-    // y_i and L_ii of a block of 64 rows, one per lane (read with v_readlane)
-    T yblk = A::zero(), dblk = A::zero();
-    int64_t blk = -1;
-    auto do_row = [&](const T (&lv)[SEG], int64_t i) {
-        if ((i >> 6) != blk) {
-            blk = i >> 6;
-            const int64_t r = (blk << 6) + lane < n ? (blk << 6) + lane : n - 1;
-            yblk = yc[r];
-            dblk = CB[r * ld];
-        }
-        const int64_t dmax = (n - 1 - i < b) ? n - 1 - i : b;
-        T p[SEG];
-#pragma unroll
-        for (int u = 0; u < SEG; ++u) {  // unconditional ring reads (always in range), then select
-            const int64_t m = m0 + u;
-            const T xv = xr[(i + m) & (BH_RING - 1)];
-            const T pr = A::mul(lv[u], xv);
-            p[u] = m <= dmax ? pr : A::zero();
-        }
-        const int nseg = (int)((dmax + SEG - 1) / SEG);
-        T sv = A::zero();  // running sum, wave-uniform between segments
-        for (int l = 0; l < nseg; ++l) {
-            T sl = sv;
-#pragma unroll
-            for (int u = 0; u < SEG; ++u) sl = A::add(sl, p[u]);
-            sv = readlane_t(sl, l);
-        }
-        const int li = (int)(i & 63);
-        const T x = div_rn(A::sub(readlane_t(yblk, li), sv), readlane_t(dblk, li));
-        if (lane == 0) {
-            xr[i & (BH_RING - 1)] = x;
-            xc[i] = x;
-        }
-    };
-    int64_t i = n - 1;
-    load_row(lvA, i);
-    load_row(lvB, i - 1);
-    for (; i >= 1; i -= 2) {
-        do_row(lvA, i);
-        load_row(lvA, i - 2);
-        do_row(lvB, i - 1);
-        load_row(lvB, i - 3);
-    }
-    if (i == 0) do_row(lvA, 0);
-}
-
-// ---------------------------------------------------------------------------
-// band_backward_reg: band_backward_hop with the lane walk unrolled and x held
-// in registers. On gfx950 one wave issues about one instruction per 4 cycles
-// and a dependent v_add_f64 every ~4.5 (scripts/micro/issue_cost.hip), so a
-// row costs ~4.5 cycles per chain add plus ~4 per other instruction; the
-// runtime loop over lanes of band_backward_hop also paid a taken branch per
-// hop (153 cycles per 16-add hop against 85 unrolled, hop_latency.hip). So:
+// N*b dependent adds: band_backward_reg, one wave per RHS column, lane l
+// holding the products of terms SEG*l+1 .. SEG*l+SEG of the row. On gfx950
+// one wave issues about one instruction per 4 cycles and a dependent
+// v_add_f64 every ~4.5 (scripts/micro/issue_cost.hip), so a row costs ~4.5
+// cycles per chain add plus ~4 per other instruction; a runtime loop over
+// lanes also paid a taken branch per hop (153 cycles per 16-add hop against
+// 85 unrolled, hop_latency.hip). So:
 //  * the NL hops are unrolled (straight-line code per row pair). The running
 //    sum moves from lane l to lane l+1 by DPP wave_shr:1 (every lane adds its
-//    own products; lane l+1 then takes lane l's sum), or by v_readlane
-//    (DPP = false);
+//    own products; lane l+1 then takes lane l's sum);
 //  * lane l keeps x[i+m] for its segment m = SEG*l+1 .. SEG*l+SEG in a
 //    register window; moving to row i-1 shifts every window by one: lane l
 //    takes lane l-1's last value through DPP and lane 0 takes the new x_i
@@ -1970,26 +973,18 @@ __device__ __forceinline__ float shr1_t(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, false));
 }
 
-template <typename T, int SEG, int NL, bool DPP, int... L>
+template <typename T, int SEG, int NL, int... L>
 __device__ __forceinline__ T lane_walk(const T (&p)[SEG], std::integer_sequence<int, L...>) {
     using A = Arith<T>;
     T sv = A::zero();
     auto hop = [&](auto lc) __attribute__((always_inline)) {
         constexpr int l = decltype(lc)::value;
-        if constexpr (DPP) {
 #pragma unroll
-            for (int u = 0; u < SEG; ++u) sv = A::add(sv, p[u]);
-            if constexpr (l + 1 < NL) sv = shr1_t(sv);
-        } else {
-            T sl = sv;
-#pragma unroll
-            for (int u = 0; u < SEG; ++u) sl = A::add(sl, p[u]);
-            sv = readlane_t(sl, l);
-        }
+        for (int u = 0; u < SEG; ++u) sv = A::add(sv, p[u]);
+        if constexpr (l + 1 < NL) sv = shr1_t(sv);
     };
     (hop(std::integral_constant<int, L>{}), ...);
-    if constexpr (DPP) return readlane_t(sv, NL - 1);
-    return sv;
+    return readlane_t(sv, NL - 1);
 }
 
 // (SEG, NL) of band_backward_reg for bandwidth b: NL lanes of SEG terms,
@@ -2018,7 +1013,7 @@ inline int64_t band_walk_terms(int64_t b) {
     return (int64_t)c.seg * c.nl;
 }
 
-template <typename T, int SEG, int NL, bool DPP>
+template <typename T, int SEG, int NL>
 __global__ __launch_bounds__(64) void band_backward_reg(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
                                                         const T* __restrict__ Yin, T* __restrict__ X) {
     using A = Arith<T>;
@@ -2053,7 +1048,7 @@ __global__ __launch_bounds__(64) void band_backward_reg(int64_t n, int64_t b, in
 #pragma unroll
             for (int u = 0; u < SEG; ++u) lv[u] = A::mul(lv[u], xw[u]);
         }
-        const T sv = lane_walk<T, SEG, NL, DPP>(lv, std::make_integer_sequence<int, NL>{});
+        const T sv = lane_walk<T, SEG, NL>(lv, std::make_integer_sequence<int, NL>{});
         const T x = div_rn(A::sub(y, sv), d);
         xc[i] = x;  // every lane, same address and value
         const T t = shr1_t(xw[SEG - 1]);
@@ -2450,20 +1445,12 @@ constexpr int TLD = 65;
 
 // LDS pointers that keep their address space across a call
 template <typename T> using lds_t = __attribute__((address_space(3))) T;
+// the f64 MFMA 16x16x4 accumulator
+typedef double bsm_d4 __attribute__((ext_vector_type(4)));
 
-// 1/sqrt(x): the hardware estimate and two Newton steps (error squares per
-// step): a short dependent chain for the blocked factor's pivots
-__device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const double h = __fma_rn(-x * y, y, 1.0);
-        y = __fma_rn(0.5 * y, h, y);
-    }
-    return y;
-}
-// one Newton step (the panel factor's pivots; BSM_BLK_PANELS=4 keeps two for A/B):
-// the estimate's error squared once
+// 1/sqrt(x): the hardware estimate and one Newton step (its error squared
+// once): a short dependent chain for the blocked factor's pivots (two steps:
+// 317 against 311 ms at C5, x error 8.8e-11 against 9.7e-11)
 __device__ __forceinline__ double rsqrt_nr1(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     const double h = __fma_rn(-x * y, y, 1.0);
@@ -2476,287 +1463,8 @@ __device__ __forceinline__ float rsqrt_nr(float x) {
 }
 __device__ __forceinline__ float rsqrt_nr1(float x) { return rsqrt_nr(x); }
 
-// Factor the 64 x 64 tile S (P[r * TLD + c], lower part) in one wave, lane r =
-// row r: right-looking, column s broadcast through LDS (colb). Out of line: in
-// the ticket loop its 64 unrolled steps would share the register budget with
-// everything the compiler hoists there. P receives L (zero upper part), rd the
-// reciprocal pivots.
-template <typename T, int N = 64>
-__device__ __forceinline__ void blk_diag_factor(lds_t<T>* P, lds_t<T>* colb, lds_t<T>* rd, int* status, int ln) {
-    T a[N];
-#pragma unroll
-    for (int c = 0; c < N; ++c) a[c] = P[ln * TLD + c];  // lanes >= N: rows below, never written back
-    bool pd = true;
-    // one instantiation per column s: a[] is only ever indexed by constants
-    auto step = [&]<int s>(std::integral_constant<int, s>) __attribute__((always_inline)) {
-        const T dd = readlane_t(a[s], s);
-        pd = pd & (dd > (T)0) & (dd < (T)INFINITY);
-        const T rp = rsqrt_nr(dd);
-        // every lane the same formula (no per-lane masks): lane s gets dd / sqrt(dd), the
-        // pivot; lanes above s form upper-triangle values that are never read and zeroed below
-        const T l = a[s] * rp;
-        a[s] = l;
-        rd[s] = rp;  // uniform value, every lane
-        if constexpr (s + 1 < N) {
-            // the next pivot's column first, by v_readlane: the chain from pivot to
-            // pivot has no LDS round trip; the later columns take the LDS broadcast
-            a[s + 1] = fma_t(-l, readlane_t(l, s + 1), a[s + 1]);
-            colb[ln] = l;
-#pragma unroll
-            for (int c = s + 2; c < N; ++c) {
-                if ((c & 31) == 0) asm volatile("" ::: "memory");  // at most 32 broadcast values in flight
-                a[c] = fma_t(-l, colb[c], a[c]);
-            }
-            asm volatile("" ::: "memory");
-        }
-    };
-    [&]<int... ss>(std::integer_sequence<int, ss...>) __attribute__((always_inline)) {
-        (step(std::integral_constant<int, ss>{}), ...);
-    }(std::make_integer_sequence<int, N>{});
-    if (ln == 0 && !pd) atomicOr(status, ST_NOT_PD);
-    if (ln < N) {
-#pragma unroll
-        for (int c = 0; c < N; ++c) P[ln * TLD + c] = c <= ln ? a[c] : (T)0;
-    }
-}
-
-// Q[c * TLD + r] = Linv[r][c] for the N x N L in P (one wave, lane c < N forms
-// column c of the inverse, rows ascending; the dot products by four chains,
-// their LDS reads 16 at a time ahead of the FMAs)
-template <typename T, int N = 64>
-__device__ __forceinline__ void blk_diag_inverse(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* rd, int ln) {
-    asm volatile("" : "+v"(ln));  // opaque: keep the per-row masks out of the ticket loop
-    T x[N];
-    auto row = [&]<int r>(std::integral_constant<int, r>) __attribute__((always_inline)) {
-        T sa[4] = {(T)0, (T)0, (T)0, (T)0};
-        auto blk16 = [&]<int q0>(std::integral_constant<int, q0>) __attribute__((always_inline)) {
-            if constexpr (q0 < r) {
-                constexpr int m = r - q0 < 16 ? r - q0 : 16;
-                T hv[16];
-                [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
-                    ((hv[is] = ((volatile const lds_t<T>*)P)[r * TLD + q0 + is]), ...);  // volatile: not hoisted
-                }(std::make_integer_sequence<int, m>{});
-                __builtin_amdgcn_sched_barrier(0);
-                [&]<int... is>(std::integer_sequence<int, is...>) __attribute__((always_inline)) {
-                    ((sa[(q0 + is) & 3] = fma_t(hv[is], x[q0 + is], sa[(q0 + is) & 3])), ...);
-                }(std::make_integer_sequence<int, m>{});
-            }
-        };
-        [&]<int... bs>(std::integer_sequence<int, bs...>) __attribute__((always_inline)) {
-            (blk16(std::integral_constant<int, 16 * bs>{}), ...);
-        }(std::make_integer_sequence<int, (N + 15) / 16>{});
-        x[r] = ((r == ln ? (T)1 : (T)0) - ((sa[0] + sa[1]) + (sa[2] + sa[3]))) *
-               ((volatile const lds_t<T>*)rd)[r];
-        // pin row r: its FMAs (pure, free to float in the DAG) complete before
-        // row r + 1's (volatile) reads, so at most 16 reads are live at once
-        asm volatile("" : "+v"(x[r]));
-    };
-    [&]<int... rs>(std::integer_sequence<int, rs...>) __attribute__((always_inline)) {
-        (row(std::integral_constant<int, rs>{}), ...);
-    }(std::make_integer_sequence<int, N>{});
-    if (ln < N) {
-#pragma unroll
-        for (int r = 0; r < N; ++r) Q[ln * TLD + r] = x[r];
-    }
-}
-
-// Factor AND invert the 64 x 64 tile S (P[r * TLD + c], lower part) as 2 x 2
-// blocks of 32 (the one-wave steps cost ~N^2 per pivot, so two 32-column
-// factors and inverses are a quarter of the 64-column ones):
-//   L11 = chol(S11), Linv11 (wave 0);  L21 = S21 Linv11^T;
-//   S22 -= L21 L21^T;  L22 = chol(S22), Linv22 (wave 0);
-//   Linv21 = -Linv22 (L21 Linv11)  (all waves; T = L21 Linv11 in Tm).
-// Out: P = L (zero upper part), Q[c * TLD + r] = Linv[r][c] (zero upper
-// part), rd = 1 / L[r][r]. colb: 64 scratch words; Tm: 32 x 32 scratch.
-// Every thread of the workgroup must call it (barriers inside).
-template <typename T>
-__device__ __noinline__ void blk_diag_2x2(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* rd, lds_t<T>* colb, lds_t<T>* Tm,
-                                             int* status, int tid) {
-    asm volatile("" : "+v"(tid));
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
-    const int gi = tid >> 3, gj = (tid & 7) * 4;  // this thread's outputs of a 32 x 32 product: row gi, cols gj..+3
-    lds_t<T>* P22 = P + 32 * TLD + 32;
-    if (w == 0) blk_diag_factor<T, 32>(P, colb, rd, status, ln);
-    __syncthreads();
-    if (w == 0) blk_diag_inverse<T, 32>(P, Q, rd, ln);
-    __syncthreads();
-    T o[4];
-    // L21[i][j] = sum_{q <= j} S21[i][q] Linv11[j][q]   (Linv11[j][q] = Q[q * TLD + j])
-#pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] = (T)0;
-#pragma unroll 8
-    for (int q = 0; q < 32; ++q) {
-        const T sv = P[(32 + gi) * TLD + q];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = fma_t(sv, Q[q * TLD + gj + u], o[u]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) P[(32 + gi) * TLD + gj + u] = o[u];
-    __syncthreads();
-    // S22[i][j] -= sum_q L21[i][q] L21[j][q]; T[i][j] = sum_{q >= j} L21[i][q] Linv11[q][j]
-    T t[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        o[u] = (T)0;
-        t[u] = (T)0;
-    }
-#pragma unroll 8
-    for (int q = 0; q < 32; ++q) {
-        const T lv = P[(32 + gi) * TLD + q];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            o[u] = fma_t(lv, P[(32 + gj + u) * TLD + q], o[u]);
-            t[u] = fma_t(lv, Q[(gj + u) * TLD + q], t[u]);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        P22[gi * TLD + gj + u] -= o[u];
-        Tm[gi * 32 + gj + u] = t[u];
-    }
-    __syncthreads();
-    if (w == 0) blk_diag_factor<T, 32>(P22, colb, rd + 32, status, ln);
-    __syncthreads();
-    if (w == 0) blk_diag_inverse<T, 32>(P22, Q + 32 * TLD + 32, rd + 32, ln);
-    __syncthreads();
-    // Linv21[i][j] = -sum_{p <= i} Linv22[i][p] T[p][j]  (Linv22[i][p] = Q[(32 + p) * TLD + 32 + i])
-#pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] = (T)0;
-#pragma unroll 8
-    for (int p = 0; p < 32; ++p) {
-        const T lv = Q[(32 + p) * TLD + 32 + gi];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = fma_t(lv, Tm[p * 32 + gj + u], o[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        Q[(gj + u) * TLD + 32 + gi] = -o[u];  // Linv21
-        Q[(32 + gj + u) * TLD + gi] = (T)0;  // Linv12
-        P[gi * TLD + 32 + gj + u] = (T)0;    // L12
-    }
-    __syncthreads();
-}
-
-// The same inverse on all 4 waves: a quad of lanes per column c = 16w + (lane
-// >> 2); lane j of the quad sums the terms q = j (mod 4) of each row's dot
-// product, two DPP butterfly adds give every lane of the quad the sum, and
-// lane j keeps x[4m + j] in xs[m]. The serial chain per row is r/4 FMAs
-// instead of r.
-template <int CTRL> __device__ __forceinline__ double dpp_quad(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-template <int CTRL> __device__ __forceinline__ float dpp_quad(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-template <typename T>
-__device__ __forceinline__ void blk_diag_inverse4(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* rd, int tid) {
-    asm volatile("" : "+v"(tid));  // opaque: keep the per-row masks out of the ticket loop
-    const int c = tid >> 2, j = tid & 3;
-    T xs[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) xs[m] = (T)0;
-#pragma unroll
-    for (int r = 0; r < 64; ++r) {
-        T s = (T)0;
-#pragma unroll
-        for (int m = 0; m < (r + 3) / 4; ++m) {  // q = 4m + j < r
-            const T p = P[r * TLD + 4 * m + j];
-            s = fma_t(4 * m + j < r ? p : (T)0, xs[m], s);
-        }
-        s = s + dpp_quad<0xb1>(s);  // quad_perm [1,0,3,2]
-        s = s + dpp_quad<0x4e>(s);  // quad_perm [2,3,0,1]
-        const T xr = ((r == c ? (T)1 : (T)0) - s) * rd[r];
-        xs[r / 4] = j == (r & 3) ? xr : xs[r / 4];
-        if ((r & 3) == 3) asm volatile("" ::: "memory");  // loads of up to 4 rows ahead
-    }
-#pragma unroll
-    for (int m = 0; m < 16; ++m) Q[c * TLD + 4 * m + j] = xs[m];
-}
-
-// Linv of the tile's L (P, lower part) from the inverses Di[p] of its four
-// 16 x 16 diagonal blocks: diagonal blocks Di, zeros above, then the blocks
-// below by distance: Linv[p2][p1] = -Di[p2] sum_q L[p2][q] Linv[q][p1].
-// Q[c * TLD + r] = Linv[r][c]. All threads; barriers inside.
-typedef double bsm_d4 __attribute__((ext_vector_type(4)));
-template <typename T>
-__device__ __forceinline__ void blk_linv_from_blocks(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di,
-                                                     lds_t<T>* Tb, int tid) {
-    (void)Tb;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int e = tid + 256 * u, c = e >> 6, r = e & 63, pr = r >> 4, pc = c >> 4;
-        Q[c * TLD + r] = pr == pc ? Di[pr * 256 + (r & 15) * 16 + (c & 15)] : (T)0;
-    }
-    __syncthreads();
-    // by distance dd, wave p1 forms block (p2, p1) = (p1 + dd, p1) on f64 MFMA
-    // 16x16x4 (lane l: A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; result
-    // rows (l >> 4) + 4q, column l & 15):
-    //   T = sum_{qb = p1}^{p2 - 1} L[p2][qb] Linv[qb][p1];  Linv[p2][p1] = -Di[p2] T
-    // T's result registers are the second product's B operand as they stand
-    // (k step q is rows 4q + (l >> 4)).
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, m = l & 15, kq = l >> 4;
-    for (int dd = 1; dd < 4; ++dd) {
-        if (w < 4 - dd) {
-            const int p1 = w, p2 = p1 + dd;
-            bsm_d4 t = {0.0, 0.0, 0.0, 0.0};
-            for (int qb = p1; qb < p2; ++qb) {
-#pragma unroll
-                for (int k4 = 0; k4 < 4; ++k4) {
-                    const int k = 16 * qb + 4 * k4 + kq;
-                    t = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(16 * p2 + m) * TLD + k],
-                                                             (double)Q[(16 * p1 + m) * TLD + k], t, 0, 0, 0);
-                }
-            }
-            bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4)
-                o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)Di[p2 * 256 + m * 16 + 4 * k4 + kq], t[k4], o, 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Q[(16 * p1 + m) * TLD + 16 * p2 + kq + 4 * q] = (T)o[q];
-        }
-        __syncthreads();
-    }
-}
-
-// Linv of the tile's L (P, lower part) on all four waves: wave 0's four DPP
-// rows invert the four 16 x 16 diagonal blocks at once (lane 16k + r: row r
-// of block k, L[q2][q] by row broadcast), then blk_linv_from_blocks.
-template <typename T>
-__device__ __forceinline__ void blk_diag_inverse_blocked(const lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di,
-                                                         lds_t<T>* Tb, int tid) {
-    asm volatile("" : "+v"(tid));  // opaque: keep the per-row masks out of the ticket loop
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
-        const int k = (tid >> 4) & 3, r = tid & 15;
-        T dv[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) dv[q] = P[(16 * k + r) * TLD + 16 * k + q];
-        T rown = (T)0;  // this row's diagonal element L[r][r]
-#pragma unroll
-        for (int q = 0; q < 16; ++q) rown = q == r ? dv[q] : rown;
-        const T rinv = (T)1 / rown;
-        T x[16];
-        auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
-            T sacc = (T)0;
-            [&]<int... qs>(std::integer_sequence<int, qs...>) __attribute__((always_inline)) {
-                ((sacc = fma_t(rowbcast<q2>(dv[qs]), x[qs], sacc)), ...);
-            }(std::make_integer_sequence<int, q2>{});
-            x[q2] = ((q2 == r ? (T)1 : (T)0) - sacc) * rowbcast<q2>(rinv);
-        };
-        [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-            (irow(std::integral_constant<int, ts>{}), ...);
-        }(std::make_integer_sequence<int, 16>{});
-#pragma unroll
-        for (int q2 = 0; q2 < 16; ++q2) Di[k * 256 + q2 * 16 + r] = x[q2];  // Di[k][row][col]
-    }
-    __syncthreads();
-    blk_linv_from_blocks<T>(P, Q, Di, Tb, tid);
-}
-
-// Block (p2, p1), p1 < p2, of Linv on one wave (f64 MFMA 16x16x4, as in
-// blk_linv_from_blocks): Linv[p2][p1] = -Di[p2] sum_{q = p1}^{p2 - 1} L[p2][q] Linv[q][p1],
+// Block (p2, p1), p1 < p2, of Linv on one wave (f64 MFMA 16x16x4):
+// Linv[p2][p1] = -Di[p2] sum_{q = p1}^{p2 - 1} L[p2][q] Linv[q][p1],
 // from row blocks < p2 of Linv already in Q (Q[c * TLD + r] = Linv[r][c]).
 template <typename T>
 __device__ __forceinline__ void blk_linv_block(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di, int p2, int p1,
@@ -2800,13 +1508,13 @@ __device__ __forceinline__ void blk_linv_diag(lds_t<T>* Q, const lds_t<T>* Di, i
 // Linv by row blocks: row block p - 1 on waves 1-3 while wave 0 factors
 // block p, the last one at the end. rd[r] = 1 / L[r][r].
 // Every thread of the workgroup must call it (barriers inside).
-// Progressive publication (dpub != nullptr, BSM_BLK_PROG=1): Linv's row block
+// Progressive publication (dpub): Linv's row block
 // p - 1 is complete once wave 0 has factored block p; wave 3, idle in the rows
 // below and the trailing update from panel 1 on, stores it to dpub (this
 // tile's Dinv, dpub[s * 64 + l] = Linv[l][s]) and raises rbf[p - 1] when the
 // stores have drained, one panel later. The next diagonal tile forms the
 // matching column block of its sub-diagonal tile and that block's update
-// while this factor runs (blk_chol, `prog`): only row block 3 is left on the
+// while this factor runs (blk_chol): only row block 3 is left on the
 // chain. Row block 3 goes out with the tile's flag, as before.
 template <typename T>
 __device__ __forceinline__ void blk_publish_rowblock(const lds_t<T>* Q, T* __restrict__ dpub, int c, int lane) {
@@ -2821,11 +1529,10 @@ __device__ __forceinline__ void blk_publish_flag(int* rbf, int c, int lane) {
     if (lane == 0) __hip_atomic_store(&rbf[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename T, bool NR1 = false>
+template <typename T>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
-                                                int* status, int tid, unsigned long long* tdbg = nullptr,
-                                                T* __restrict__ dpub = nullptr, int* rbf = nullptr,
-                                                int* pflag = nullptr, T* __restrict__ p3 = nullptr) {
+                                                int* status, int tid, unsigned long long* tdbg,
+                                                T* __restrict__ dpub, int* rbf, int* pflag) {
     long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
     asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2863,7 +1570,7 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
                 const T piv = rowbcast<t>(nxt);
                 pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
-                const T rp = NR1 ? rsqrt_nr1(piv) : rsqrt_nr(piv);
+                const T rp = rsqrt_nr1(piv);
                 rps[t] = rp;
                 const T l = dv[t] * rp;  // lane t: the pivot's square root
                 dv[t] = l;
@@ -2887,14 +1594,6 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];  // Di[p][row][col]
 #pragma unroll
             for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
-            if (p3 && p == 3 && (tid & 63) < 16) {
-                // BSM_BLK_PROG=2: Di[3] out at once (its flag rbf[3] at the
-                // loop's end, beside rbf[2], before Linv's last row block is
-                // assembled): the next tile's last column block needs only it
-                // and L's blocks (3, c < 3), which go out with Linv's row blocks
-#pragma unroll
-                for (int q2 = 0; q2 < 16; ++q2) st_sc1(&p3[768 + q2 * 16 + r], x[q2]);
-            }
         }
         // pflag: the caller's global stores (the sub-diagonal tile) drain on
         // every wave during block 0's factor; the flag follows the barrier
@@ -2903,13 +1602,6 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
         const long long t1 = tdbg ? clock64() : 0;
         if (pflag && p == 0 && tid == 192) __hip_atomic_store(pflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (dpub && w == 3 && p >= 1) blk_publish_rowblock<T>(Q, dpub, p - 1, tid & 63);
-        if (p3 && w == 3 && p >= 1) {  // L's block (3, p - 1), final since panel p - 1: raised with rbf[p - 1]
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = (tid & 63) + 64 * u;
-                st_sc1(&p3[(p - 1) * 256 + i], (T)P[(48 + (i >> 4)) * TLD + 16 * (p - 1) + (i & 15)]);
-            }
-        }
         // 2. rows below the block, one 16-row block per wave on f64 MFMA
         //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
         const int l = tid & 63, m = l & 15, kq = l >> 4;
@@ -2956,7 +1648,6 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
     }
     // Linv's last row block and diagonal block
     if (w < 3) {
-        if (p3 && w == 0) blk_publish_flag(rbf, 3, tid & 63);  // Di[3], stored after the last pivots
         blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
     } else {
         if (dpub) blk_publish_flag(rbf, 2, tid & 63);
@@ -3003,179 +1694,15 @@ __device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B,
         for (int q = 0; q < 4; ++q) X[cb][q] = (T)c[cb][q];
 }
 
-// ---------------------------------------------------------------------------
-// The chain workgroup's dataflow (BSM_BLK_CHAIN=2, an A/B variant). One block
-// column K of the blocked factor, as tasks over 16 x 16 blocks of the diagonal
-// tile (P, row-major) and of L_{K,K-1}^T (A):
-//   PR(w)        wave w: its 16 rows of S_{K,K} to P and of S_{K,K-1}^T to A,
-//                then its row block of L_{K,K-1} = S_{K,K-1} Linv_{K-1}^T (Q
-//                still holds Linv_{K-1}^T), in place in A;
-//   U1(pi, pj)   P[pi][pj] -= L_{K,K-1}[pi] L_{K,K-1}[pj]^T (block column K-1);
-//   F(p)         the 16 x 16 diagonal block p: factor, inverse Di[p], 1/pivots;
-//   R(pb, p)     L[pb][p] = S[pb][p] Di[p]^T;
-//   U(pi, pj, p) P[pi][pj] -= L[pi][p] L[pj][p]^T;
-//   LD(p), LB(p2, p1)  Linv's diagonal and off-diagonal blocks into Q.
-// Each task is the same MFMA / DPP sequence per element as blk_diag_panels and
-// the update of the one-workgroup-per-tile form, so the factor is bit-identical
-// to both; only the order of independent blocks changes. Wave 0 runs the
-// pivot chain's tasks, F(p) -> R(p+1, p) -> U(p+1, p+1, p) -> F(p+1), with no
-// workgroup barrier between them; waves 1-3 take the other tasks from an LDS
-// queue in priority order. A task waits on the done flags (LDS) of the tasks
-// it reads from; every dependency is earlier in the queue or on wave 0's list,
-// which only waits on earlier queue tasks, so the order cannot deadlock
-// (checked by simulation when the table was made).
-enum { TK_U1 = 1, TK_F, TK_R, TK_U, TK_LD, TK_LB };
-struct ChainTask {
-    uint8_t type, a, b, c;
-    int8_t dep[4];
-};
-constexpr int CH_ALLPR = 44;  // pseudo-task: every PR done (Q may be overwritten)
-__constant__ ChainTask kChainTasks[44] = {
-    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 0 PR(0)
-    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 1 PR(1)
-    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 2 PR(2)
-    {0, 0, 0, 0, {-1, -1, -1, -1}},  // 3 PR(3)
-    {TK_U1, 0, 0, 0, {0, -1, -1, -1}},  // 4
-    {TK_U1, 1, 0, 0, {0, 1, -1, -1}},  // 5
-    {TK_U1, 1, 1, 0, {1, -1, -1, -1}},  // 6
-    {TK_U1, 2, 0, 0, {0, 2, -1, -1}},  // 7
-    {TK_U1, 2, 1, 0, {1, 2, -1, -1}},  // 8
-    {TK_U1, 2, 2, 0, {2, -1, -1, -1}},  // 9
-    {TK_U1, 3, 0, 0, {0, 3, -1, -1}},  // 10
-    {TK_U1, 3, 1, 0, {1, 3, -1, -1}},  // 11
-    {TK_U1, 3, 2, 0, {2, 3, -1, -1}},  // 12
-    {TK_U1, 3, 3, 0, {3, -1, -1, -1}},  // 13
-    {TK_F, 0, 0, 0, {4, -1, -1, -1}},  // 14
-    {TK_F, 1, 0, 0, {24, -1, -1, -1}},  // 15
-    {TK_F, 2, 0, 0, {30, -1, -1, -1}},  // 16
-    {TK_F, 3, 0, 0, {33, -1, -1, -1}},  // 17
-    {TK_R, 1, 0, 0, {14, 5, -1, -1}},  // 18
-    {TK_R, 2, 0, 0, {14, 7, -1, -1}},  // 19
-    {TK_R, 3, 0, 0, {14, 10, -1, -1}},  // 20
-    {TK_R, 2, 1, 0, {15, 25, -1, -1}},  // 21
-    {TK_R, 3, 1, 0, {15, 27, -1, -1}},  // 22
-    {TK_R, 3, 2, 0, {16, 31, -1, -1}},  // 23
-    {TK_U, 1, 1, 0, {18, 6, -1, -1}},  // 24
-    {TK_U, 2, 1, 0, {19, 18, 8, -1}},  // 25
-    {TK_U, 2, 2, 0, {19, 9, -1, -1}},  // 26
-    {TK_U, 3, 1, 0, {20, 18, 11, -1}},  // 27
-    {TK_U, 3, 2, 0, {20, 19, 12, -1}},  // 28
-    {TK_U, 3, 3, 0, {20, 13, -1, -1}},  // 29
-    {TK_U, 2, 2, 1, {21, 26, -1, -1}},  // 30
-    {TK_U, 3, 2, 1, {22, 21, 28, -1}},  // 31
-    {TK_U, 3, 3, 1, {22, 29, -1, -1}},  // 32
-    {TK_U, 3, 3, 2, {23, 32, -1, -1}},  // 33
-    {TK_LD, 0, 0, 0, {14, 44, -1, -1}},  // 34
-    {TK_LD, 1, 0, 0, {15, 44, -1, -1}},  // 35
-    {TK_LD, 2, 0, 0, {16, 44, -1, -1}},  // 36
-    {TK_LD, 3, 0, 0, {17, 44, -1, -1}},  // 37
-    {TK_LB, 1, 0, 0, {15, 34, -1, -1}},  // 38
-    {TK_LB, 2, 0, 0, {16, 34, 38, -1}},  // 39
-    {TK_LB, 2, 1, 0, {16, 35, -1, -1}},  // 40
-    {TK_LB, 3, 0, 0, {17, 34, 38, 39}},  // 41
-    {TK_LB, 3, 1, 0, {17, 35, 40, -1}},  // 42
-    {TK_LB, 3, 2, 0, {17, 36, -1, -1}},  // 43
-};
-constexpr int CH_W0 = 11, CH_NQ = 29;
-__constant__ uint8_t kChainWave0[CH_W0] = {4, 14, 18, 24, 15, 21, 30, 16, 23, 33, 17};
-__constant__ uint8_t kChainQueue[CH_NQ] = {5,  6,  7,  8,  9,  10, 11, 12, 13, 19, 20, 25, 26, 27, 28,
-                                           29, 34, 22, 31, 32, 38, 35, 39, 40, 36, 41, 42, 43, 37};
-
-// F(p): wave 0's 16 x 16 block factor and inverse of blk_diag_panels
-template <typename T, bool NR1>
-__device__ __forceinline__ void blk_block_factor(lds_t<T>* P, lds_t<T>* Di, lds_t<T>* rd, int p, int tid, bool& pd) {
-    const int c0 = 16 * p, r = tid & 15;
-    T dv[16], rps[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dv[j] = P[(c0 + r) * TLD + c0 + j];
-    auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
-        const T piv = rowbcast<t>(dv[t]);
-        pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
-        const T rp = NR1 ? rsqrt_nr1(piv) : rsqrt_nr(piv);
-        rps[t] = rp;
-        const T l = dv[t] * rp;
-        dv[t] = l;
-        [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
-            ((dv[t + 1 + js] = fma_t(-l, rowbcast<t + 1 + js>(l), dv[t + 1 + js])), ...);
-        }(std::make_integer_sequence<int, 15 - t>{});
-    };
-    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-        (step(std::integral_constant<int, ts>{}), ...);
-    }(std::make_integer_sequence<int, 16>{});
-#pragma unroll
-    for (int j = 0; j < 16; ++j) P[(c0 + r) * TLD + c0 + j] = j <= r ? dv[j] : (T)0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(dv[j]));
-    T x[16];
-    auto irow = [&]<int q2>(std::integral_constant<int, q2>) __attribute__((always_inline)) {
-        T sm = (T)0;
-        [&]<int... qs>(std::integer_sequence<int, qs...>) __attribute__((always_inline)) {
-            ((sm = fma_t(rowbcast<q2>(dv[qs]), x[qs], sm)), ...);
-        }(std::make_integer_sequence<int, q2>{});
-        x[q2] = ((q2 == r ? (T)1 : (T)0) - sm) * rps[q2];
-    };
-    [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-        (irow(std::integral_constant<int, ts>{}), ...);
-    }(std::make_integer_sequence<int, 16>{});
-#pragma unroll
-    for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
-}
-
-// R(pb, p): L[pb][p] = S[pb][p] Di[p]^T (one wave, f64 MFMA 16x16x4)
 template <typename T>
-__device__ __forceinline__ void blk_rows_below(lds_t<T>* P, const lds_t<T>* Di, int pb, int p, int l) {
-    const int m = l & 15, kq = l >> 4, r0 = 16 * pb, c0 = 16 * p;
-    bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
-        const int k = 4 * k4 + kq;
-        o = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(r0 + m) * TLD + c0 + k], (double)Di[p * 256 + m * 16 + k],
-                                                 o, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) P[(r0 + kq + 4 * q) * TLD + c0 + m] = (T)o[q];
-}
-
-// U(pi, pj, p): P[pi][pj] -= L[pi][p] L[pj][p]^T (K4 k-steps of 4: 4 within
-// the tile's panel p, from P); U1: the same with the 64 columns of L_{K,K-1}^T
-// in A (16 k-steps)
-template <typename T, int K4>
-__device__ __forceinline__ void blk_block_update(lds_t<T>* P, const lds_t<T>* X, int pi, int pj, int p, int l) {
-    const int m = l & 15, kq = l >> 4, i0 = 16 * pi, j0 = 16 * pj;
-    bsm_d4 o;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = (double)P[(i0 + kq + 4 * q) * TLD + j0 + m];
-#pragma unroll
-    for (int k4 = 0; k4 < K4; ++k4) {
-        const int k = 4 * k4 + kq;
-        if (K4 == 4)  // L columns of panel p, rows i0.. / j0.. (P row-major)
-            o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)P[(i0 + m) * TLD + 16 * p + k],
-                                                     (double)P[(j0 + m) * TLD + 16 * p + k], o, 0, 0, 0);
-        else  // X = L_{K,K-1}^T: X[k][r] = L[r][k]
-            o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)X[k * TLD + i0 + m], (double)X[k * TLD + j0 + m], o, 0,
-                                                     0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
-}
-
-// MODE: 0 one workgroup per tile (default), 1 / 2 the chain workgroup and its
-// dataflow form (BSM_BLK_CHAIN): an instance per mode, so the default kernel
-// carries none of the chain's registers.
-template <typename T, int MODE>
 __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                 T* __restrict__ Dinv, int* __restrict__ flags,
                                                 int* __restrict__ ticket, int* __restrict__ status,
                                                 unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
-                                                int panels, T* __restrict__ pend, int* __restrict__ pendf,
-                                                int chain_mode, int* __restrict__ rbf, T* __restrict__ pub3) {
+                                                int* __restrict__ rbf) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
-    __shared__ T AT[64][TLD];  // the dataflow chain: S_{K,K-1}^T, then L_{K,K-1}^T in place
-    __shared__ int tdone[48];  // the dataflow chain's task flags (CH_ALLPR included)
-    __shared__ int qhead, prcnt, subcnt;
+    __shared__ T AT[64][TLD];  // L_{K,K-1}^T as its column blocks form
     __shared__ T rd[64];
     __shared__ T Di[4 * 256];  // blk_diag_panels: the 16 x 16 diagonal blocks' inverses
     __shared__ T Tb[3 * 256];  //                  and its block products
@@ -3242,288 +1769,18 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
     const int rb = 16 * w + (lane >> 4), cm = lane & 15;
     lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
     lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
-    const bool chain = MODE != 0 && pend != nullptr;
     for (;;) {
         if (tid == 0) tk = atomicAdd(ticket, 1);
         __syncthreads();
         const int64_t t0 = tk;
         if (dbg && tid == 0) __hip_atomic_fetch_max(&dbg[0], (unsigned long long)t0, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_SYSTEM);
-        if (chain && t0 == 0) {
-            // THE CHAIN (ticket 0, one workgroup for the whole factor): for each
-            // block column K, the sub-diagonal tile L_{K,K-1} = S_{K,K-1}
-            // Linv_{K-1}^T with Linv_{K-1} still in LDS from the previous
-            // factor, the diagonal update by it, the factor of the diagonal
-            // tile, Dinv[K] and L_{K,K} out. S_{K,K} and S_{K,K-1} with every
-            // block column J <= K-2 applied come from the pending tile K
-            // (ticketed below, publishing to pend), which has the chain's whole
-            // factor of K-1 to finish its last update. Against one workgroup per
-            // diagonal tile this removes the hand-off of Dinv between
-            // workgroups (flag wait + staging of Linv) on the chain.
-            T acc[4][4], acc2[4][4];
-            long long ck[6] = {0, 0, 0, 0, 0, 0};
-            if (MODE == 2) {
-                // the dataflow form (see kChainTasks)
-                lds_t<T>* const ATl = (lds_t<T>*)&AT[0][0];
-                bool pd = true;
-                auto wait_done = [&](int id) {
-                    long long spins = 0;
-                    while (__hip_atomic_load(&tdone[id], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spins > SPIN_LIMIT) {
-                            if (lane == 0) atomicOr(status, ST_TIMEOUT);
-                            return;
-                        }
-                    }
-                };
-                auto set_done = [&](int id) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_store(&tdone[id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                };
-                auto run = [&](int id, int slot) {
-                    const ChainTask tk = kChainTasks[id];
-                    const long long cw = (tdbg && slot >= 0) ? clock64() : 0;
-#pragma unroll
-                    for (int d = 0; d < 4; ++d)
-                        if (tk.dep[d] >= 0) wait_done(tk.dep[d]);
-                    const long long cr = (tdbg && slot >= 0) ? clock64() : 0;
-                    switch (tk.type) {
-                        case TK_U1: blk_block_update<T, 16>(PTl, ATl, tk.a, tk.b, 0, lane); break;
-                        case TK_F:
-                            blk_block_factor<T, true>(PTl, (lds_t<T>*)Di, (lds_t<T>*)rd, tk.a, tid, pd);
-                            break;
-                        case TK_R: blk_rows_below<T>(PTl, (lds_t<T>*)Di, tk.a, tk.b, lane); break;
-                        case TK_U: blk_block_update<T, 4>(PTl, PTl, tk.a, tk.b, tk.c, lane); break;
-                        case TK_LD: blk_linv_diag<T>(QTl, (lds_t<T>*)Di, tk.a, lane); break;
-                        case TK_LB: blk_linv_block<T>(PTl, QTl, (lds_t<T>*)Di, tk.a, tk.b, lane); break;
-                        default: break;
-                    }
-                    set_done(id);
-                    if (tdbg && slot >= 0 && lane == 0) {  // BSM_BLK_DEBUG: wave 0's task `slot`: wait, run
-                        const long long ce = clock64();
-                        __hip_atomic_fetch_add(&tdbg[24 + slot], (unsigned long long)(cr - cw), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_fetch_add(&tdbg[36 + slot], (unsigned long long)(ce - cr), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                };
-                auto load_pend2 = [&](int64_t Kp) {
-                    const long long cw = tdbg ? clock64() : 0;
-                    wait_flag(&pendf[Kp]);
-                    if (tdbg && tid == 0)
-                        __hip_atomic_fetch_add(&tdbg[0], (unsigned long long)(clock64() - cw), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    const T* pp = pend + Kp * 8192 + tid;
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            acc[cb][q] = ld_sc1(pp + (4 * cb + q) * 256);
-                            acc2[cb][q] = ld_sc1(pp + 4096 + (4 * cb + q) * 256);
-                        }
-                };
-                load_pend2(0);
-                // Linv's strictly upper blocks stay zero for the whole factor:
-                // LD / LB only ever write the lower ones
-#pragma unroll
-                for (int u = 0; u < 16; ++u) QT[tid >> 2][16 * (tid & 3) + u] = (T)0;
-                for (int64_t K = 0; K < nb64; ++K) {
-                    if (tid < 48) tdone[tid] = 0;
-                    if (tid == 0) {
-                        qhead = 0;
-                        prcnt = 0;
-                        subcnt = 0;
-                    }
-                    __syncthreads();
-                    if (tdbg) ck[0] = clock64();
-                    // PR(w): this wave's rows of S_{K,K} to P, its strip of S_{K,K-1}^T
-                    // to A, its row block of L_{K,K-1} (A and Q), back into its strip
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
-                            AT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
-                        }
-                    T o[4][4] = {};
-                    mfma_tile<T, false, true>(ATl, QTl, o, w, lane);
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) AT[16 * cb + cm][rb + 4 * q] = o[cb][q];
-                    set_done(w);
-                    if (lane == 0 && __hip_atomic_fetch_add(&prcnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3)
-                        __hip_atomic_store(&tdone[CH_ALLPR], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    // L_{K,K-1} to the band; the tile's flag once all four waves'
-                    // stores have drained (pending tile K+1's last update waits on it)
-                    if (K > 0) {
-#pragma unroll
-                        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const int r = rb + 4 * q, c = 16 * cb + cm;
-                                if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
-                            }
-                    }
-                    auto sub_done = [&] {
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0 &&
-                            __hip_atomic_fetch_add(&subcnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 3 &&
-                            K > 0 && DM > 1)
-                            __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    };
-                    if (tdbg) ck[1] = clock64();
-                    if (w == 0) {  // the pivot chain; its own stores drain behind F(0)
-                        for (int i = 0; i < CH_W0; ++i) {
-                            run(kChainWave0[i], i);
-                            if (i == 1) sub_done();
-                        }
-                    } else {
-                        sub_done();
-                        for (;;) {
-                            int qi = 0;
-                            if (lane == 0) qi = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            qi = __builtin_amdgcn_readfirstlane(qi);
-                            if (qi >= CH_NQ) break;
-                            run(kChainQueue[qi], -1);
-                        }
-                    }
-                    if (tdbg) ck[2] = clock64();
-                    __syncthreads();
-                    // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]; L_{K,K} to the band
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        const int e = tid + 256 * u;
-                        st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                    if (tid == 0) __hip_atomic_store(&flags[K * DM], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {  // no tile of this kernel reads L_{K,K}: drains later
-                        const int e = tid + 256 * u, r = e & 63, c = e >> 6;
-                        if (r >= c && in_band(K, K, r, c)) st_sc1(&CB[band_idx(K, K, r, c)], PT[r][c]);
-                    }
-                    if (K + 1 < nb64) load_pend2(K + 1);
-                    if (tdbg && tid == 0) {
-                        ck[3] = clock64();
-                        __hip_atomic_fetch_add(&tdbg[20], (unsigned long long)(ck[1] - ck[0]), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_fetch_add(&tdbg[21], (unsigned long long)(ck[2] - ck[1]), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_fetch_add(&tdbg[22], (unsigned long long)(ck[3] - ck[2]), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_fetch_add(&tdbg[23], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const unsigned long long wc = wall_clock64();
-                        if (K == 0) __hip_atomic_store(&tdbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (K == nb64 - 1)
-                            __hip_atomic_store(&tdbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                if (w == 0 && lane == 0 && !pd) atomicOr(status, ST_NOT_PD);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                continue;
-            }
-            auto load_pend = [&](int64_t Kp) {
-                const long long cw = tdbg ? clock64() : 0;
-                wait_flag(&pendf[Kp]);
-                if (tdbg && tid == 0)
-                    __hip_atomic_fetch_add(&tdbg[0], (unsigned long long)(clock64() - cw), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                const T* pp = pend + Kp * 8192 + tid;  // element (cb, q) of thread tid at (4 cb + q) * 256 + tid
-#pragma unroll
-                for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        acc[cb][q] = ld_sc1(pp + (4 * cb + q) * 256);
-                        acc2[cb][q] = ld_sc1(pp + 4096 + (4 * cb + q) * 256);
-                    }
-            };
-            load_pend(0);
-            for (int64_t K = 0; K < nb64; ++K) {
-                if (tdbg) ck[0] = clock64();
-                if (K > 0) {
-                    // L_{K,K-1} = S_{K,K-1} Linv_{K-1}^T; QT holds Linv_{K-1}^T
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
-                    __syncthreads();
-                    T o[4][4] = {};
-                    mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int r = rb + 4 * q, c = 16 * cb + cm;
-                            if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
-                        }
-                    __syncthreads();  // every wave has read PT
-#pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = o[cb][q];
-                    __syncthreads();
-                    mfma_tile<T, true>(PTl, PTl, acc, w, lane);  // S_{K,K} -= L_{K,K-1} L_{K,K-1}^T
-                    // L_{K,K-1} drained: its flag (pending tile K+1's last update waits on it)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                    if (tid == 0 && DM > 1)
-                        __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (tdbg) ck[1] = clock64();
-#pragma unroll
-                for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
-                __syncthreads();
-                blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
-                                         (lds_t<T>*)rd, status, tid, tdbg);
-                if (tdbg) ck[2] = clock64();
-                // Dinv[K][q * TLD + l] = Linv[l][q] = QT[q][l]; L_{K,K} to the band
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int e = tid + 256 * u;
-                    st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
-                }
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int e = tid + 256 * u, r = e & 63, c = e >> 6;
-                    if (r >= c && in_band(K, K, r, c)) st_sc1(&CB[band_idx(K, K, r, c)], PT[r][c]);
-                }
-                // Dinv[K] at once (drained, then its flag): tile (K+2, K) needs it for
-                // pending tile K+2, whose last update the chain waits for after
-                // the NEXT factor (a flag deferred to the next round stalled the
-                // chain: 36 us per block column against 21)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) __hip_atomic_store(&flags[K * DM], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (K + 1 < nb64) load_pend(K + 1);
-                if (tdbg && tid == 0) {  // BSM_BLK_DEBUG: the chain's three steps per block column
-                    ck[3] = clock64();
-                    __hip_atomic_fetch_add(&tdbg[20], (unsigned long long)(ck[1] - ck[0]), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&tdbg[21], (unsigned long long)(ck[2] - ck[1]), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&tdbg[22], (unsigned long long)(ck[3] - ck[2]), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&tdbg[23], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long wc = wall_clock64();
-                    if (K == 0) __hip_atomic_store(&tdbg[12], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (K == nb64 - 1) __hip_atomic_store(&tdbg[13], wc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            continue;
-        }
-        const int64_t t = chain ? t0 - 1 : t0;
+        const int64_t t = t0;
         if (t >= nb64 * DM) break;
         const int64_t K = t / DM, d = t % DM, I = K + d;
         int* fl = flags + K * DM;
         // no such tile (past the matrix or the band), or the sub-diagonal tile
-        // (K + 1, K), which diagonal tile K + 1's workgroup (or the chain) forms
+        // (K + 1, K), which diagonal tile K + 1's workgroup forms
         // (one hand-off on the chain per block column instead of two)
         if (I >= nb64 || 64 * d - 63 > b || d == 1) {
             __syncthreads();
@@ -3552,13 +1809,10 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
         // left-looking updates from block columns J in the band of both I and K
         // (with sub, J = K - 1 comes after tile (K, K - 1) is formed, below)
         const int64_t Jlo = I - (DM - 1) > 0 ? I - (DM - 1) : 0;
-        long long cp0 = 0, cp1 = 0;  // BSM_BLK_DEBUG (pending tiles): the last J's flag wait and the rest
         for (int64_t J = Jlo; J < (sub ? K - 1 : K); ++J) {
-            if (tdbg && chain && d == 0 && J + 2 == K) cp0 = clock64();
             wait_flag(&flags[J * DM + (I - J)]);
             if (d > 0) wait_flag(&flags[J * DM + (K - J)]);
             if (sub) wait_flag(&flags[J * DM + (K - 1 - J)]);
-            if (tdbg && chain && d == 0 && J + 2 == K) cp1 = clock64();
             stage(PT, I, J);
             if (d > 0) stage(QT, K, J);
             if (sub) stage(QT, K - 1, J);
@@ -3567,42 +1821,14 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             if (sub) mfma_tile<T, true>(PTl, QTl, acc2, w, lane);
             __syncthreads();
         }
-        if (chain && d == 0) {
-            // pending tile K for the chain: S_{K,K} and S_{K,K-1} with block
-            // columns J <= K-2 applied, in the accumulator layout, element
-            // (cb, q) of every thread contiguous (2 KiB per store instruction;
-            // thread-contiguous rows made each 8-B store touch its own line:
-            // 48.6k cycles from the last update to the publication)
-            T* pp = pend + K * 8192 + tid;
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    st_sc1(pp + (4 * cb + q) * 256, acc[cb][q]);
-                    st_sc1(pp + 4096 + (4 * cb + q) * 256, acc2[cb][q]);
-                }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&pendf[K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tdbg && tid == 0 && cp0) {
-                __hip_atomic_fetch_add(&tdbg[1], (unsigned long long)(cp1 - cp0), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(&tdbg[2], (unsigned long long)(clock64() - cp1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(&tdbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (dbg && tid == 0) __hip_atomic_fetch_add(&dbg[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            continue;
-        }
         long long cw0 = 0, cw1 = 0, cs1 = 0, cs2 = 0, cs3 = 0;  // BSM_BLK_DEBUG: the chain's steps
-        if (sub && rbf && panels == 1) {
-            // Progressive (BSM_BLK_PROG=1): column block c of L_{K,K-1} =
-            // S_{K,K-1} (row block c of Linv_{K-1})^T as soon as tile K - 1 has
-            // published that row block, then its share of the update
-            // S_{K,K} -= L_{K,K-1}[:, c] L_{K,K-1}[:, c]^T. Blocks 0-2 overlap
-            // tile K - 1's factor. Per output element the MFMA sequence is
-            // mfma_tile's (k ascending from the same start), so the bits are
-            // those of the one-shot form below.
+        if (sub) {
+            // Progressive: column block c of L_{K,K-1} = S_{K,K-1} (row block c
+            // of Linv_{K-1})^T as soon as tile K - 1 has published that row
+            // block, then its share of the update S_{K,K} -= L_{K,K-1}[:, c]
+            // L_{K,K-1}[:, c]^T. Blocks 0-2 overlap tile K - 1's factor. Per
+            // output element the MFMA sequence is mfma_tile's (k ascending from
+            // the same start), so the bits are those of the whole-tile form.
             lds_t<T>* const ATl = (lds_t<T>*)&AT[0][0];
             const int kq = lane >> 4, m = lane & 15;
 #pragma unroll
@@ -3615,40 +1841,8 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
 #pragma unroll
                 for (int q = 0; q < 4; ++q) ca[cb][q] = (double)acc[cb][q];
             const T* dk = Dinv + (K - 1) * 4096;
-            // BSM_BLK_PROG=2: column block 3 by the triangular form
-            // L[:, 3] = (S[:, 3] - sum_{c<3} L[:, c] L_{K-1}[3][c]^T) Di[3]^T: the
-            // sum runs while tile K - 1 still factors its last panel, and only
-            // Di[3] (published by its wave 0 at once) is waited for
-            const T* p3k = pub3 ? pub3 + (K - 1) * 1024 : nullptr;
-            bsm_d4 t3 = {0.0, 0.0, 0.0, 0.0};  // prog 2: S[:, 3] - sum_{c < 3} L[:, c] L_{K-1}[3][c]^T, as c forms
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                if (p3k && c == 3) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) AT[48 + m][16 * w + kq + 4 * q] = (T)t3[q];
-                    if (tdbg) cw0 = clock64();
-                    wait_flag(&rbf[(K - 1) * 4 + 3]);
-                    if (tdbg) cw1 = clock64();
-                    Di[tid] = ld_sc1(&p3k[768 + tid]);  // Di[3][row][col] of tile K - 1
-                    __syncthreads();
-                    if (tdbg) cs1 = clock64();
-                    bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                    for (int k4 = 0; k4 < 4; ++k4) {
-                        const int k = 4 * k4 + kq;
-                        oc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)ATl[(48 + k) * TLD + 16 * w + m],
-                                                                  (double)Di[m * 16 + k], oc, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int r = rb + 4 * q, cc = 48 + cm;
-                        const T o = (T)oc[q];
-                        if (in_band(K, K - 1, r, cc)) st_sc1(&CB[band_idx(K, K - 1, r, cc)], o);
-                        AT[cc][r] = o;
-                    }
-                    __syncthreads();
-                    if (tdbg) cs2 = clock64();
-                } else {
                 if (tdbg && c == 3) cw0 = clock64();
                 wait_flag(c < 3 ? &rbf[(K - 1) * 4 + c] : &flags[(K - 1) * DM]);
                 if (tdbg && c == 3) cw1 = clock64();
@@ -3658,18 +1852,12 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                     const int i = tid + 256 * u, s = i >> 4, j = i & 15;
                     v[u] = s < 16 * c + 16 ? ld_sc1(&dk[s * 64 + 16 * c + j]) : (T)0;
                 }
-                const T l3 = p3k && c < 3 ? ld_sc1(&p3k[c * 256 + tid]) : (T)0;  // L_{K-1}'s block (3, c)
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = tid + 256 * u, s = i >> 4, j = i & 15;
                     if (s < 16 * c + 16) QT[s][16 * c + j] = v[u];
                 }
-                if (p3k && c < 3) Tb[c * 256 + tid] = l3;
                 __syncthreads();
-                if (p3k && c == 0) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) t3[q] = (double)PT[48 + m][16 * w + kq + 4 * q];
-                }
                 if (tdbg && c == 3) cs1 = clock64();
                 bsm_d4 oc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -3687,15 +1875,6 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                 }
                 __syncthreads();
                 if (tdbg && c == 3) cs2 = clock64();
-                if (p3k && c < 3) {
-#pragma unroll
-                    for (int k4 = 0; k4 < 4; ++k4) {
-                        const int k = 4 * k4 + kq;
-                        t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)ATl[(16 * c + k) * TLD + 16 * w + m],
-                                                                  (double)Tb[c * 256 + m * 16 + k], t3, 0, 0, 0);
-                    }
-                }
-                }
 #pragma unroll
                 for (int k4 = 0; k4 < 4; ++k4) {
                     const int k = 16 * c + 4 * k4 + kq;
@@ -3713,42 +1892,6 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
             // the tile's flag (read by tiles below, not by this chain) is raised
             // inside the factor, once every wave's stores have drained there
             if (tdbg) cs3 = clock64();
-        } else if (sub) {
-            // L_{K,K-1} = S_{K,K-1} L_{K-1,K-1}^-T once diagonal tile K - 1 is done
-            if (tdbg) cw0 = clock64();
-            wait_flag(&flags[(K - 1) * DM]);
-            if (tdbg) cw1 = clock64();
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc2[cb][q];
-            stage_dinv(QT, K - 1);
-            __syncthreads();
-            if (tdbg) cs1 = clock64();
-            T o[4][4] = {};
-            mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int r = rb + 4 * q, c = 16 * cb + cm;
-                    if (in_band(K, K - 1, r, c)) st_sc1(&CB[band_idx(K, K - 1, r, c)], o[cb][q]);
-                }
-            if (tdbg) cs2 = clock64();
-            // the J = K - 1 update of the diagonal tile with it: PT[t][r] = L_{K,K-1}[r][t].
-            // The stores above drain meanwhile: the tile's flag (read by tiles
-            // below, not by this chain) goes out after the update.
-            __syncthreads();  // every wave has read PT (the product) before it is overwritten
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = o[cb][q];
-            __syncthreads();
-            mfma_tile<T, true>(PTl, PTl, acc, w, lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&flags[(K - 1) * DM + 1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tdbg) cs3 = clock64();
         }
         if (d == 0) {
             const long long c0 = tdbg ? clock64() : 0;
@@ -3758,29 +1901,15 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
 #pragma unroll
                 for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
             __syncthreads();
-            if (panels == 3) {  // 2 x 2 blocks of 32
-                blk_diag_2x2<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, (lds_t<T>*)Tb,
-                                (lds_t<T>*)Di, status, tid);
-            } else if (panels == 4) {  // A/B: the panels with two Newton steps per pivot (round-2 form)
-                blk_diag_panels<T, false>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
-                                          (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg);
-            } else if (panels) {  // factor and inverse by 16-column panels on all four waves (default);
-                // one Newton step per pivot: C5 factor 317 -> 311 ms, x error 8.8e-11 -> 9.7e-11
-                blk_diag_panels<T, true>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di,
-                                         (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, tdbg,
-                                         rbf ? Dinv + K * 4096 : nullptr, rbf ? rbf + K * 4 : nullptr,
-                                         rbf && sub ? &flags[(K - 1) * DM + 1] : nullptr,
-                                         rbf && pub3 ? pub3 + K * 1024 : nullptr);
-            } else {  // one-wave factor; the inverse below
-                if (w == 0)
-                    blk_diag_factor<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)rd, status, lane);
-                __syncthreads();
-            }
+            // factor and inverse by 16-column panels on all four waves, the
+            // products on f64 MFMA; one Newton step per pivot (C5 factor 317 ->
+            // 311 ms, x error 8.8e-11 -> 9.7e-11 against two); Linv's row blocks
+            // 0-2 published as they form (rbf), its flag and L_{K,K-1}'s after
+            // the first barrier
+            blk_diag_panels<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
+                               (lds_t<T>*)rd, status, tid, tdbg, Dinv + K * 4096, rbf + K * 4,
+                               sub ? &flags[(K - 1) * DM + 1] : nullptr);
             const long long c1 = tdbg ? clock64() : 0;
-            if (!panels)
-                blk_diag_inverse_blocked<T>((lds_t<T>*)&PT[0][0], (lds_t<T>*)&QT[0][0], (lds_t<T>*)Di, (lds_t<T>*)Tb,
-                                            tid);
-
             __syncthreads();
             if (tdbg && tid == 0) {  // cycles: factor, inverse (BSM_BLK_DEBUG)
                 const long long c2 = clock64();
@@ -3801,20 +1930,12 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-            // Dinv[K][q * 64 + l] = Linv[l][q] = QT[q][l] (progressive: row blocks
-            // 0-2 are out already, row block 3 is left)
-            if (rbf && panels == 1) {
+            // Dinv[K][q * 64 + l] = Linv[l][q] = QT[q][l] (row blocks 0-2 are
+            // out already, row block 3 is left)
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = tid + 256 * u, q = i >> 4, j = i & 15;
-                    st_sc1(&Dinv[K * 4096 + q * 64 + 48 + j], QT[q][48 + j]);
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int e = tid + 256 * u;
-                    st_sc1(&Dinv[K * 4096 + e], QT[e >> 6][e & 63]);
-                }
+            for (int u = 0; u < 4; ++u) {
+                const int i = tid + 256 * u, q = i >> 4, j = i & 15;
+                st_sc1(&Dinv[K * 4096 + q * 64 + 48 + j], QT[q][48 + j]);
             }
             if (tdbg) {  // the publication: stores drained, then the flag (below)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3874,7 +1995,7 @@ inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 // --------------------------------------------------------------------------
 struct Band {
     DBuf cb;
-    DBuf r;  // 1 / L[k][k] per column (+64 scratch entries), band_chol3
+    DBuf r;  // 1 / L[k][k] per column (+64 scratch entries)
     int64_t n = 0, b = 0, ld = 1;
 };
 
@@ -3896,63 +2017,6 @@ int band_analyse(const bsm_csr* a, hipStream_t s, int64_t* bw_out, bool* sorted,
     return BSM_OK;
 }
 
-template <typename T, int M>
-int launch_chol(Band& bd, int* progress, int* status, hipStream_t s, unsigned long long* trace) {
-    const int64_t n_tiles = (bd.n + TR - 1) / TR;
-    const size_t shm = (size_t)(bd.b + 1) * sizeof(T);
-    int dev = 0, cus = 0;
-    BSM_HIP_TRY(hipGetDevice(&dev));
-    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    int per_cu = 0;
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol<T, M>, CH_THREADS, shm));
-    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol does not fit a CU");
-    int64_t grid = cus;  // one per CU; tickets keep it correct when fewer are resident
-    if (grid > n_tiles) grid = n_tiles;
-    if (grid < 1) grid = 1;
-    band_chol<T, M><<<(unsigned)grid, CH_THREADS, shm, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), progress, status,
-                                                             status + 1, n_tiles, trace);
-    BSM_HIP_TRY(hipGetLastError());
-    return BSM_OK;
-}
-
-template <typename T, int M, int RW = 1>
-int launch_chol3(Band& bd, int* progress, int* status, hipStream_t s, unsigned long long* trace) {
-    const int64_t n_tiles = (bd.n + TR - 1) / TR;
-    int dev = 0, cus = 0;
-    BSM_HIP_TRY(hipGetDevice(&dev));
-    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    int per_cu = 0;
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol3<T, M, RW>, 1024 / RW, 0));
-    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol3 does not fit a CU");
-    int64_t grid = cus;  // one per CU; tickets keep it correct when fewer are resident
-    if (grid > n_tiles) grid = n_tiles;
-    if (grid < 1) grid = 1;
-    band_chol3<T, M, RW><<<(unsigned)grid, 1024 / RW, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), progress,
-                                                            status, status + 1, n_tiles, trace);
-    BSM_HIP_TRY(hipGetLastError());
-    return BSM_OK;
-}
-
-template <typename T, int M>
-int launch_chol4(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
-    const int64_t n_tiles = (bd.n + C4_TB - 1) / C4_TB;
-    int dev = 0, cus = 0;
-    BSM_HIP_TRY(hipGetDevice(&dev));
-    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    int per_cu = 0;
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol4<T, M>, C4_NT, 0));
-    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol4 does not fit a CU");
-    band_chol4_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
-    BSM_HIP_TRY(hipGetLastError());
-    int64_t grid = (int64_t)cus * per_cu;  // all resident when the chip is free; tickets keep order otherwise
-    if (grid > n_tiles) grid = n_tiles;
-    if (grid < 1) grid = 1;
-    band_chol4<T, M><<<(unsigned)grid, C4_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
-                                                     status + 1, n_tiles, trace);
-    BSM_HIP_TRY(hipGetLastError());
-    return BSM_OK;
-}
-
 template <typename T, int M, int RP>
 int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long long* trace) {
     constexpr int C5_NT = 64 * (16 / RP);
@@ -3963,7 +2027,7 @@ int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     int per_cu = 0;
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, band_chol5<T, M, RP>, C5_NT, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "band_chol5 does not fit a CU");
-    band_chol4_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
+    chol_prog_init<<<nblk(n_tiles, 256), 256, 0, s>>>(n_tiles, bd.b, fprog);
     BSM_HIP_TRY(hipGetLastError());
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > n_tiles) grid = n_tiles;
@@ -4004,105 +2068,44 @@ int band_factor(const bsm_csr* a, Band& bd, hipStream_t s) {
     BSM_TRY(band_setup<T>(a, bd, s, 64 * 17 - TR));  // accumulators per row pair lane set
     stage_mark("band_setup", s);
     if (bd.n == 0) return BSM_OK;
-    const int64_t bw = bd.b, need = bw + TR;
+    const int64_t bw = bd.b;
     const int64_t n_tiles = (bd.n + TR - 1) / TR;
     DBuf prog;
     BSM_TRY(prog.alloc((n_tiles + 1) * sizeof(int) + 16));
     BSM_HIP_TRY(hipMemsetAsync(prog.p, 0, (n_tiles + 1) * sizeof(int) + 16, s));
     int* status = prog.as<int>() + n_tiles;
-    // optional diagnostic trace: per-tile-row clocks + blocking-poll counts
+    // optional diagnostic trace (BSM_CHOL_TRACE=1): cycles per phase of the row-blocks
     DBuf trace_buf;
     const bool tracing = getenv("BSM_CHOL_TRACE") != nullptr;
     if (tracing) {
-        BSM_TRY(trace_buf.alloc((3 * TRACE_TILES + 8) * sizeof(unsigned long long)));
-        BSM_HIP_TRY(hipMemsetAsync(trace_buf.p, 0, (3 * TRACE_TILES + 8) * sizeof(unsigned long long), s));
+        BSM_TRY(trace_buf.alloc(24 * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(trace_buf.p, 0, 24 * sizeof(unsigned long long), s));
     }
     unsigned long long* tr = tracing ? trace_buf.as<unsigned long long>() : nullptr;
     int rc;
-    const char* cv = getenv("BSM_CHOL_VARIANT");
-    // band_chol3 indexes the band with 32-bit offsets
-    const bool fits32 = (int64_t)a->rows * (bw + 1) + band_pad(bw + 1) < ((int64_t)1 << 31);
-    const bool v1 = (cv && atoi(cv) == 1) || bw > 64 * 16 || !fits32;
-    // default band_chol5 (tile events, two rows per wave); BSM_CHOL_VARIANT = 4 band_chol4, 0 band_chol3, 1 band_chol (A/B)
-    const bool v4 = (!cv || atoi(cv) == 4 || atoi(cv) == 5) && bw + C4_TB - 1 <= 64 * 16;
-    // default band_chol5 (two rows per wave); BSM_CHOL_VARIANT=4: band_chol4 (A/B)
-    const bool v5 = v4 && !(cv && atoi(cv) == 4);
-    if (v5) {
-        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
-        const int64_t w4 = bw + C4_TB - 1;
-#ifdef BSM_C5_RP4  // A/B build: four rows per wave (BSM_CHOL_RPW=4), M = 16 only
-        if (w4 > 512 && getenv("BSM_CHOL_RPW") && atoi(getenv("BSM_CHOL_RPW")) == 4)
-            rc = launch_chol5<T, 16, 4>(bd, prog.as<int>(), status, s, tr);
-        else
-#endif
-        if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr);
-        else rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr);
-    } else if (v4) {
-        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
-        const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
-        if (w4 <= 64) rc = launch_chol4<T, 1>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 128) rc = launch_chol4<T, 2>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 256) rc = launch_chol4<T, 4>(bd, prog.as<int>(), status, s, tr);
-        else if (w4 <= 512) rc = launch_chol4<T, 8>(bd, prog.as<int>(), status, s, tr);
-        else rc = launch_chol4<T, 16>(bd, prog.as<int>(), status, s, tr);
-    } else if (!v1) {
-        BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));  // R[n .. n+63]: dummy store / staging targets
-        if (bw <= 64) rc = launch_chol3<T, 1>(bd, prog.as<int>(), status, s, tr);
-        else if (bw <= 128) rc = launch_chol3<T, 2>(bd, prog.as<int>(), status, s, tr);
-        else if (bw <= 256) rc = launch_chol3<T, 4>(bd, prog.as<int>(), status, s, tr);
-        else if (bw <= 512) rc = launch_chol3<T, 8>(bd, prog.as<int>(), status, s, tr);
-        else rc = launch_chol3<T, 16>(bd, prog.as<int>(), status, s, tr);
-    } else if (need <= 64) rc = launch_chol<T, 1>(bd, prog.as<int>(), status, s, tr);
-    else if (need <= 128) rc = launch_chol<T, 2>(bd, prog.as<int>(), status, s, tr);
-    else if (need <= 256) rc = launch_chol<T, 4>(bd, prog.as<int>(), status, s, tr);
-    else if (need <= 512) rc = launch_chol<T, 8>(bd, prog.as<int>(), status, s, tr);
-    else rc = launch_chol<T, 17>(bd, prog.as<int>(), status, s, tr);
+    BSM_TRY(bd.r.alloc((bd.n + 64) * sizeof(T)));
+    const int64_t w4 = bw + C4_TB - 1;  // accumulator columns: i0 - jb <= b + 15
+    if (w4 <= 64) rc = launch_chol5<T, 1, 2>(bd, prog.as<int>(), status, s, tr);
+    else if (w4 <= 128) rc = launch_chol5<T, 2, 2>(bd, prog.as<int>(), status, s, tr);
+    else if (w4 <= 256) rc = launch_chol5<T, 4, 2>(bd, prog.as<int>(), status, s, tr);
+    else if (w4 <= 512) rc = launch_chol5<T, 8, 2>(bd, prog.as<int>(), status, s, tr);
+    else if (w4 <= 1024) rc = launch_chol5<T, 16, 2>(bd, prog.as<int>(), status, s, tr);
+    else rc = launch_chol5<T, 17, 2>(bd, prog.as<int>(), status, s, tr);  // b <= 1073
     BSM_TRY(rc);
     stage_mark("cholesky", s);
-    if (tracing && v4) {
+    if (tracing) {
         std::vector<unsigned long long> h(17);
         BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
         BSM_HIP_TRY(hipStreamSynchronize(s));
         const double nb = h[15] ? (double)h[15] : 1.0, nt = h[16] ? (double)h[16] : 1.0;
         fprintf(stderr,
-                "[bsm chol4 trace] row-blocks %llu; cycles per tile (non-last): pollT %.0f stageT %.0f trsm %.0f "
+                "[bsm chol trace] row-blocks %llu; cycles per tile (non-last): pollT %.0f stageT %.0f trsm %.0f "
                 "publish %.0f pollU+stageU %.0f update %.0f; last tile: pollT %.0f stageT %.0f trsm %.0f (-%.0f) "
                 "publish %.0f diag-sums %.0f; diagonal block: barrier %.0f factor %.0f publish %.0f; per "
                 "row-block: non-last tiles %.0f\n",
                 h[15], h[0] / nt, h[1] / nt, h[2] / nt, h[3] / nt, h[4] / nt, h[5] / nt, h[6] / nb, h[7] / nb,
                 h[8] / nb, h[9] / nb, h[10] / nb, h[11] / nb, h[12] / nb, h[13] / nb, h[14] / nb,
                 (double)(h[0] + h[1] + h[2] + h[3] + h[4] + h[5]) / nb);
-    } else if (tracing) {
-        std::vector<unsigned long long> h(3 * TRACE_TILES + 8);
-        BSM_HIP_TRY(hipMemcpyAsync(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost, s));
-        BSM_HIP_TRY(hipStreamSynchronize(s));
-        const int64_t nt = n_tiles < TRACE_TILES ? n_tiles : TRACE_TILES;
-        double dur = 0, pro = 0, gap = 0;
-        int64_t cnt = 0;
-        for (int64_t I = 1; I < nt; ++I) {
-            if (!h[3 * I] || !h[3 * I + 2]) continue;
-            dur += (double)(h[3 * I + 2] - h[3 * I + 1]);
-            pro += (double)(h[3 * I + 1] - h[3 * I]);
-            gap += (double)(h[3 * I + 1]) - (double)(h[3 * (I - 1) + 1]);
-            ++cnt;
-        }
-        const double us = 0.01;  // wall_clock64 ticks at 100 MHz
-        const double steps = (double)(bd.b + TR);
-        fprintf(stderr,
-                "[bsm chol trace] tile-rows %lld (traced %lld): run %.1f us (%.3f us/step), prologue wait %.1f us, "
-                "start-to-start %.2f us (= %.1f steps); blocking polls %llu, spins %llu\n",
-                (long long)n_tiles, (long long)cnt, dur / cnt * us, dur / cnt * us / steps, pro / cnt * us,
-                gap / cnt * us, gap / cnt / (dur / cnt / steps), h[3 * TRACE_TILES], h[3 * TRACE_TILES + 1]);
-        const unsigned long long* ph = &h[3 * TRACE_TILES + 2];
-        const double nbd = (double)nt * (double)((bd.b + 3) / 4);  // boundaries traced (band_chol3)
-        if (ph[0])
-            fprintf(stderr,
-                    "[bsm chol trace] band_chol3 cycles per batch of 4 columns: steps %.0f, store+stage %.0f, "
-                    "poll %.0f, barrier %.0f, after barrier %.0f\n",
-                    ph[0] / nbd, ph[1] / nbd, ph[2] / nbd, ph[3] / nbd, ph[4] / nbd);
     }
     int st = 0;
     BSM_HIP_TRY(read_dev(&st, status, sizeof(int), s));
@@ -4408,52 +2411,23 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
     const int64_t n = bd.n, nb64 = (n + 63) / 64, DM = (63 + bd.b) / 64 + 1;
     BSM_TRY(dinv.alloc((size_t)(nb64 > 0 ? nb64 : 1) * 4096 * sizeof(T)));
     if (n == 0) return BSM_OK;
-    // BSM_BLK_CHAIN (default 0): one workgroup per diagonal tile (round 2);
-    // 1: one workgroup runs the diagonal chain with Linv in LDS, fed by
-    // pending tiles (pend: S_{K,K}, S_{K,K-1} per block column, 64 KiB each),
-    // barriers between its steps; 2: the same workgroup as a dataflow of
-    // 16 x 16 block tasks over its four waves. Measured on one box
-    // (profiles/r03_o_blk_chain_ab.log): 0 318.6 ms, 1 336.2 ms; 2 is slower
-    // still (24.4 against 21.7 us per block column, profiles/r03_j_*: each
-    // task pays ~400 cycles of flag polling and ~900 of dispatch, and the four
-    // serial 16 x 16 factors stay on the chain). All three give the same bits.
-    const char* ce = getenv("BSM_BLK_CHAIN");
-    const int chain_mode = ce ? atoi(ce) : 0;  // 0: per-tile, 1: the chain workgroup, 2: its dataflow form
-    const bool chain = chain_mode != 0;
-    // BSM_BLK_PROG (default 1, per-tile form with panels = 1 only): tile K
-    // publishes Linv_K by 16-row blocks as its factor forms them, each with a
-    // flag (rbf[4K + c], c < 3; row block 3 goes with the tile's flag), and
-    // tile K + 1 forms its sub-diagonal tile and update block by block
-    // against them; 0: the whole Linv_K after the factor (round 2 / 3 form).
-    // Same bits either way.
-    const char* pge = getenv("BSM_BLK_PROG");
-    const char* pe0 = getenv("BSM_BLK_PANELS");
-    const bool prog = !chain && (!pge || atoi(pge) != 0) && (!pe0 || atoi(pe0) == 1);
-    // BSM_BLK_PROG=2: tile K also publishes L_K's blocks (3, c < 3) with Linv's
-    // row blocks and Di[3] the moment its last pivot block is factored; tile
-    // K + 1 forms its last column block by the triangular form against Di[3]
-    // (a reassociation: not the bits of modes 0 / 1, within the tolerance)
-    const bool prog2 = prog && pge && atoi(pge) == 2;
-    DBuf pub3;
-    if (prog2) BSM_TRY(pub3.alloc((size_t)nb64 * 1024 * sizeof(T)));
-    DBuf fl, pend;
-    const size_t nfl = (size_t)(nb64 * DM + 2 + (chain ? nb64 : 0) + (prog ? 4 * nb64 : 0));
+    // flags: one per tile, the ticket, the status word, then 4 per block
+    // column for Linv's progressive row blocks (rbf)
+    DBuf fl;
+    const size_t nfl = (size_t)(nb64 * DM + 2 + 4 * nb64);
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* flags = fl.as<int>();
     int* tix = flags + nb64 * DM;
     int* st = tix + 1;
-    int* pendf = chain ? st + 1 : nullptr;
-    int* rbf = prog ? st + 1 : nullptr;  // (chain and prog exclude each other)
-    if (chain) BSM_TRY(pend.alloc((size_t)nb64 * 8192 * sizeof(T)));
+    int* rbf = st + 1;
     int dev = 0, cus = 0, per_cu = 0;
     BSM_HIP_TRY(hipGetDevice(&dev));
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    auto kern = chain_mode == 2 ? blk_chol<T, 2> : chain_mode == 1 ? blk_chol<T, 1> : blk_chol<T, 0>;
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, blk_chol<T>, 256, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_chol does not fit a CU");
     int64_t grid = (int64_t)cus * per_cu;
-    if (grid > nb64 * DM + (chain ? 1 : 0)) grid = nb64 * DM + (chain ? 1 : 0);
+    if (grid > nb64 * DM) grid = nb64 * DM;
     // BSM_BLK_DEBUG=1: watchdog counters in host memory and chain timers;
     // =2: the chain timers alone (device memory: no PCIe atomics on the chain)
     unsigned long long* hdbg = nullptr;
@@ -4468,19 +2442,8 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
         BSM_HIP_TRY(hipMemsetAsync(tdb.p, 0, 48 * sizeof(unsigned long long), s));
     }
     g_blk_phase = "blk_chol launch";
-    // BSM_BLK_PANELS: 1 (default) the diagonal tile by 16-column panels on four
-    // waves, the products on f64 MFMA (C5 0.41 s); 0 the one-wave 64-column
-    // factor, then the block inverse (0.49 s); 3 the tile as 2 x 2 blocks of 32
-    // (0.57 s); 4 the panels with two Newton steps per pivot (A/B). Tried and
-    // dropped: the 64-column inverse formed on a second
-    // wave behind the factor, meeting it every 8 columns (0.98 s: the factor
-    // waits for the inverse's long rows at the barriers).
-    const char* pe = getenv("BSM_BLK_PANELS");
-    const int panels = pe ? atoi(pe) : 1;
-    kern<<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
-                                               tdb.as<unsigned long long>(), panels, chain ? pend.as<T>() : nullptr,
-                                               pendf, chain_mode, prog ? rbf : nullptr,
-                                               prog2 ? pub3.as<T>() : nullptr);
+    blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
+                                                tdb.as<unsigned long long>(), rbf);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());
@@ -4609,63 +2572,25 @@ static int solve_general(const bsm_csr* a, uint64_t k, uint64_t n, const void* b
     return rc;
 }
 
-// band backward solve: the lane-hopping chain (band_backward_hop) for b up
-// to 64*32; the two-wave LDS chain (band_backward) beyond that or when
-// BSM_BW_VARIANT=1 (A/B).
+// band backward solve: band_backward_reg over W = band_walk_terms(b) terms
+// per row (ld >= W + 1 is set by band_setup)
 template <typename T>
 static int launch_backward(uint64_t n, uint64_t k, int64_t b, int64_t ld, const T* cb, const T* y, T* x,
                            hipStream_t s) {
-    const char* e = getenv("BSM_BW_VARIANT");
-    const bool legacy = (e && atoi(e) == 1) || b >= BH_RING || b > 64 * 32;
     const int64_t N = (int64_t)n;
-    const bool hop = e && (atoi(e) == 2 || atoi(e) == 3);  // 2: hop with 32-term segments, 3: hop
-    if (legacy)
-        band_backward<T><<<(unsigned)k, 128, 0, s>>>(N, b, ld, cb, y, x);
-    else if (!hop) {
-        // register window, unrolled walk of W = band_walk_terms(b) terms
-        // (ld >= W + 1 is set by band_factor); BSM_BW_VARIANT=4: v_readlane
-        // hops (16 x 64 only), 5: 16-term segments on 64 lanes for 512 < b <= 1024
-        const bool rl = e && atoi(e) == 4, seg16 = e && atoi(e) == 5;
-        BSM_REQUIRE(ld >= band_walk_terms(b) + 1, BSM_ERR_INVALID, "backward: band ld %lld too small",
-                    (long long)ld);
-        auto go = [&]<int SEG, int NL>() {
-            if constexpr (SEG == 16 && NL == 64) {
-                if (rl) {
-                    band_backward_reg<T, SEG, NL, false><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-                    return;
-                }
-            }
-            band_backward_reg<T, SEG, NL, true><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-        };
-        const BwCfg c = band_walk_cfg(b);
-        // BSM_BW_SEG=20|25 (A/B, 896 < b <= 1000): other segment lengths over
-        // the same W = 1000 terms in the same order
-        static const int bw_seg = getenv("BSM_BW_SEG") ? atoi(getenv("BSM_BW_SEG")) : 0;
-        if (seg16 && b > 512 && b <= 1024) go.template operator()<16, 64>();
-        else if (c.seg == 40 && bw_seg == 25) go.template operator()<25, 40>();
-        else if (c.seg == 40 && bw_seg == 20) go.template operator()<20, 50>();
-        else if (c.seg == 40) go.template operator()<40, 25>();
-        else if (c.seg == 1) go.template operator()<1, 64>();
-        else if (c.seg == 2) go.template operator()<2, 64>();
-        else if (c.seg == 4) go.template operator()<4, 64>();
-        else if (c.seg == 8) go.template operator()<8, 64>();
-        else if (c.seg == 12) go.template operator()<12, 64>();
-        else if (c.seg == 16 && c.nl == 56) go.template operator()<16, 56>();
-        else if (c.seg == 16) go.template operator()<16, 64>();
-        else go.template operator()<32, 64>();
-    } else if (b <= 64)
-        band_backward_hop<T, 1><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64 * 4)
-        band_backward_hop<T, 4><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64 * 8)
-        band_backward_hop<T, 8><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else if (b <= 64 * 16 && atoi(e) != 2)
-        // 16-term segments: at C5 (b = 1000) 4.2 s against 5.0 s with 32-term
-        // segments, whose per-row product set-up (registers spill to AGPRs)
-        // costs more than the 31 lane hops it saves (BSM_BW_VARIANT=2: A/B)
-        band_backward_hop<T, 16><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
-    else
-        band_backward_hop<T, 32><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x);
+    BSM_REQUIRE(ld >= band_walk_terms(b) + 1, BSM_ERR_INVALID, "backward: band ld %lld too small", (long long)ld);
+    auto go = [&]<int SEG, int NL>() { band_backward_reg<T, SEG, NL><<<(unsigned)k, 64, 0, s>>>(N, b, ld, cb, y, x); };
+    const BwCfg c = band_walk_cfg(b);
+    if (c.seg == 40) go.template operator()<40, 25>();
+    else if (c.seg == 1) go.template operator()<1, 64>();
+    else if (c.seg == 2) go.template operator()<2, 64>();
+    else if (c.seg == 4) go.template operator()<4, 64>();
+    else if (c.seg == 8) go.template operator()<8, 64>();
+    else if (c.seg == 12) go.template operator()<12, 64>();
+    else if (c.seg == 16 && c.nl == 56) go.template operator()<16, 56>();
+    else if (c.seg == 16) go.template operator()<16, 64>();
+    else if (c.seg == 32) go.template operator()<32, 64>();
+    else BSM_REQUIRE(false, BSM_ERR_UNSUPPORTED, "backward: band %lld too wide", (long long)b);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }
@@ -4687,14 +2612,13 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
         // the reference's forward pass divides by the LAST stored entry of
         // each L row and its backward pass by the FIRST of each L^T row: with
         // every pivot > 0 (checked) both are L_ii, as used below.
-        BSM_REQUIRE(bd.b < FW_RING - FW_BLOCK && bd.b < BW_RING, BSM_ERR_UNSUPPORTED, "band too wide");
         DBuf bc, yc, xc;
         BSM_TRY(to_colmajor(a->dtype, n, k, b_dev, bc, s));
         BSM_TRY(yc.alloc(n * k * sizeof(T)));
         BSM_TRY(xc.alloc(n * k * sizeof(T)));
         if (n && k) {
-            // forward_substitution(l, b) over rows 0..n of L (lib.rs:31-44)
-            const char* fv = getenv("BSM_FW_VARIANT");
+            // forward_substitution(l, b) over rows 0..n of L (lib.rs:31-44);
+            // BSM_FW_TRACE=1: cycles per phase
             DBuf ftr;
             unsigned long long* ftp = nullptr;
             if (getenv("BSM_FW_TRACE")) {
@@ -4702,16 +2626,8 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
                 BSM_HIP_TRY(hipMemsetAsync(ftr.p, 0, 8 * sizeof(unsigned long long), s));
                 ftp = ftr.as<unsigned long long>();
             }
-            if ((fv && atoi(fv) == 1) || bd.b + 16 * 64 + 64 > FW2_RING)
-                band_forward<T><<<(unsigned)k, FW_BLOCK, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
-                                                                 bc.as<T>(), yc.as<T>());
-            else if (fv && atoi(fv) == 2)
-                band_forward2<T, 16, 16><<<(unsigned)k, 1024, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
-                                                                      bc.as<T>(), yc.as<T>(), ftp);
-            else if (fv && atoi(fv) == 3)
-                band_forward2<T, 16, 8><<<(unsigned)k, 1024, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
-                                                                     bc.as<T>(), yc.as<T>(), ftp);
-            else if ((fv && atoi(fv) == 4) || bd.b <= FW3_NEAR || k * (1 + FW3_HELPERS) > 256)
+            // one solving workgroup per column for narrow bands (or many columns)
+            if (bd.b <= FW3_NEAR || k * (1 + FW3_HELPERS) > 256)
                 band_forward2<T, 8, 24><<<(unsigned)k, 512, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(),
                                                                     bc.as<T>(), yc.as<T>(), ftp);
             else {  // default: the far prefixes on FW3_HELPERS helper workgroups per column

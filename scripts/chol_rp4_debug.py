@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Locate the first wrong entry of an A/B band_chol5 build's factor against
-band_chol4 (BSM_CHOL_VARIANT=4), in dependency order (row-block, then column),
+the band oracle's (plain C, test infrastructure), in dependency order
+(row-block, then column),
 and print the pattern of wrong entries in that row-block: which of its 16 rows
 (and so which wave: rows RP*w .. RP*w + RP - 1), which columns (tile K =
 col // 16, slot m = (col - jb) // 64, lane = (col - jb) % 64), and the values.
@@ -8,7 +9,8 @@ col // 16, slot m = (col - jb) // 64, lane = (col - jb) % 64), and the values.
   BSM_LIB_PATH=basic_sparse_matrix_amd/lib/libbsm_hip_rp4.so \
       python scripts/chol_rp4_debug.py --g 500 --rpw 4
 
-Diagnostic only (the band_chol5 RP = 4 wrong-bits investigation, round 5).
+Diagnostic only (the band_chol5 RP = 4 wrong-bits investigation, round 5;
+the A/B build: scripts/perf/build_rp4.sh).
 """
 import argparse
 import json
@@ -23,8 +25,7 @@ from basic_sparse_matrix_amd import Csr  # noqa: E402
 from oracle import pyoracle as orc  # noqa: E402  (the input matrix only)
 
 
-def factor(A, variant, rpw=None):
-    os.environ["BSM_CHOL_VARIANT"] = variant
+def factor(A, rpw=None):
     if rpw:
         os.environ["BSM_CHOL_RPW"] = str(rpw)
     else:
@@ -46,10 +47,11 @@ def main():
     n = a.g * a.g
     rp, ci, v = orc.poisson2d(a.g)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
-    ref = factor(A, "4")
+    erp, eci, ev = orc.cholesky(n, n, rp, ci, v, band=True)
+    ref = (np.asarray(erp).astype(np.int64), np.asarray(eci).astype(np.int64), np.asarray(ev))
     b = a.g  # Poisson 2D bandwidth
     for rep in range(a.reps):
-        got = factor(A, "5", a.rpw)
+        got = factor(A, a.rpw)
         res = {"g": a.g, "rpw": a.rpw, "rep": rep, "lib": os.environ.get("BSM_LIB_PATH", "default")}
         if not (np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])):
             res["structure_differs"] = True

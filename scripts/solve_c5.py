@@ -48,9 +48,8 @@ def system(g, dt):
 
 
 def band_kernel():
-    """The reference-order factor kernel the library picks (BSM_CHOL_VARIANT)."""
-    return {"4": "band_chol4", "0": "band_chol3", "1": "band_chol"}.get(os.environ.get("BSM_CHOL_VARIANT", ""),
-                                                                      "band_chol5")
+    """The reference-order factor kernel the library runs."""
+    return "band_chol5"
 
 
 def leading_system(g, rows_g):

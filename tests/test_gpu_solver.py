@@ -103,11 +103,9 @@ def csr_arrays(dense):
     return rp, nzc.astype(np.uint64), dense[nzr, nzc]
 
 
-@pytest.mark.parametrize("chol_variant", ["0", "1", "4", "5"])  # band_chol3 / band_chol / band_chol4 / band_chol5
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("n,density", [(1, 1.0), (7, 0.5), (33, 0.2), (64, 0.05), (150, 0.1), (300, 0.02)])
-def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, chol_variant):
-    monkeypatch.setenv("BSM_CHOL_VARIANT", chol_variant)
+def test_cholesky_random_vs_literal_oracle(orc, dtype, n, density):
     rng = np.random.default_rng(n)
     a = random_spd(rng, n, density, dtype)
     rp, ci, v = csr_arrays(a)
@@ -118,10 +116,7 @@ def test_cholesky_random_vs_literal_oracle(orc, monkeypatch, dtype, n, density, 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("g", [3, 16, 40])
-@pytest.mark.parametrize("variant", ["0", "1", "3", "4", "5"])  # BSM_BW_VARIANT / BSM_FW_VARIANT A/B kernels (see kernels_solve.hip)
-def test_poisson_cholesky_and_solve_vs_oracle(orc, monkeypatch, dtype, g, variant):
-    monkeypatch.setenv("BSM_BW_VARIANT", variant)
-    monkeypatch.setenv("BSM_FW_VARIANT", variant)
+def test_poisson_cholesky_and_solve_vs_oracle(orc, dtype, g):
     n = g * g
     rp, ci, v = orc.poisson2d(g)
     v = v.astype(dtype)
@@ -159,48 +154,27 @@ def test_csr_triangular_solves_vs_oracle(orc, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("g", [5, 17, 40, 63, 100])
-def test_poisson_cholesky_variants_vs_oracle(orc, monkeypatch, dtype, g):
-    """Every Cholesky kernel (BSM_CHOL_VARIANT 0 = band_chol3, 1 = band_chol,
-    4 = band_chol4, 5 = band_chol5) gives the band oracle's factor bit for bit, including
-    bandwidths that are not a multiple of the 16-row tiles and last
-    row-blocks that are cut short."""
+@pytest.mark.parametrize("g", [5, 17, 40, 63, 100, 130, 260])
+def test_poisson_cholesky_bandwidths_vs_oracle(orc, dtype, g):
+    """band_chol5 gives the band oracle's factor bit for bit at every slot
+    count M (bandwidths 5 .. 260: M = 1, 2, 4, 8), including bandwidths that
+    are not a multiple of the 16-row tiles and last row-blocks that are cut
+    short. M = 16 is pinned by the C5 fixture (below), M = 17 by the
+    bandwidth-1060 solve."""
     n = g * g
     rp, ci, v = orc.poisson2d(g)
     v = v.astype(dtype)
     expect = orc.cholesky(n, n, rp, ci, v, band=True)
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
-    for variant in ("0", "1", "4", "5"):
-        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
-        assert_csr_exact(A.cholesky_decomp(), *expect)
-
-
-def test_poisson_500_chol4_equals_chol3_f64(monkeypatch):
-    """250,000 unknowns, bandwidth 500: band_chol3, band_chol4 and band_chol5 factors are
-    identical bit for bit (all are pinned to the oracle at smaller sizes)."""
-    from oracle import pyoracle as orc
-
-    g = 500
-    n = g * g
-    rp, ci, v = orc.poisson2d(g)
-    A = Csr.from_csr_arrays((n, n), rp, ci, v)
-    out = {}
-    for variant in ("0", "4", "5"):
-        monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
-        L = A.cholesky_decomp()
-        out[variant] = (np.asarray(L.row_index), np.asarray(L.col_index), bits(np.asarray(L.v)))
-        del L
-    for a, b, c in zip(out["0"], out["4"], out["5"]):
-        assert np.array_equal(a, b)
-        assert np.array_equal(a, c)  # band_chol5 (two rows per wave)
+    assert_csr_exact(A.cholesky_decomp(), *expect)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_forward_helper_prefixes_vs_oracle(orc, monkeypatch, dtype):
+def test_forward_helper_prefixes_vs_oracle(orc, dtype):
     """Bandwidth 200 > FW3_NEAR: the default forward solve takes the far
     prefixes of the rows' sums from helper workgroups; with 3 RHS columns
-    (three solver/helper groups) the solution equals the single-workgroup
-    kernel (BSM_FW_VARIANT=4) and the band oracle bit for bit."""
+    (three solver/helper groups) and with one the solution equals the band
+    oracle bit for bit."""
     g = 200
     n = g * g
     rp, ci, v = orc.poisson2d(g)
@@ -208,14 +182,11 @@ def test_forward_helper_prefixes_vs_oracle(orc, monkeypatch, dtype):
     A = Csr.from_csr_arrays((n, n), rp, ci, v)
     b = orc.gen_x_cols(1004, n, 3, dtype=dtype)
     ex = orc.solve(n, rp, ci, v, b, band=True)
-    got = {}
-    for fv in ("0", "4"):
-        monkeypatch.setenv("BSM_FW_VARIANT", fv)
-        x = solve(A, Dense.from_columns(b))
-        got[fv] = [bits(x.get_col(j)).tolist() for j in range(3)]
+    x = solve(A, Dense.from_columns(b))
     for j in range(3):
-        assert got["0"][j] == bits(ex[j]).tolist()
-        assert got["4"][j] == got["0"][j]
+        assert bits(x.get_col(j)).tolist() == bits(ex[j]).tolist()
+    x1 = solve(A, Dense.from_columns(b[:1]))
+    assert bits(x1.get_col(0)).tolist() == bits(ex[0]).tolist()
 
 
 def test_poisson_250_bit_exact_solve_f64(orc):
@@ -232,9 +203,9 @@ def test_poisson_250_bit_exact_solve_f64(orc):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_wide_band_solve_vs_oracle(orc, dtype):
-    """Bandwidth 1060 (> 1024: the 32-term lane segments of the backward
-    chain; band_chol takes b <= 1072) on a short banded SPD system,
-    bit-exact vs the band oracle."""
+    """Bandwidth 1060 (> 1024: band_chol5's 17th accumulator slot and the
+    32-term lane segments of the backward chain; bands up to 1073) on a
+    short banded SPD system, bit-exact vs the band oracle."""
     n, g = 2400, 1060
     rows, cols, vals = [], [], []
     for i in range(n):
@@ -352,14 +323,12 @@ def test_short_rhs_column_panics():
     assert np.asarray(got.v).tolist() == [3.0, 2.0]
 
 
-@pytest.mark.parametrize("variant", ["5", "4", "0", "1"])  # band_chol5 / band_chol4 / band_chol3 / band_chol
-def test_cholesky_finishes_beside_a_kernel_holding_cus(orc, monkeypatch, variant):
+def test_cholesky_finishes_beside_a_kernel_holding_cus(orc):
     """The persistent factor kernels take row-blocks by atomic ticket, so
     they finish (bit-exact) while other work holds part of the GPU: large f64
     GEMMs queued on a torch side stream run concurrently on the CUs."""
     import torch
 
-    monkeypatch.setenv("BSM_CHOL_VARIANT", variant)
     g = 150
     n = g * g
     rp, ci, v = orc.poisson2d(g)
