@@ -147,6 +147,7 @@ SIGNATURES = [
     ("bsm_mcsr_copy_y", _int, [_vp, _int, _vp, _vp]),
     ("bsm_mcsr_output", _int, [_vp, ctypes.POINTER(_vp)]),
     ("bsm_mcsr_compact", _int, [_vp]),
+    ("bsm_mcsr_set_output_rank", _int, [_vp, _int]),
     ("bsm_mcsr_slot_read", _int, [_vp, _int, _u32, _u32, _vp, _vp]),
     ("bsm_mcsr_slot_write", _int, [_vp, _int, _u32, _u32, _vp, _vp]),
     ("bsm_mcsr_free", None, [_vp]),

@@ -61,7 +61,7 @@ constexpr int EV_PER_STEP = 5;  // start, last SpMM end (compute), last all-gath
 struct Local {
     int device = 0, rank = 0;
     std::vector<bsm_csr*> pieces;  // round c: piece c*world + rank
-    bool compacts = false;         // the process's first device compacts the output
+    bool compacts = false;         // this device compacts the output (bsm_mcsr_set_output_rank)
     // prepared for k
     void* y = nullptr;      // P*pad x k, slot order
     int32_t* nz = nullptr;  // P*pad
@@ -91,6 +91,7 @@ struct bsm_mcsr {
     uint64_t k = 0;
     bool prepared = false, squeeze = false;
     int schedule = 0;
+    int out_rank = -1;  // -1: every process's first local device compacts; r: only rank r
     // one call at a time per matrix: the gathered Y, the output buffers, the
     // events and the collectives of a step are shared state (recursive:
     // mul_dense runs prepare, step and output under the same hold)
@@ -860,9 +861,13 @@ int bsm_mcsr_output(const bsm_mcsr* m, bsm_csr** out) {
     BSM_REQUIRE(m && out, BSM_ERR_INVALID, "bsm_mcsr_output: bad argument");
     std::lock_guard<std::recursive_mutex> hold(m->mu);
     BSM_REQUIRE(m->prepared, BSM_ERR_INVALID, "bsm_mcsr_output: prepare the matrix first");
-    const Local& L = m->loc[0];
+    int li = 0;
+    while (li < m->ctx->n_local && !m->loc[li].compacts) ++li;
+    BSM_REQUIRE(li < m->ctx->n_local, BSM_ERR_INVALID,
+                "bsm_mcsr_output: no local device compacts the output (output rank %d)", m->out_rank);
+    const Local& L = m->loc[li];
     DeviceGuard g(L.device);
-    hipStream_t s = m->ctx->compute[0];
+    hipStream_t s = m->ctx->compute[li];
     int64_t nnz = 0;
     BSM_HIP_TRY(read_dev(&nnz, L.rp_out + m->rows, sizeof(nnz), s));
     bsm_csr* r = nullptr;
@@ -915,6 +920,20 @@ int bsm_mcsr_mul_dense(bsm_mcsr* m, uint64_t k, uint64_t x_rows, const void* con
     BSM_TRY(bsm_mcsr_sync(m));
     for (auto& L : m->loc) L.steps = std::max(0, L.steps - 1);  // not a timed step
     return bsm_mcsr_output(m, out);
+}
+
+int bsm_mcsr_set_output_rank(bsm_mcsr* m, int rank) {
+    BSM_REQUIRE(m && rank >= -1 && rank < m->ctx->world, BSM_ERR_INVALID, "bsm_mcsr_set_output_rank: bad argument");
+    std::lock_guard<std::recursive_mutex> hold(m->mu);
+    m->out_rank = rank;
+    for (int i = 0; i < m->ctx->n_local; ++i) {
+        Local& L = m->loc[i];
+        L.compacts = rank < 0 ? i == 0 : L.rank == rank;
+        DeviceGuard g(L.device);
+        free_local_buffers(L);
+    }
+    m->prepared = false;
+    return BSM_OK;
 }
 
 int bsm_mcsr_compact(bsm_mcsr* m) {

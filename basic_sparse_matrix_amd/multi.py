@@ -204,6 +204,13 @@ class MultiCsr:
         local device `local` into caller device buffers (0 = skip)."""
         _lib.check(_lib.load().bsm_mcsr_copy_y(self.handle, local, y_ptr, nnz_ptr))
 
+    def set_output_rank(self, rank: int) -> None:
+        """bsm_mcsr_set_output_rank: only global rank `rank` compacts the
+        gathered Y into the output Csr (-1: every process). The other ranks
+        keep no output buffers and skip the compaction. Call before
+        prepare (it drops a prepared schedule's buffers)."""
+        _lib.check(_lib.load().bsm_mcsr_set_output_rank(self.handle, int(rank)))
+
     def compact(self) -> None:
         """bsm_mcsr_compact: the gathered Y -> the output Csr (async; after the
         slot exchange on an external context)."""

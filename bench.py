@@ -539,6 +539,10 @@ def main():
         ctx.broadcast([x.data_ptr()], x.numel() * es, root=0)  # X replicated over RCCL (untimed setup)
     log(f"rank {rank}: pieces {my_pieces} of {m.pieces} ({chunks} round(s)), nnz {nnz_total:,} in total, generated in "
         f"{gen_ms:.0f} ms; RCCL context {comm_init_ms:.0f} ms")
+    # the output Csr is returned on rank 0 (Csr::mul_dense has one caller):
+    # the other ranks keep the gathered Y only, no output buffers, no compaction
+    if world > 1:
+        m.set_output_rank(0)
     # the schedule's per-matrix preparation (outside the timed region, like the
     # matrix itself; reported per phase as plan_ms)
     plan = m.prepare(k, args.schedule)

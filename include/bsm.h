@@ -362,8 +362,17 @@ void bsm_mcsr_reset_times(bsm_mcsr* m);
  * nonzero counts on local device i, copied into caller device buffers
  * (either may be NULL); synchronous. */
 int bsm_mcsr_copy_y(const bsm_mcsr* m, int local, void* y, int32_t* row_nnz);
-/* The last step's output Csr as a new handle on the first local device. */
+/* The last step's output Csr as a new handle on the local device that
+ * compacts it (the first local device, or the output rank's: below). */
 int bsm_mcsr_output(const bsm_mcsr* m, bsm_csr** out);
+/* Which global rank compacts the gathered Y into the output Csr: -1 (the
+ * default) every process (its first local device), r >= 0 only rank r. The
+ * other ranks then allocate no output buffers (rows x k x (4 + sizeof(T)) B,
+ * 3.84 GB per rank at C4) and skip the compaction; bsm_mcsr_output there
+ * returns BSM_ERR_INVALID. Drops a prepared schedule's buffers (call before
+ * bsm_mcsr_prepare). Reference: Csr::mul_dense returns one Csr to its one
+ * caller (src/sparse.rs:426-446); the row split is this build's. */
+int bsm_mcsr_set_output_rank(bsm_mcsr* m, int rank);
 /* The compaction of the gathered Y into the output Csr (asynchronous, on the
  * compute stream; bsm_mcsr_step does it itself on a context with a
  * communicator). For an external context, after the slot exchange. */

@@ -17,6 +17,8 @@ bit for bit against the single-GPU bsm_csr_mul_dense and the CPU oracle
 JSON.
 
 argv: out_json mode(upload|generate) rows n_cols kind a b k chunks schedule(auto|tiled|panel) dtype(f64|f32|i32)
+env DIST_OUTPUT_RANK=r: only rank r compacts and returns the output Csr
+(bsm_mcsr_set_output_rank); the other ranks must refuse bsm_mcsr_output.
 """
 
 import hashlib
@@ -82,26 +84,41 @@ def main():
     bd = m.bounds().astype(np.int64)
     res["squeeze"] = bool(np.any(np.diff(bd)[:-1] != m.piece_rows))
     res["empty_pieces"] = int(np.sum(np.diff(bd) == 0))
+    out_rank = int(os.environ.get("DIST_OUTPUT_RANK", "-1"))
+    if out_rank >= 0:
+        m.set_output_rank(out_rank)
     m.prepare(k, schedule)
     res["plan"] = m.plan_info()
+    root = out_rank if out_rank >= 0 else 0
     torch.cuda.synchronize()
     outs = []
+    holds_output = out_rank < 0 or rank == out_rank
     for it in range(2):  # a second step over the slots of the first exchange
         m.step([x.data_ptr()])
         m.sync()
         exchange_slots(m, world, rank, chunks)
         m.compact()
         m.sync()
-        outs.append(m.output().download())
-    got = outs[-1]
-    res["steps_equal"] = same_csr(outs[0], got)
-    h = hashlib.sha256()
-    for arr in got:
-        h.update(np.ascontiguousarray(arr).tobytes())
+        if holds_output:
+            outs.append(m.output().download())
+    if holds_output:
+        got = outs[-1]
+        res["steps_equal"] = same_csr(outs[0], got)
+        h = hashlib.sha256()
+        for arr in got:
+            h.update(np.ascontiguousarray(arr).tobytes())
+        digest = h.hexdigest()
+    else:  # no output here: bsm_mcsr_output must refuse
+        try:
+            m.output()
+            res["steps_equal"] = False
+        except _lib.BsmError:
+            res["steps_equal"] = True
+        digest = None
     digests = [None] * world
-    dist.all_gather_object(digests, h.hexdigest())
-    res["ranks_agree"] = len(set(digests)) == 1
-    if rank == 0:
+    dist.all_gather_object(digests, digest)
+    res["ranks_agree"] = len({d for d in digests if d is not None}) == 1 and (out_rank < 0 or digests.count(None) == world - 1)
+    if rank == root:
         if mode == "upload":
             want = orc.mul_dense(rows, n_cols, rp, ci, v, x_cols)
             res["oracle_equal"] = same_csr(got, want)

@@ -127,6 +127,18 @@ def test_external_ranks_generate_schedules(tmp_path, world, rows, n_cols, kind, 
             assert r["plan"]["tiled_pieces"] == 0, r
 
 
+@pytest.mark.parametrize("world,out_rank", [(3, 0), (8, 5)])
+def test_external_ranks_single_output_rank(tmp_path, world, out_rank):
+    """bsm_mcsr_set_output_rank: only one rank compacts the gathered Y and
+    returns the output Csr (the other ranks hold no output buffers and refuse
+    bsm_mcsr_output); that Csr is the single-GPU one and the oracle's."""
+    res = _run(tmp_path, world, ["upload", 3000, 2000, 1, 0, 40, 32, 2, "auto", "f64"],
+               {"DIST_OUTPUT_RANK": str(out_rank)}, timeout=100 if world < 8 else 240)
+    assert all(r["ranks_agree"] and r["steps_equal"] for r in res), res
+    r = res[out_rank]
+    assert r["oracle_equal"] and r["single_equal"], r
+
+
 @pytest.mark.parametrize("config,chunks,world", [("c3", 1, 2), ("c3", 3, 2), ("c3", 1, 8), ("c3", 2, 8)])
 def test_bench_ranks_one_gpu_gloo_exchange(config, chunks, world):
     """bench.py's N > 1 path (the rank's pieces, my_rows, the barriers, the
