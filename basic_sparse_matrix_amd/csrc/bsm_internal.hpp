@@ -200,15 +200,12 @@ struct bsm_tiled {
     uint32_t stage = 4;          // k = 1: chunks per pipeline stage
     uint64_t rows = 0, n_cols = 0, nnz = 0;
     uint32_t nw = 0, rpw = 0, nb = 0, rw = 0, pshift = 0;
-    uint32_t half = 0;           // k = 32: two half-width passes: 1 = 8-B lanes (spmm_tiled_k32h), 2 / 3 = 16-B lanes
-                                 // (spmm_tiled_k32h16, 8 / 4 waves per CU)
     uint64_t chunks = 0;         // total, without the over-read padding
     int64_t* offs = nullptr;     // nw*nb + 1 chunk offsets
     void* meta = nullptr;        // (chunks + overread) * 64 meta words (col << 8 | row, or col << 11 | row at k = 1)
     uint32_t meta_bytes = 4;     // 8: k = 32 on 2^24 columns or more
     void* val = nullptr;         // (chunks + overread) * 64 values of dtype
     unsigned* bar = nullptr;     // batch arrival counters of the SpMM (one launch at a time per copy)
-    void* xsplit = nullptr;      // half >= 2: X re-laid as two half tables [2][n_cols][16] (n_cols * 256 B)
 };
 
 // Device-resident finalised Csr<T>.

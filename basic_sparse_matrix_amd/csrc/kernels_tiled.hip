@@ -253,43 +253,16 @@ __device__ __forceinline__ void madd(vec2_t<T>& y, const vec2_t<T>& x, const Idx
     y = make_v2(add_rn(lo_of(y), mul_rn(v, lo_of(x))), add_rn(hi_of(y), mul_rn(v, hi_of(x))));
 }
 // the chunk's rows are distinct (dummies all hit the scratch row), so its
-// 16 read-add-write updates are independent: done in parts of SUM_PART
-// entries (LDS reads, multiply-adds, writes). With all 16 at once (64 VGPRs
-// of Y rows for f64) the allocator parked gathered rows in AGPRs and waited
-// for every outstanding load at the loop's back edge (vmcnt(0) once per
-// PHASES chunks); parts of 8 keep the pipeline (vmcnt >= 21 in the loop).
-#ifndef BSM_SUM_PART
-#define BSM_SUM_PART 16
-#endif
-constexpr int SUM_PART = BSM_SUM_PART;
-static_assert(16 % SUM_PART == 0, "SUM_PART divides the chunk");
-template <int B, typename T, typename M, int... I>
-__device__ __forceinline__ void sum_part(const vec2_t<T> (&x)[16], const Idx<T, M>& c, vec2_t<T>* yw, int q,
-                                         std::integer_sequence<int, I...>) {
-    vec2_t<T> y[sizeof...(I)];
-    ((y[I] = *yaddr<B + I>(c, yw, q)), ...);
-    (madd<B + I>(y[I], x[B + I], c), ...);
-    ((*yaddr<B + I>(c, yw, q) = y[I]), ...);
-}
-template <typename T, typename M, int... P>
+// 16 read-add-write updates are independent: all 16 LDS reads, then the
+// multiply-adds, then the writes (split into parts of 8 or 4 they measured
+// 33 % slower at C4: round 4)
+template <typename T, typename M, int... I>
 __device__ __forceinline__ void sum_chunk(const vec2_t<T> (&x)[16], const Idx<T, M>& c, vec2_t<T>* yw, int q,
-                                          std::integer_sequence<int, P...>) {
-    (sum_part<P * SUM_PART>(x, c, yw, q, std::make_integer_sequence<int, SUM_PART>{}), ...);
-}
-
-// BSM_TILED_LDSADD=1 (A/B): the chunk's Y update as LDS atomic adds of the
-// rounded products (ds_add_f64: y + RN(v*x), the same two roundings), no
-// read-back of the rows into registers
-template <int I>
-__device__ __forceinline__ void madd_lds(double2* yp, const double2& x, const Idx<double>& c) {
-    const double v = bv<I>(c);
-    __hip_atomic_fetch_add(&yp->x, __dmul_rn(v, x.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(&yp->y, __dmul_rn(v, x.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <int... I>
-__device__ __forceinline__ void sum_chunk_lds(const double2 (&x)[16], const Idx<double>& c, double2* yw, int q,
-                                              std::integer_sequence<int, I...>) {
-    (madd_lds<I>(yaddr<I>(c, yw, q), x[I], c), ...);
+                                          std::integer_sequence<int, I...>) {
+    vec2_t<T> y[sizeof...(I)];
+    ((y[I] = *yaddr<I>(c, yw, q)), ...);
+    (madd<I>(y[I], x[I], c), ...);
+    ((*yaddr<I>(c, yw, q) = y[I]), ...);
 }
 
 // Batch pacing. Within a batch the layout keeps the waves on the same
@@ -319,7 +292,7 @@ __device__ __forceinline__ bool batch_wait(unsigned* bar, uint32_t target, int l
     return false;  // not all resident: stop pacing
 }
 
-template <bool PROBE, bool ATOM, typename T, typename M>
+template <bool PROBE, typename T, typename M>
 __device__ __forceinline__ void spmm_tiled_k32_body(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const M* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
@@ -359,8 +332,7 @@ __device__ __forceinline__ void spmm_tiled_k32_body(
                     load_idx(MI[(k + 4) % 6], meta, val, i + k + 4, lane);
                     gather<PROBE>(XS[(k + 2) % 3], MI[(k + 2) % 6], X, q, xmask, SEQ);
                     __builtin_amdgcn_sched_barrier(0);  // this phase's loads stay ahead of its sums
-                    if constexpr (ATOM) sum_chunk_lds(XS[k % 3], MI[k], yw, q, SEQ);
-                    else sum_chunk<T>(XS[k % 3], MI[k], yw, q, std::make_integer_sequence<int, 16 / SUM_PART>{});
+                    sum_chunk<T>(XS[k % 3], MI[k], yw, q, SEQ);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -380,12 +352,12 @@ __device__ __forceinline__ void spmm_tiled_k32_body(
 
 // f64: the whole 512-register budget of one wave per SIMD (LDS allows one
 // workgroup per CU anyway); the gathers two chunks ahead take 192 of it.
-template <bool PROBE, bool ATOM, typename T = double, typename M = uint32_t>
+template <bool PROBE, typename T = double, typename M = uint32_t>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void spmm_tiled_k32(
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const M* __restrict__ meta, const T* __restrict__ val, const vec2_t<T>* __restrict__ X,
     vec2_t<T>* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
-    spmm_tiled_k32_body<PROBE, ATOM, T, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
+    spmm_tiled_k32_body<PROBE, T, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
 }
 // f32 (F2 words, see Vec2<float>)
 template <typename M = uint32_t>
@@ -393,226 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
     const M* __restrict__ meta, const float* __restrict__ val, const F2* __restrict__ X, F2* __restrict__ Y,
     int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t xmask, uint32_t spins) {
-    spmm_tiled_k32_body<false, false, float, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
-}
-
-// ---------------------------------------------------------------------------
-// k = 32 in two half-width passes (BSM_TILED_HALF=1, round 3 A/B). The L2
-// misses of spmm_tiled_k32 are one X sweep per batch and XCD (1.3 TB at C4):
-// an XCD holds only the ~20k Y rows that fit its LDS. Here a Y row in LDS is
-// half a row (16 doubles, 128 B), so eight waves per CU hold twice the rows
-// and every X panel fetched into L2 serves twice the gathers; each batch is
-// swept twice (columns 0-15, then 16-31), so the stream is read twice and
-// each gather moves one 128-B line. Same copy, same chunks, same per-element
-// order: bit-identical to spmm_tiled_k32. Lane 16g+q gathers X[col][16h+q]
-// (8 B) for entry (u, g) of the chunk.
-// ---------------------------------------------------------------------------
-constexpr uint32_t HALF_WAVES_PER_CU = 8;
-constexpr uint32_t HALF_RW_MAX = 155;  // 8 waves x (RW+1) rows x 128 B <= 160 KiB of LDS
-
-template <int... I>
-__device__ __forceinline__ void gather_h(double (&x)[16], const Idx<double>& c, const double* __restrict__ Xh, int q,
-                                         std::integer_sequence<int, I...>) {
-    ((x[I] = Xh[(int64_t)(bm<I>(c) >> 8) * 32 + q]), ...);
-}
-template <int I>
-__device__ __forceinline__ void madd_h(double& y, double x, const Idx<double>& c) {
-    y = __dadd_rn(y, __dmul_rn(bv<I>(c), x));
-}
-template <int... I>
-__device__ __forceinline__ void sum_chunk_h(const double (&x)[16], const Idx<double>& c, double* yw, int q,
-                                            std::integer_sequence<int, I...>) {
-    double y[16];
-    ((y[I] = yw[(bm<I>(c) & 255u) * 16 + q]), ...);
-    (madd_h<I>(y[I], x[I], c), ...);
-    ((yw[(bm<I>(c) & 255u) * 16 + q] = y[I]), ...);
-}
-
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void spmm_tiled_k32h(
-    uint64_t rows, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
-    const uint32_t* __restrict__ meta, const double* __restrict__ val, const double* __restrict__ X,
-    double* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar) {
-    extern __shared__ double yhlds[];
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wave = threadIdx.x / WAVE;
-    const int g = lane >> 4, q = lane & 15;
-    double* yw = yhlds + (size_t)wave * (rw + 1) * 16;
-    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
-    const uint64_t w0 = gw * rpw;
-    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
-    const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
-    constexpr auto SEQ = std::make_integer_sequence<int, 16>{};
-    bool sync = bar != nullptr;
-    for (uint32_t st = 0; st < 2 * nb; ++st) {  // step = (batch, half)
-        const uint32_t b = st >> 1, h = st & 1;
-        const uint64_t r0 = w0 + (uint64_t)b * rw;
-        if (r0 >= wend) {
-            if (sync) batch_arrive(bar, 2 * nb - st, lane);
-            break;
-        }
-        if (sync && st > 0) sync = batch_wait(bar, waves * st, lane);
-        const int nr = (int)min<uint64_t>(rw, wend - r0);
-        for (int r = g; r < nr; r += 4) yw[r * 16 + q] = 0.0;
-        const double* Xh = X + 16 * h;
-        const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
-        if (c1 > c0) {  // (c1 - c0) % PHASES == 0
-            Idx<double> M[6];
-            double XS[3][16];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
-            gather_h(XS[0], M[0], Xh, q, SEQ);
-            gather_h(XS[1], M[1], Xh, q, SEQ);
-            for (int64_t i = c0; i < c1; i += PHASES) {
-#pragma unroll
-                for (int k = 0; k < PHASES; ++k) {
-                    load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
-                    gather_h(XS[(k + 2) % 3], M[(k + 2) % 6], Xh, q, SEQ);
-                    __builtin_amdgcn_sched_barrier(0);
-                    sum_chunk_h(XS[k % 3], M[k], yw, q, SEQ);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-        for (int rb = 0; rb < nr; rb += 4) {  // Y half rows; nonzero counts over both halves
-            const int r = rb + g;
-            const bool live = r < nr;
-            const double y = live ? yw[r * 16 + q] : 0.0;
-            if (live) Y[(r0 + r) * 32 + 16 * h + q] = y;
-            const uint64_t m = __ballot(y != 0.0);
-            if (live && q == 0 && row_nnz) {
-                const int n = __popcll((m >> (16 * g)) & 0xffffull);
-                row_nnz[r0 + r] = h ? row_nnz[r0 + r] + n : n;  // the same lane wrote the first half
-            }
-        }
-        if (sync) batch_arrive(bar, 1, lane);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k = 32 in two half-width passes with 16-B lanes (BSM_TILED_HALF=2, round 5).
-// spmm_tiled_k32h above gathers a half row (128 B) as 16 lanes x 8 B: the
-// same 16 wave-instructions per chunk move half the bytes and it ran at 285
-// against 180 ms. Here a half row is 8 lanes x 16 B (one 128-B line), so a
-// gather instruction moves 8 half rows = 1 KiB as in spmm_tiled_k32, and a
-// chunk takes 8 of them per half: the instruction count per byte is
-// spmm_tiled_k32's while an XCD holds twice the Y rows (8 waves x 155 rows x
-// 128 B of LDS per CU), which halves the L2 fills per X sweep (one fill
-// serves ~4 gathers instead of ~2).
-// Step u of a chunk gives 8-lane group g = 2r + s (lanes 16r + 8s .. + 7) the
-// entry loaded by lane 16r + 2u + s: two DPP row broadcasts, one per bank
-// pair (bank_mask 0x3: lanes 0-7 of each row, 0xc: lanes 8-15). Any
-// bijection of a chunk's 64 entries onto (step, group) keeps the per-row
-// order, since a chunk holds at most one entry of a row: bit-identical to
-// spmm_tiled_k32.
-// ---------------------------------------------------------------------------
-// (the first move of each pair leaves lanes 8-15 undefined: mov_dpp, no
-// initialising move; the second writes them)
-template <int U>
-__device__ __forceinline__ uint32_t bm8(uint32_t mi) {
-    const int a = __builtin_amdgcn_mov_dpp((int)mi, 0x150 + 2 * U, 0xf, 0x3, false);
-    return (uint32_t)__builtin_amdgcn_update_dpp(a, (int)mi, 0x150 + 2 * U + 1, 0xf, 0xc, false);
-}
-template <int U>
-__device__ __forceinline__ double bv8(double vi) {
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(vi), 0x150 + 2 * U, 0xf, 0x3, false);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(vi), 0x150 + 2 * U, 0xf, 0x3, false);
-    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, __double2hiint(vi), 0x150 + 2 * U + 1, 0xf, 0xc, false),
-                            __builtin_amdgcn_update_dpp(lo, __double2loint(vi), 0x150 + 2 * U + 1, 0xf, 0xc, false));
-}
-// Xh: one half table, row c's 16 doubles (128 B, one line) at Xh + 8 c
-template <int... U>
-__device__ __forceinline__ void gather_h16(double2 (&x)[8], const Idx<double>& c, const double2* __restrict__ Xh,
-                                           int j, std::integer_sequence<int, U...>) {
-    ((x[U] = Xh[(int64_t)(bm8<U>(c.mi) >> 8) * 8 + j]), ...);
-}
-// X (n_cols x 32, row-major) -> two half tables Xs[h][c][0..15] = X[c][16h ..
-// 16h + 15]. Gathering half rows straight from X touches every other 128-B
-// line at a 256-B stride, and the L2 hit rate did not rise with the doubled
-// Y rows (0.545 against 0.50 at C4, PMC round 5): with the halves
-// contiguous a pass's lines are dense in memory.
-__global__ __launch_bounds__(256) void x_split_halves(uint64_t n_cols, const double2* __restrict__ X,
-                                                      double2* __restrict__ Xs) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // 16 B of X
-    if (i >= n_cols * 16) return;
-    const uint64_t c = i >> 4, q = i & 15;
-    Xs[(q >> 3) * n_cols * 8 + c * 8 + (q & 7)] = X[i];
-}
-template <int U>
-__device__ __forceinline__ void madd_h16(double2& y, const double2& x, const Idx<double>& c) {
-    const double v = bv8<U>(c.vi);
-    y = make_double2(__dadd_rn(y.x, __dmul_rn(v, x.x)), __dadd_rn(y.y, __dmul_rn(v, x.y)));
-}
-template <int... U>
-__device__ __forceinline__ void sum_chunk_h16(const double2 (&x)[8], const Idx<double>& c, double2* yw, int j,
-                                              std::integer_sequence<int, U...>) {
-    double2 y[8];
-    ((y[U] = yw[(bm8<U>(c.mi) & 255u) * 8 + j]), ...);
-    (madd_h16<U>(y[U], x[U], c), ...);
-    ((yw[(bm8<U>(c.mi) & 255u) * 8 + j] = y[U]), ...);
-}
-
-// NW waves per CU: 8 (155 rows each, two waves per SIMD) or 4 (255 rows
-// each, the 8-bit row field's limit; one wave per SIMD, the whole register file)
-template <int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void spmm_tiled_k32h16(
-    uint64_t rows, uint64_t n_cols, uint32_t rpw, uint32_t nb, uint32_t rw, const int64_t* __restrict__ offs,
-    const uint32_t* __restrict__ meta, const double* __restrict__ val, const double2* __restrict__ X,
-    double2* __restrict__ Y, int32_t* __restrict__ row_nnz, unsigned* bar, uint32_t spins) {
-    extern __shared__ __align__(16) unsigned char yh16_raw[];
-    double2* const yh16 = reinterpret_cast<double2*>(yh16_raw);
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wave = threadIdx.x / WAVE;
-    const int g = lane >> 3, j = lane & 7;  // 8-lane group, lane in group
-    double2* yw = yh16 + (size_t)wave * (rw + 1) * 8;
-    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
-    const uint64_t w0 = gw * rpw;
-    const uint64_t wend = min<uint64_t>(rows, w0 + rpw);
-    const uint32_t waves = gridDim.x * (blockDim.x / WAVE);
-    constexpr auto SEQ = std::make_integer_sequence<int, 8>{};
-    bool sync = bar != nullptr;
-    for (uint32_t st = 0; st < 2 * nb; ++st) {  // step = (batch, half)
-        const uint32_t b = st >> 1, h = st & 1;
-        const uint64_t r0 = w0 + (uint64_t)b * rw;
-        if (r0 >= wend) {
-            if (sync) batch_arrive(bar, 2 * nb - st, lane);
-            break;
-        }
-        if (sync && st > 0) sync = batch_wait(bar, waves * st, lane, spins);
-        const int nr = (int)min<uint64_t>(rw, wend - r0);
-        for (int r = g; r < nr; r += 8) yw[r * 8 + j] = make_double2(0.0, 0.0);
-        const double2* Xh = X + h * n_cols * 8;
-        const int64_t c0 = offs[gw * nb + b], c1 = offs[gw * nb + b + 1];
-        if (c1 > c0) {  // (c1 - c0) % PHASES == 0
-            Idx<double> M[6];
-            double2 XS[3][8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) load_idx(M[k], meta, val, c0 + k, lane);
-            gather_h16(XS[0], M[0], Xh, j, SEQ);
-            gather_h16(XS[1], M[1], Xh, j, SEQ);
-            for (int64_t i = c0; i < c1; i += PHASES) {
-#pragma unroll
-                for (int k = 0; k < PHASES; ++k) {
-                    load_idx(M[(k + 4) % 6], meta, val, i + k + 4, lane);
-                    gather_h16(XS[(k + 2) % 3], M[(k + 2) % 6], Xh, j, SEQ);
-                    __builtin_amdgcn_sched_barrier(0);
-                    sum_chunk_h16(XS[k % 3], M[k], yw, j, SEQ);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-        for (int rb = 0; rb < nr; rb += 8) {  // Y half rows; nonzero counts over both halves
-            const int r = rb + g;
-            const bool live = r < nr;
-            const double2 y = live ? yw[r * 8 + j] : make_double2(0.0, 0.0);
-            if (live) Y[(r0 + r) * 16 + 8 * h + j] = y;
-            const uint64_t m0 = __ballot(y.x != 0.0), m1 = __ballot(y.y != 0.0);
-            if (live && j == 0 && row_nnz) {
-                const int n = __popcll((m0 >> (8 * g)) & 0xffull) + __popcll((m1 >> (8 * g)) & 0xffull);
-                row_nnz[r0 + r] = h ? row_nnz[r0 + r] + n : n;  // the same lane wrote the first half
-            }
-        }
-        if (sync) batch_arrive(bar, 1, lane);
-    }
+    spmm_tiled_k32_body<false, float, M>(rows, rpw, nb, rw, offs, meta, val, X, Y, row_nnz, bar, xmask, spins);
 }
 
 // ---------------------------------------------------------------------------
@@ -784,17 +537,12 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
             (void)hipGetLastError();
         }
     }
-    // k = 32: BSM_TILED_HALF=1 / 2 selects the two half-width passes (8 waves per CU) with
-    // 8-B / 16-B lanes (spmm_tiled_k32h / spmm_tiled_k32h16)
-    // (3: spmm_tiled_k32h16 with 4 waves per CU of 255 rows each)
-    const uint32_t half_env = env_u32("BSM_TILED_HALF", 0);
-    const uint32_t half = k == 32 && !f32 && !wide && half_env >= 1 && half_env <= 3 ? half_env : 0u;
-    const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : (half == 1 || half == 2 ? HALF_WAVES_PER_CU : 4u);
+    const uint32_t wpc = k == 1 ? K1_WAVES_PER_CU : 4u;
     const uint32_t nw_env = env_u32("BSM_TILED_WAVES", wpc * (uint32_t)cus);
-    const uint32_t nw = half ? (nw_env + wpc - 1) / wpc * wpc : nw_env;  // whole workgroups
+    const uint32_t nw = nw_env;
     const uint32_t k1_stage = env_u32("BSM_TILED_K1_STAGE", K1_STAGE_DEFAULT) == 8 ? 8u : 4u;
     const uint32_t rw_cap =
-        k == 1 ? K1_RW_MAX : (half == 3 ? RW_MAX_F32 : (half ? HALF_RW_MAX : (f32 ? RW_MAX_F32 : RW_MAX)));
+        k == 1 ? K1_RW_MAX : (f32 ? RW_MAX_F32 : RW_MAX);
     uint32_t rw_max = env_u32("BSM_TILED_RW", rw_cap);
     rw_max = rw_max < 8u ? 8u : (rw_max > rw_cap ? rw_cap : rw_max);
     const uint32_t pshift = env_u32("BSM_TILED_PSHIFT", k == 1 ? K1_PSHIFT : PSHIFT);
@@ -888,7 +636,6 @@ int tiled_create(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const 
     t->nb = nb;
     t->rw = rw;
     t->pshift = pshift;
-    t->half = half;
     t->chunks = (uint64_t)total;
     t->overread = overread;
     t->stage = k1_stage;
@@ -906,7 +653,7 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
     BSM_REQUIRE(!neg_init || t->k == 1, BSM_ERR_INVALID, "tiled: -0 init only for k = 1");
     if (t->rows == 0) return BSM_OK;
     unsigned* bar = nullptr;
-    if (t->bar && (t->nb > 1 || t->half) && env_u32("BSM_TILED_SYNC", 1)) {
+    if (t->bar && t->nb > 1 && env_u32("BSM_TILED_SYNC", 1)) {
         BSM_HIP_TRY(hipMemsetAsync(t->bar, 0, 8 * BAR_STRIDE * sizeof(unsigned), s));
         bar = t->bar;
     }
@@ -942,33 +689,15 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
                 t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint32_t*>(t->meta),
                 static_cast<const float*>(t->val), static_cast<const F2*>(x), static_cast<F2*>(y), row_nnz,
                 bar, 0xffffffffu, spins);
-    } else if (t->half >= 2) {
-        const uint32_t wpc = t->half == 2 ? HALF_WAVES_PER_CU : 4u;
-        const size_t lds = (size_t)wpc * (t->rw + 1) * 128;
-        static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
-        auto kern = t->half == 2 ? spmm_tiled_k32h16<8> : spmm_tiled_k32h16<4>;
-        if (!t->xsplit) BSM_HIP_TRY(hipMalloc(&const_cast<bsm_tiled*>(t)->xsplit, t->n_cols * 256));
-        x_split_halves<<<dim3((unsigned)((t->n_cols * 16 + 255) / 256)), 256, 0, s>>>(
-            t->n_cols, static_cast<const double2*>(x), static_cast<double2*>(t->xsplit));
-        kern<<<dim3(t->nw / wpc), 64 * wpc, lds, s>>>(
-            t->rows, t->n_cols, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint32_t*>(t->meta),
-            static_cast<const double*>(t->val), static_cast<const double2*>(t->xsplit), static_cast<double2*>(y),
-            row_nnz, bar, spins);
-    } else if (t->half) {
-        const size_t lds = (size_t)HALF_WAVES_PER_CU * (t->rw + 1) * 128;
-        spmm_tiled_k32h<<<dim3(t->nw / HALF_WAVES_PER_CU), 64 * HALF_WAVES_PER_CU, lds, s>>>(
-            t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint32_t*>(t->meta),
-            static_cast<const double*>(t->val), static_cast<const double*>(x), static_cast<double*>(y), row_nnz, bar);
     } else {
         const size_t lds = (size_t)4 * (t->rw + 1) * 256;
         // BSM_TILED_PROBE_MASK=<mask> (measurement only, wrong results): see gather()
         static const uint32_t xmask = env_u32("BSM_TILED_PROBE_MASK", 0xffffffffu);
-        static const bool atom = env_u32("BSM_TILED_LDSADD", 0) == 1;
-        auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true, false>
-                                         : (atom ? spmm_tiled_k32<false, true> : spmm_tiled_k32<false, false>);
+        auto kern = xmask != 0xffffffffu ? spmm_tiled_k32<true>
+                                         : spmm_tiled_k32<false>;
         static const uint32_t spins = env_u32("BSM_TILED_SPINS", 4000);
         if (t->meta_bytes == 8)  // 2^24 columns or more
-            spmm_tiled_k32<false, false, double, uint64_t><<<dim3(t->nw / 4), 256, lds, s>>>(
+            spmm_tiled_k32<false, double, uint64_t><<<dim3(t->nw / 4), 256, lds, s>>>(
                 t->rows, t->rpw, t->nb, t->rw, t->offs, static_cast<const uint64_t*>(t->meta),
                 static_cast<const double*>(t->val), static_cast<const double2*>(x), static_cast<double2*>(y), row_nnz,
                 bar, 0xffffffffu, spins);
@@ -988,7 +717,6 @@ void tiled_destroy(bsm_tiled* t) {
     if (t->meta) (void)hipFree(t->meta);
     if (t->val) (void)hipFree(t->val);
     if (t->bar) (void)hipFree(t->bar);
-    if (t->xsplit) (void)hipFree(t->xsplit);
     delete t;
 }
 

@@ -62,14 +62,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # faster than the L2 serves them.
 L2_GATHER_PEAK_GBS = 17_030.0  # 17.03 TB/s: "mode 2 ... 8191" line (0.987 ms for 6.57e7 entries)
 L2_GATHER_PEAK_SRC = "profiles/r03_gather_ceiling.log"
-# The Infinity-Cache-served rate of uniformly random 256-B X-row gathers (no
-# L2 re-use): the tiled loop at C4 with one panel (BSM_TILED_PSHIFT=24) and
-# every column folded into a 256 MB table (BSM_TILED_PROBE_MASK=2^20-1):
-# 2.56 TB in 358 ms (a 1 GB table: 357 ms, the same). C3's X is 256 MB and a
-# row meets ~0.2 other entries of its X rows per L2 lifetime, so its row kernel
-# is bound by this rate, not by the L2's.
-IC_GATHER_PEAK_GBS = 7_150.0
-IC_GATHER_PEAK_SRC = "profiles/r04_b_c4_ic_gather_probe.log"
+# The Infinity-Cache service rate of L2 misses. Every byte a kernel misses
+# in L2 (its PMC traffic: X rows it gathers past L2, the index/value stream,
+# the writes) is served by the Infinity Cache or HBM. The ceiling is the
+# fastest Infinity-Cache-served gather rate measured on this chip:
+# MI355X_MICROARCH.md §Indexed rows, 38 MB table of uniformly random rows,
+# 8.6 TB/s. Our own probe (the tiled loop at C4 with one panel and every
+# column folded into a 256 MB table: BSM_TILED_PSHIFT=24,
+# BSM_TILED_PROBE_MASK=2^20-1) moved 2.68 TB of L2-miss bytes (2.56 TB of
+# gathers + the 124 GB stream) in 358 ms: 7.50 TB/s (a 1 GB table: the same);
+# roofline_gather reports the kernel's fraction of that too.
+IC_SERVICE_PEAK_GBS = 8_600.0
+IC_SERVICE_PEAK_SRC = "MI355X_MICROARCH.md §Indexed rows (38 MB table, Infinity Cache)"
+IC_PROBE_GBS = 7_500.0
+IC_PROBE_SRC = "profiles/r04_b_c4_ic_gather_probe.log"
 # k = 1 (C2, spmm_tiled_k1): the same kernel with every gather confined to one
 # L2-resident 2 MiB panel (BSM_TILED_K1_PROBE=262143): 59 us at C2, i.e. C2's
 # B_gather (216,000,008 B) at 3,661 GB/s. Each 8-B gather moves a 128-B line
@@ -92,20 +98,35 @@ def b_gather(rows, nnz, k, es=8):
     return 8 * (rows + 1) + (4 + es) * nnz + es * nnz * k + es * rows * k
 
 
-def gather_ceiling(tiled, k, x_bytes):
-    """The gather ceiling that bounds this schedule (measured, per config):
-    the tiled k = 32 copy re-reads X panels from L2; a row kernel on an X
-    beyond L2 (C3: 256 MB) is served by the Infinity Cache; the tiled k = 1
-    copy (C2) moves a 128-B line per 8-B gather."""
+def gather_ceiling(tiled, k, x_bytes, gather_bytes, traffic):
+    """The gather ceiling that bounds this schedule (measured, per config).
+    The tiled k = 1 copy (C2) moves a 128-B line per 8-B gather: its own
+    one-panel probe. Otherwise a gather is served by L2 or, when it misses,
+    by the Infinity Cache; hits and misses overlap, so the kernel cannot be
+    faster than either side alone: peak = min(L2 gather ceiling, IC service
+    ceiling x B_gather / miss bytes), B_gather and the miss bytes (the
+    kernel's PMC traffic, profiles/pmc_traffic_<config>.json) per SpMM. Without a PMC
+    record: the L2 ceiling for the tiled copy, the IC ceiling for a row
+    kernel on an X beyond L2."""
     if tiled and k == 1:
         return {"bound": "l2_line_gather_k1", "peak": K1_GATHER_PEAK_GBS, "peak_source": K1_GATHER_PEAK_SRC,
                 "peak_model": "the same kernel, every gather in one L2-resident 2 MiB panel (BSM_TILED_K1_PROBE)"}
+    l2 = {"bound": "l2_gather", "peak": L2_GATHER_PEAK_GBS, "peak_source": L2_GATHER_PEAK_SRC,
+          "peak_model": "the same inner loop on a static L2-resident X table"}
+    if traffic:
+        ic = IC_SERVICE_PEAK_GBS * gather_bytes / traffic
+        out = l2 if L2_GATHER_PEAK_GBS <= ic else {
+            "bound": "ic_miss_service", "peak": round(ic, 1),
+            "peak_source": f"{IC_SERVICE_PEAK_SRC}; miss bytes: PMC traffic",
+            "peak_model": "IC service ceiling x B_gather / the kernel's L2-miss bytes"}
+        return dict(out, peak_rule="min(L2 gather ceiling, IC service ceiling x B_gather / miss bytes)",
+                    ic_service_peak=IC_SERVICE_PEAK_GBS, miss_bytes_per_spmm=traffic,
+                    ic_probe_peak=round(IC_PROBE_GBS * gather_bytes / traffic, 1), ic_probe_source=IC_PROBE_SRC)
     if not tiled and x_bytes > (32 << 20):
-        return {"bound": "ic_gather", "peak": IC_GATHER_PEAK_GBS, "peak_source": IC_GATHER_PEAK_SRC,
-                "peak_model": "uniformly random 256-B row gathers served by the Infinity Cache (256 MB table, no "
-                              "L2 re-use)"}
-    return {"bound": "l2_gather", "peak": L2_GATHER_PEAK_GBS, "peak_source": L2_GATHER_PEAK_SRC,
-            "peak_model": "the same inner loop on a static L2-resident X table"}
+        return {"bound": "ic_gather", "peak": IC_SERVICE_PEAK_GBS, "peak_source": IC_SERVICE_PEAK_SRC,
+                "peak_model": "uniformly random row gathers served by the Infinity Cache (no L2 re-use, no PMC "
+                              "record for this run)"}
+    return l2
 
 
 def kernel_label(rows, nnz, k, panel_cols, tiled=False):
@@ -634,6 +655,7 @@ def main():
                 traffic_src = os.path.relpath(pmc_json, ROOT)
             else:
                 pmc = None
+        gceil = gather_ceiling(tiled, k, n_cols * k * es, b_gather(my_rows, my_nnz, k, es), traffic)
         solo_rccl = os.environ.get("BSM_MULTI_SOLO_RCCL") == "1"
         comm = ((f"external rank contexts, Y slots exchanged over torch.distributed {backend} on the host "
                  f"({world} ranks; a logic check, not a measurement)") if external else
@@ -706,11 +728,13 @@ def main():
                 "bytes_per_launch_alg": b_launch,
             },
             "roofline_gather": dict(
-                gather_ceiling(tiled, k, n_cols * k * es),
+                gceil,
                 model="B_gather (SURVEY.md §8d traffic model: every nnz gathers its whole X row)",
                 achieved=round(achieved_gather, 2),
                 unit="GB/s",
-                frac=round(achieved_gather / gather_ceiling(tiled, k, n_cols * k * es)["peak"], 5),
+                frac=round(achieved_gather / gceil["peak"], 5),
+                **({"ic_probe_frac": round(achieved_gather / gceil["ic_probe_peak"], 5)}
+                   if "ic_probe_peak" in gceil else {}),
                 bytes_per_launch_gather=b_gather(my_rows, my_nnz, k, es),
             ),
             "end_to_end_ms": e2e,

@@ -86,42 +86,6 @@ def test_tiled_equals_rowwave_random(orc, geometry, rw, waves, pshift):
     assert np.array_equal(got.view(np.uint64), dense.view(np.uint64))
 
 
-@pytest.mark.parametrize("half", ["2", "3"])
-@pytest.mark.parametrize("rw,waves,pshift", [(None, None, None), (16, 64, 10), (144, 8, 6)])
-def test_tiled_half16_equals_rowwave(geometry, monkeypatch, rw, waves, pshift, half):
-    """The half-width schedule with 16-B lanes (spmm_tiled_k32h16: Y half
-    rows of 128 B, two passes per batch; 8 waves per CU of up to 155 rows or
-    4 of up to 255): the same bits and counts as the one-row-per-wave kernel,
-    also with unsorted rows, NaN/inf and exact cancellations."""
-    device = _dev()
-    geometry(rw, waves, pshift)
-    monkeypatch.setenv("BSM_TILED_HALF", half)
-    rows, n_cols, k = 30_000, 200_000, 32
-    blk = device.DeviceCsrBlock.generate(1000, 0, rows, n_cols, _lib.ROWLEN_UNIFORM, 0, 120)
-    x = device.gen_dense(1001, 0, n_cols, k)
-    assert blk.plan_tiled(k, force=True) is not None
-    y1, n1 = _spmm(blk, x, tiled=True)
-    y0, n0 = _spmm(blk, x, tiled=False)
-    assert _same(y1, y0) and torch.equal(n1, n0)
-    rng = np.random.default_rng(5)
-    rows, n_cols = 2000, 3000
-    lens = rng.integers(0, 40, size=rows)
-    lens[17] = 900
-    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-    ci = np.concatenate([rng.permutation(rng.choice(n_cols, size=n, replace=False)) for n in lens]).astype(np.int32)
-    v = rng.integers(-3, 4, size=rp[-1]).astype(np.float64)
-    v[v == 0] = -0.0
-    xs = rng.integers(-2, 3, size=(n_cols, k)).astype(np.float64)
-    xs[7, 3] = np.nan
-    xs[11, :] = np.inf
-    blk = _block(rp, ci, v, n_cols)
-    x = torch.as_tensor(xs, device="cuda")
-    assert blk.plan_tiled(k, force=True) is not None
-    y1, n1 = _spmm(blk, x, True)
-    y0, n0 = _spmm(blk, x, False)
-    assert _same(y1, y0) and torch.equal(n1, n0)
-
-
 def test_tiled_tiny_and_uneven(geometry):
     """Fewer rows than waves, one long row among short ones, empty matrix rows."""
     geometry(None, 64, 8)
