@@ -105,6 +105,8 @@ SIGNATURES = [
     ("bsm_backward_substitution", _int, [_vp, _u64, _u64, _pp, _pp]),
     ("bsm_solve", _int, [_vp, _u64, _u64, _pp, _pp]),
     ("bsm_solve_blocked", _int, [_vp, _u64, _u64, _pp, _pp]),
+    ("bsm_solve_nd", _int, [_vp, _u64, _u64, _pp, _pp]),
+    ("bsm_nd_analyse", _int, [_u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64p, _vp, _u64, _u64p]),
     ("bsm_dev_gen_row_ptr", _int, [_u64, _u64, _u64, _u32, _int, _u32, _u32, _vp, _vp, _u64, _vp]),
     ("bsm_dev_gen_entries", _int, [_int, _u64, _u64, _u64, _u32, _int, _vp, _vp, _vp, _vp]),
     ("bsm_dev_gen_dense", _int, [_int, _u64, _u64, _u64, _u64, _int, _vp, _vp]),

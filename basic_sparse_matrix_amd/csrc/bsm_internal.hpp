@@ -331,4 +331,5 @@ int solve_dispatch_full(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_
                         hipStream_t s);
 int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev,
                            hipStream_t s);
+int solve_dispatch_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s);
 }  // namespace bsm

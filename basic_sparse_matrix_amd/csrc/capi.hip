@@ -986,6 +986,20 @@ int bsm_solve_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* cons
     return download_columns(a->dtype, n, k, x.p, x_cols, s);
 }
 
+int bsm_solve_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols, void* const* x_cols) {
+    BSM_REQUIRE(a && (k == 0 || (b_cols && x_cols)), BSM_ERR_INVALID, "null argument");
+    BSM_REQUIRE(a->rows == a->cols, BSM_ERR_PANIC,
+                "solve: cholesky_decomp().unwrap() on a non-square matrix panics (lib.rs:20)");
+    BSM_REQUIRE(a->dtype == BSM_F32 || a->dtype == BSM_F64, BSM_ERR_INVALID, "f32/f64 only");
+    hipStream_t s;
+    BSM_TRY(ctx_stream(&s));
+    DBuf b, x;
+    BSM_TRY(upload_columns(a->dtype, n, k, b_cols, b, s));
+    BSM_TRY(x.alloc(n * k * dtype_size(a->dtype)));
+    BSM_TRY(solve_dispatch_nd(a, k, n, b.p, x.p, s));
+    return download_columns(a->dtype, n, k, x.p, x_cols, s);
+}
+
 // ---- device-level entry points --------------------------------------------
 uint64_t bsm_dev_scan_workspace_bytes(uint64_t n) {
     return ((n * sizeof(int32_t) + 255) / 256) * 256 + scan_workspace_bytes(n);

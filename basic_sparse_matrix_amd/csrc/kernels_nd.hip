@@ -1,0 +1,615 @@
+// kernels_nd.hip -- solve(order="nd"): x = A^-1 b (src/lib.rs:11-24) by a
+// multifrontal Cholesky of P A P^T on the nested-dissection separator tree
+// (nd_order.cpp), on gfx950. DESIGN.md §4.9.
+//
+// Each tree node is a dense front F (f_pad x f_pad, column-major): its own
+// np columns (padded to np_pad = 64 * npt with identity pivots), then its m
+// front rows st (ancestors' columns), f = np_pad + m, f_pad = 64 * nt. Per
+// level of the tree (height), bottom-up:
+//   nd_factor  -- partial Cholesky of every front of the level: left-looking
+//                 64 x 64 tiles on f64 MFMA, tickets in column order across
+//                 the level's fronts, one flag per tile (write-through
+//                 hand-offs as in blk_chol). Pivot tiles: L and the inverse
+//                 diagonal tiles Dinv; trailing tiles: the update block
+//                 U = F22 - L21 L21^T left in place.
+//   nd_extend  -- U of each child added into its parent's front (children
+//                 slot 0, then slot 1: a fixed order, so the bits repeat).
+// The solves walk the same levels: forward bottom-up (a child's update
+// vector into its parent), backward top-down (the ancestors' x gathered).
+// Not bit-exact with the reference (another elimination order, FMA); within
+// the north star's f64 tolerance (tests/test_gpu_solver_nd.py).
+#include <algorithm>
+#include <cstdlib>
+#include <thread>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "bsm_internal.hpp"
+#include "nd.hpp"
+
+namespace bsm {
+namespace {
+
+#include "solve_tiles.hpp"
+
+struct NdDev {
+    int64_t foff;      // the front at F + foff
+    int64_t dinv_off;  // npt inverse diagonal tiles (Dinv[q * 64 + l] = Linv[l][q])
+    int64_t flag_off;  // nt x npt tile flags
+    int64_t st_off;    // m front rows (st) and their places in the parent's front (ri)
+    int64_t voff;      // f_pad solve-vector entries per right-hand column
+    int64_t start;     // own columns [start, start + np)
+    int32_t ld, np, np_pad, m, npt, nt, parent, kid0, kid1, pad;
+};
+
+__device__ __forceinline__ int32_t lower_bound_i32(const int32_t* a, int32_t len, int64_t x) {
+    int32_t lo = 0, hi = len;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// A's lower triangle (j <= i, as band_fill reads it) into the fronts: entry
+// (i, j) goes to the front owning column min(pinv i, pinv j)
+template <typename T>
+__global__ __launch_bounds__(256) void nd_assemble(int64_t n, const int64_t* __restrict__ rp,
+                                                   const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                   const int32_t* __restrict__ pinv, const int32_t* __restrict__ owner,
+                                                   const NdDev* __restrict__ nodes, const int32_t* __restrict__ st,
+                                                   T* __restrict__ F) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t pi = pinv[i];
+    for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+        const int64_t j = col[e];
+        if (j > i) continue;
+        const int64_t pj = pinv[j];
+        const int64_t r = pi > pj ? pi : pj, c = pi > pj ? pj : pi;
+        const NdDev& nd = nodes[owner[c]];
+        const int64_t lc = c - nd.start;
+        const int64_t lr = r < nd.start + nd.np ? r - nd.start : nd.np_pad + lower_bound_i32(st + nd.st_off, nd.m, r);
+        F[nd.foff + lc * nd.ld + lr] = val[e];
+    }
+}
+
+// identity on the padding pivots [np, np_pad) of every front
+template <typename T>
+__global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ nodes, T* __restrict__ F) {
+    const NdDev& nd = nodes[blockIdx.x];
+    for (int d = nd.np + (int)threadIdx.x; d < nd.np_pad; d += 64) F[nd.foff + (int64_t)d * nd.ld + d] = (T)1;
+}
+
+// Partial Cholesky of the fronts of one level. tiles[t] = (node, I, K):
+// column-major order across the level's fronts (K, then node, then I), so a
+// tile only waits on tiles of earlier tickets. Tile (I, K), I >= K:
+//     S = F_IK - sum_{J < min(K, npt)} L_IJ L_KJ^T
+//     K < npt, I == K: L_KK = chol(S), Dinv_K = L_KK^-1   (flag)
+//     K < npt, I >  K: L_IK = S L_KK^-T                    (flag)
+//     K >= npt       : U_IK = S (the update block, for nd_extend)
+template <typename T>
+__global__ __launch_bounds__(256) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
+                                                 int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
+                                                 int* __restrict__ flags, int* __restrict__ ticket,
+                                                 int* __restrict__ status) {
+    __shared__ T PT[64][TLD];
+    __shared__ T QT[64][TLD];
+    __shared__ T rd[64];
+    __shared__ T Di[4 * 256];
+    __shared__ T Tb[3 * 256];
+    __shared__ int64_t tk;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rb = 16 * w + (lane >> 4), cm = lane & 15;
+    lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
+    lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
+    auto wait_flag = [&](const int* f) {
+        long long spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > SPIN_LIMIT) {
+                if (lane == 0) atomicOr(status, ST_TIMEOUT);
+                return;
+            }
+        }
+    };
+    for (;;) {
+        if (tid == 0) tk = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int64_t t = tk;
+        if (t >= ntiles) break;
+        const int4 tl = tiles[t];
+        const NdDev& nd = nodes[tl.x];
+        const int I = tl.y, K = tl.z, npt = nd.npt;
+        const int64_t ld = nd.ld;
+        T* const Fn = F + nd.foff;
+        int* const fl = flags + nd.flag_off;
+        // X[t][r] = L[64 I2 + r][64 J + t] (sc1: other workgroups wrote it)
+        auto stage = [&](T (*X)[TLD], int I2, int J) {
+            T v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u, r = e & 63, c = e >> 6;
+                v[u] = ld_sc1(&Fn[(int64_t)(64 * J + c) * ld + 64 * I2 + r]);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u;
+                X[e >> 6][e & 63] = v[u];
+            }
+        };
+        T acc[4][4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                acc[cb][q] = Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q];
+        const int Jn = K < npt ? K : npt;
+        for (int J = 0; J < Jn; ++J) {
+            wait_flag(&fl[I * npt + J]);
+            if (I != K) wait_flag(&fl[K * npt + J]);
+            stage(PT, I, J);
+            if (I != K) stage(QT, K, J);
+            __syncthreads();
+            mfma_tile<T, true>(PTl, I != K ? QTl : PTl, acc, w, lane);
+            __syncthreads();
+        }
+        if (K < npt && I == K) {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
+            __syncthreads();
+            blk_diag_panels<T>(PTl, QTl, (lds_t<T>*)Di, (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, nullptr, nullptr,
+                               nullptr, nullptr);
+            __syncthreads();
+            T* const dk = Dinv + nd.dinv_off + (int64_t)K * 4096;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u, q = e >> 6, l = e & 63;
+                st_sc1(&dk[e], (T)QT[q][l]);  // Dinv[q * 64 + l] = Linv[l][q]
+                const int r = e & 63, c = e >> 6;
+                Fn[(int64_t)(64 * K + c) * ld + 64 * K + r] = r >= c ? (T)PT[r][c] : (T)0;
+            }
+        } else if (K < npt) {
+            wait_flag(&fl[K * npt + K]);
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) PT[16 * cb + cm][rb + 4 * q] = acc[cb][q];  // S^T
+            const T* const dk = Dinv + nd.dinv_off + (int64_t)K * 4096;
+            T v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = ld_sc1(&dk[tid + 256 * u]);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u;
+                QT[e >> 6][e & 63] = v[u];  // QT[s][c] = Linv[c][s]
+            }
+            __syncthreads();
+            T o[4][4] = {};
+            mfma_tile<T, false, true>(PTl, QTl, o, w, lane);
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_sc1(&Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q], o[cb][q]);
+        } else {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q] = acc[cb][q];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (K < npt && tid == 0) __hip_atomic_store(&fl[I * npt + K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// U of a child into its parent's front: task (child, b) adds column b of the
+// child's update block, rows a >= b, at (ri[a], ri[b]). One wave per task.
+template <typename T>
+__global__ __launch_bounds__(256) void nd_extend(const NdDev* __restrict__ nodes, const int2* __restrict__ tasks,
+                                                 int64_t ntasks, const int32_t* __restrict__ ri, T* __restrict__ F) {
+    const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (task >= ntasks) return;
+    const int lane = threadIdx.x & 63;
+    const int2 tk = tasks[task];
+    const NdDev& c = nodes[tk.x];
+    const NdDev& p = nodes[c.parent];
+    const int32_t* rc = ri + c.st_off;
+    const int b = tk.y;
+    const T* src = F + c.foff + (int64_t)(c.np_pad + b) * c.ld + c.np_pad;
+    T* dst = F + p.foff + (int64_t)rc[b] * p.ld;
+    for (int a = b + lane; a < c.m; a += 64) dst[rc[a]] += src[a];
+}
+
+// right-hand sides into the new order: bp[col * n + q] = b[perm[q] * k + col] (b row-major n x k)
+template <typename T>
+__global__ __launch_bounds__(256) void nd_gather(int64_t n, int64_t k, const int64_t* __restrict__ perm,
+                                                 const T* __restrict__ b, T* __restrict__ bp) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const int64_t o = perm[q];
+    for (int64_t c = 0; c < k; ++c) bp[c * n + q] = b[o * k + c];
+}
+template <typename T>
+__global__ __launch_bounds__(256) void nd_scatter(int64_t n, int64_t k, const int64_t* __restrict__ perm,
+                                                  const T* __restrict__ xp, T* __restrict__ x) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const int64_t o = perm[q];
+    for (int64_t c = 0; c < k; ++c) x[o * k + c] = xp[c * n + q];
+}
+
+// Forward solve of one level, one workgroup per (node, column): v = the
+// node's pivots of bp plus its children's update vectors; per pivot tile K
+// y_K = Dinv_K v_K, then v_I -= L_IK y_K below. v (at V + voff) ends as y
+// over the pivots and the update vector u over the front rows. V is read and
+// written write-through (rows change hands between threads).
+template <typename T>
+__global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ nodes, const int32_t* __restrict__ lvl,
+                                                  int64_t n, const T* __restrict__ bp, T* __restrict__ V, int64_t vtot,
+                                                  const T* __restrict__ F, const T* __restrict__ Dinv,
+                                                  const int32_t* __restrict__ ri) {
+    __shared__ T vk[64], yk[64];
+    const int tid = threadIdx.x;
+    const NdDev& nd = nodes[lvl[blockIdx.x]];
+    const int64_t col = blockIdx.y;
+    T* const v = V + col * vtot + nd.voff;
+    const int fp = 64 * nd.nt;
+    for (int r = tid; r < fp; r += 256) st_sc1(&v[r], r < nd.np ? bp[col * n + nd.start + r] : (T)0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int kid = s == 0 ? nd.kid0 : nd.kid1;
+        if (kid < 0) continue;
+        const NdDev& c = nodes[kid];
+        const T* u = V + col * vtot + c.voff + c.np_pad;
+        const int32_t* rc = ri + c.st_off;
+        for (int a = tid; a < c.m; a += 256) {
+            T* d = &v[rc[a]];
+            st_sc1(d, ld_sc1(d) + u[a]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const T* const Fn = F + nd.foff;
+    const int64_t ld = nd.ld;
+    for (int K = 0; K < nd.npt; ++K) {
+        if (tid < 64) vk[tid] = ld_sc1(&v[64 * K + tid]);
+        __syncthreads();
+        if (tid < 64) {
+            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096;
+            T y = (T)0;
+            for (int q = 0; q < 64; ++q) y = fma_t(g[q * 64 + tid], vk[q], y);
+            yk[tid] = y;
+            st_sc1(&v[64 * K + tid], y);
+        }
+        __syncthreads();
+        for (int r = 64 * (K + 1) + tid; r < fp; r += 256) {
+            const T* lc = Fn + (int64_t)64 * K * ld + r;
+            T s0 = (T)0, s1 = (T)0;
+            for (int t = 0; t < 64; t += 2) {
+                s0 = fma_t(lc[(int64_t)t * ld], yk[t], s0);
+                s1 = fma_t(lc[(int64_t)(t + 1) * ld], yk[t + 1], s1);
+            }
+            st_sc1(&v[r], ld_sc1(&v[r]) - (s0 + s1));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
+// Backward solve of one level, one workgroup per (node, column): w = y over
+// the pivots, the ancestors' x over the front rows; per pivot tile K from the
+// last, x_K = Dinv_K^T (y_K - L_{>K,K}^T w_{>K}); the pivots' x to xp.
+template <typename T>
+__global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nodes, const int32_t* __restrict__ lvl,
+                                                   int64_t n, T* __restrict__ xp, T* __restrict__ V, int64_t vtot,
+                                                   const T* __restrict__ F, const T* __restrict__ Dinv,
+                                                   const int32_t* __restrict__ st) {
+    __shared__ T red[64][65];
+    __shared__ T zk[64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const NdDev& nd = nodes[lvl[blockIdx.x]];
+    const int64_t col = blockIdx.y;
+    T* const w = V + col * vtot + nd.voff;
+    const int fp = 64 * nd.nt;
+    for (int a = tid; a < nd.m; a += 256) st_sc1(&w[nd.np_pad + a], xp[col * n + st[nd.st_off + a]]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const T* const Fn = F + nd.foff;
+    const int64_t ld = nd.ld;
+    for (int K = nd.npt - 1; K >= 0; --K) {
+        T acc[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = (T)0;
+        const T* lc = Fn + (int64_t)(64 * K + 16 * wv) * ld;
+        for (int r = 64 * (K + 1) + lane; r < fp; r += 64) {
+            const T wr = ld_sc1(&w[r]);
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma_t(lc[(int64_t)c * ld + r], wr, acc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) red[16 * wv + c][lane] = acc[c];
+        __syncthreads();
+        if (tid < 64) {
+            T s0 = (T)0, s1 = (T)0;
+            for (int l = 0; l < 64; l += 2) {
+                s0 += red[tid][l];
+                s1 += red[tid][l + 1];
+            }
+            zk[tid] = ld_sc1(&w[64 * K + tid]) - (s0 + s1);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096 + (int64_t)tid * 64;
+            T x = (T)0;
+            for (int q = 0; q < 64; ++q) x = fma_t(g[q], zk[q], x);  // Linv[q][tid] = Dinv[tid * 64 + q]
+            st_sc1(&w[64 * K + tid], x);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    for (int p = tid; p < nd.np; p += 256) xp[col * n + nd.start + p] = ld_sc1(&w[p]);
+}
+
+inline unsigned nd_blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+// the device form of a plan: node descriptors, front rows, tile and task lists
+struct NdLayout {
+    std::vector<NdDev> dev;
+    std::vector<int32_t> st, ri, pinv, owner, lvl_nodes;
+    std::vector<int4> tiles;
+    std::vector<int2> ext;
+    std::vector<int64_t> tiles_off, lvl_off, ext_off;  // per level (ext: per level and slot)
+    int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
+};
+
+void nd_layout(const NdPlan& P, NdLayout& L) {
+    const int32_t nn = (int32_t)P.nodes.size();
+    L.dev.resize((size_t)nn);
+    int64_t st_total = 0;
+    for (int32_t i = 0; i < nn; ++i) {
+        const NdNode& x = P.nodes[(size_t)i];
+        NdDev& d = L.dev[(size_t)i];
+        d.np = (int32_t)(x.end - x.start);
+        d.npt = (d.np + 63) / 64;
+        d.np_pad = 64 * d.npt;
+        d.m = (int32_t)x.st.size();
+        d.nt = (d.np_pad + d.m + 63) / 64;
+        d.ld = 64 * d.nt;
+        d.start = x.start;
+        d.parent = x.parent;
+        d.kid0 = x.kids[0];
+        d.kid1 = x.kids[1];
+        d.pad = 0;
+        d.foff = L.f_elems;
+        L.f_elems += (int64_t)d.ld * d.ld;
+        d.dinv_off = L.dinv_elems;
+        L.dinv_elems += (int64_t)d.npt * 4096;
+        d.flag_off = L.n_flags;
+        L.n_flags += (int64_t)d.nt * d.npt;
+        d.voff = L.vtot;
+        L.vtot += d.ld;
+        d.st_off = st_total;
+        st_total += d.m;
+    }
+    L.st.resize((size_t)st_total);
+    L.ri.resize((size_t)st_total);
+    for (int32_t i = 0; i < nn; ++i) {
+        const NdNode& x = P.nodes[(size_t)i];
+        const NdDev& d = L.dev[(size_t)i];
+        for (int32_t a = 0; a < d.m; ++a) L.st[(size_t)(d.st_off + a)] = (int32_t)x.st[(size_t)a];
+        if (x.parent < 0) continue;
+        // a front row of the child is a pivot of the parent or one of its front rows
+        const NdNode& px = P.nodes[(size_t)x.parent];
+        const NdDev& pd = L.dev[(size_t)x.parent];
+        size_t j = 0;
+        for (int32_t a = 0; a < d.m; ++a) {
+            const int64_t q = x.st[(size_t)a];
+            if (q < px.end) {
+                L.ri[(size_t)(d.st_off + a)] = (int32_t)(q - px.start);
+            } else {
+                while (px.st[j] < q) ++j;
+                L.ri[(size_t)(d.st_off + a)] = pd.np_pad + (int32_t)j;
+            }
+        }
+    }
+    L.pinv.resize((size_t)P.n);
+    L.owner.resize((size_t)P.n);
+    for (int64_t v = 0; v < P.n; ++v) L.pinv[(size_t)v] = (int32_t)P.pinv[(size_t)v];
+    for (int32_t i = 0; i < nn; ++i)
+        for (int64_t q = P.nodes[(size_t)i].start; q < P.nodes[(size_t)i].end; ++q) L.owner[(size_t)q] = i;
+    // per level: the nodes, the factor's tiles (K, node, I) and the extend tasks (slot, node, b)
+    std::vector<std::vector<int32_t>> by_level((size_t)P.n_levels);
+    for (int32_t i = 0; i < nn; ++i) by_level[(size_t)P.nodes[(size_t)i].level].push_back(i);
+    for (const auto& lv : by_level) {
+        L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
+        L.lvl_nodes.insert(L.lvl_nodes.end(), lv.begin(), lv.end());
+        L.tiles_off.push_back((int64_t)L.tiles.size());
+        int32_t kmax = 0;
+        for (int32_t i : lv) kmax = std::max(kmax, L.dev[(size_t)i].nt);
+        for (int32_t K = 0; K < kmax; ++K)
+            for (int32_t i : lv) {
+                const NdDev& d = L.dev[(size_t)i];
+                for (int32_t I = K; I < d.nt; ++I)
+                    if (K < d.nt) L.tiles.push_back(make_int4(i, I, K, 0));
+            }
+        for (int s = 0; s < 2; ++s) {
+            L.ext_off.push_back((int64_t)L.ext.size());
+            for (int32_t i : lv) {
+                const NdNode& x = P.nodes[(size_t)i];
+                if (x.parent < 0 || x.slot != s) continue;
+                for (int32_t b = 0; b < L.dev[(size_t)i].m; ++b) L.ext.push_back(make_int2(i, b));
+            }
+        }
+    }
+    L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
+    L.tiles_off.push_back((int64_t)L.tiles.size());
+    L.ext_off.push_back((int64_t)L.ext.size());
+}
+
+template <typename T>
+int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
+    stage_reset(s);
+    const int64_t N = (int64_t)n;
+    // A's pattern to the host for the analysis
+    std::vector<int64_t> rp((size_t)N + 1);
+    std::vector<int32_t> cl((size_t)a->nnz);
+    BSM_HIP_TRY(hipMemcpyAsync(rp.data(), a->row_ptr, (size_t)(N + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (a->nnz)
+        BSM_HIP_TRY(hipMemcpyAsync(cl.data(), a->col, (size_t)a->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    stage_mark("nd_pattern_d2h", s);
+    const char* le = getenv("BSM_ND_LEAF");
+    const char* te = getenv("BSM_ND_THREADS");
+    const int64_t leaf = le ? atoll(le) : 256;
+    int threads = te ? atoi(te) : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    NdPlan P;
+    const int arc = nd_analyse(N, rp.data(), cl.data(), leaf, threads, P);
+    BSM_REQUIRE(arc == 0, BSM_ERR_UNSUPPORTED,
+                "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
+    NdLayout L;
+    nd_layout(P, L);
+    stage_mark("nd_analyse", s);
+    if (getenv("BSM_ND_TRACE")) {
+        int64_t mx = 0;
+        for (const auto& d : L.dev) mx = std::max<int64_t>(mx, d.ld);
+        fprintf(stderr,
+                "[bsm nd] n %lld nodes %zu levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms; fronts "
+                "%.3f GB (largest %lld), tiles %zu, extend columns %zu\n",
+                (long long)N, L.dev.size(), P.n_levels, P.ms_graph, P.ms_order, P.ms_symbolic,
+                (double)L.f_elems * sizeof(T) * 1e-9, (long long)mx, L.tiles.size(), L.ext.size());
+    }
+    // device plan: one upload of the packed arrays
+    const int32_t nn = (int32_t)L.dev.size();
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t o_dev = 0, o_st = o_dev + al(L.dev.size() * sizeof(NdDev)),
+                 o_ri = o_st + al(L.st.size() * 4), o_pinv = o_ri + al(L.ri.size() * 4),
+                 o_owner = o_pinv + al(L.pinv.size() * 4), o_lvl = o_owner + al(L.owner.size() * 4),
+                 o_tiles = o_lvl + al(L.lvl_nodes.size() * 4), o_ext = o_tiles + al(L.tiles.size() * sizeof(int4)),
+                 o_perm = o_ext + al(L.ext.size() * sizeof(int2)), total = o_perm + al((size_t)N * 8);
+    std::vector<char> hp(total);
+    auto put = [&](size_t o, const void* p, size_t b) {
+        if (b) memcpy(hp.data() + o, p, b);
+    };
+    put(o_dev, L.dev.data(), L.dev.size() * sizeof(NdDev));
+    put(o_st, L.st.data(), L.st.size() * 4);
+    put(o_ri, L.ri.data(), L.ri.size() * 4);
+    put(o_pinv, L.pinv.data(), L.pinv.size() * 4);
+    put(o_owner, L.owner.data(), L.owner.size() * 4);
+    put(o_lvl, L.lvl_nodes.data(), L.lvl_nodes.size() * 4);
+    put(o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
+    put(o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
+    put(o_perm, P.perm.data(), (size_t)N * 8);
+    DBuf plan;
+    BSM_TRY(plan.alloc(total));
+    BSM_HIP_TRY(hipMemcpyAsync(plan.p, hp.data(), total, hipMemcpyHostToDevice, s));
+    char* pb = plan.as<char>();
+    const NdDev* d_nodes = (const NdDev*)(pb + o_dev);
+    const int32_t* d_st = (const int32_t*)(pb + o_st);
+    const int32_t* d_ri = (const int32_t*)(pb + o_ri);
+    const int32_t* d_pinv = (const int32_t*)(pb + o_pinv);
+    const int32_t* d_owner = (const int32_t*)(pb + o_owner);
+    const int32_t* d_lvl = (const int32_t*)(pb + o_lvl);
+    const int4* d_tiles = (const int4*)(pb + o_tiles);
+    const int2* d_ext = (const int2*)(pb + o_ext);
+    const int64_t* d_perm = (const int64_t*)(pb + o_perm);
+    // numeric storage
+    DBuf fr, dv, fl;
+    BSM_TRY(fr.alloc((size_t)L.f_elems * sizeof(T)));
+    BSM_TRY(dv.alloc((size_t)std::max<int64_t>(L.dinv_elems, 1) * sizeof(T)));
+    const size_t nfl = (size_t)L.n_flags + (size_t)P.n_levels + 2;
+    BSM_TRY(fl.alloc(nfl * sizeof(int)));
+    BSM_HIP_TRY(hipMemsetAsync(fr.p, 0, (size_t)L.f_elems * sizeof(T), s));
+    BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
+    int* d_flags = fl.as<int>();
+    int* d_tickets = d_flags + L.n_flags;
+    int* d_status = d_tickets + P.n_levels;
+    T* F = fr.as<T>();
+    stage_mark("nd_upload", s);
+    nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals), d_pinv,
+                                                     d_owner, d_nodes, d_st, F);
+    BSM_HIP_TRY(hipGetLastError());
+    nd_pad_pivots<T><<<(unsigned)nn, 64, 0, s>>>(d_nodes, F);
+    BSM_HIP_TRY(hipGetLastError());
+    stage_mark("nd_assemble", s);
+    int dev = 0, cus = 0, per_cu = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nd_factor<T>, 256, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "nd_factor does not fit a CU");
+    for (int32_t lv = 0; lv < P.n_levels; ++lv) {
+        const int64_t t0 = L.tiles_off[(size_t)lv], nt = L.tiles_off[(size_t)lv + 1] - t0;
+        if (nt > 0) {
+            const int64_t grid = std::min<int64_t>(nt, (int64_t)cus * per_cu);
+            nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
+                                                        d_tickets + lv, d_status);
+            BSM_HIP_TRY(hipGetLastError());
+        }
+        for (int sl = 0; sl < 2; ++sl) {
+            const int64_t e0 = L.ext_off[(size_t)(2 * lv + sl)], ne = L.ext_off[(size_t)(2 * lv + sl) + 1] - e0;
+            if (ne <= 0) continue;
+            nd_extend<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext + e0, ne, d_ri, F);
+            BSM_HIP_TRY(hipGetLastError());
+        }
+    }
+    stage_mark("nd_factor", s);
+    if (k > 0) {
+        DBuf bpb, vb;
+        BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T)));
+        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(L.vtot, 1) * k * sizeof(T)));
+        nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
+                                                       bpb.as<T>());
+        BSM_HIP_TRY(hipGetLastError());
+        for (int32_t lv = 0; lv < P.n_levels; ++lv) {
+            const int64_t o = L.lvl_off[(size_t)lv], c = L.lvl_off[(size_t)lv + 1] - o;
+            if (c <= 0) continue;
+            nd_forward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
+                                                                        vb.as<T>(), L.vtot, F, dv.as<T>(), d_ri);
+            BSM_HIP_TRY(hipGetLastError());
+        }
+        stage_mark("nd_forward", s);
+        for (int32_t lv = P.n_levels - 1; lv >= 0; --lv) {
+            const int64_t o = L.lvl_off[(size_t)lv], c = L.lvl_off[(size_t)lv + 1] - o;
+            if (c <= 0) continue;
+            nd_backward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
+                                                                         vb.as<T>(), L.vtot, F, dv.as<T>(), d_st);
+            BSM_HIP_TRY(hipGetLastError());
+        }
+        stage_mark("nd_backward", s);
+        nd_scatter<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, bpb.as<T>(), static_cast<T*>(x_dev));
+        BSM_HIP_TRY(hipGetLastError());
+    }
+    int h = 0;
+    BSM_HIP_TRY(read_dev(&h, d_status, sizeof(int), s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));
+    stage_mark("nd_copy_out", s);
+    BSM_REQUIRE(!(h & ST_TIMEOUT), BSM_ERR_HIP, "nd factor: tile hand-off timed out");
+    BSM_REQUIRE(!(h & ST_NOT_PD), BSM_ERR_UNSUPPORTED,
+                "cholesky: matrix is not positive definite (a pivot is <= 0 or not finite)");
+    return BSM_OK;
+}
+
+}  // namespace
+
+// solve (lib.rs:11-24) by the nested-dissection multifrontal factorisation
+int solve_dispatch_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
+    BSM_REQUIRE(a->rows == n, BSM_ERR_PANIC,
+                "solve: b has %llu rows but A has %llu (index out of bounds in the reference)", (unsigned long long)n,
+                (unsigned long long)a->rows);
+    BSM_REQUIRE(n < ((uint64_t)1 << 31), BSM_ERR_UNSUPPORTED, "solve nd: n >= 2^31");
+    if (n == 0) return BSM_OK;
+    if (a->dtype == BSM_F64) return nd_solve<double>(a, k, n, b_dev, x_dev, s);
+    if (a->dtype == BSM_F32) return nd_solve<float>(a, k, n, b_dev, x_dev, s);
+    set_error("solve: f32/f64 only");
+    return BSM_ERR_INVALID;
+}
+
+}  // namespace bsm

@@ -39,37 +39,10 @@
 namespace bsm {
 namespace {
 
+#include "solve_tiles.hpp"
+
 constexpr int TR = 16;              // rows per tile-row
-constexpr long long SPIN_LIMIT = 1ll << 25;
 
-enum { ST_NOT_PD = 1, ST_TIMEOUT = 2, ST_EMPTY_ROW = 4, ST_COL_OOB = 8 };
-
-// Row-block tickets for the persistent Cholesky grids, handed out in
-// ascending order: a workgroup only ever waits on LOWER row-blocks, which
-// workgroups already running hold, so progress needs no co-residency of the
-// grid (a CU held by another kernel or stream only slows the factor down).
-__device__ __forceinline__ int64_t next_ticket(int* ticket, int* s_tk) {
-    __syncthreads();  // every thread has read the previous ticket
-    if (threadIdx.x == 0) *s_tk = atomicAdd(ticket, 1);
-    __syncthreads();
-    return *s_tk;
-}
-
-// ---- write-through (sc1) loads/stores of T via same-width integers --------
-template <typename T> struct Bits;
-template <> struct Bits<double> { using U = unsigned long long; };
-template <> struct Bits<float> { using U = unsigned int; };
-
-template <typename T> __device__ __forceinline__ T ld_sc1(const T* p) {
-    using U = typename Bits<T>::U;
-    U u = __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_bit_cast(T, u);
-}
-template <typename T> __device__ __forceinline__ void st_sc1(T* p, T v) {
-    using U = typename Bits<T>::U;
-    __hip_atomic_store(reinterpret_cast<U*>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // powf(x, 0.5) as LLVM lowers it: x == -inf ? +inf : |sqrt(x)| (correctly
 // rounded sqrt; -0 -> +0). Matches the oracle and the reference's goldens.
@@ -122,20 +95,6 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// Lane j of each 16-lane row to the whole row (DPP row_newbcast:j, gfx90a+; the
-// one DPP form 64-bit data may use): a VALU move, no LDS, no SGPR. Full masks
-// and bound_ctrl make the old value dead, so a double is ONE v_mov_b64_dpp
-// (with old = 0 and no bound_ctrl it was two v_mov_b32_dpp after two moves
-// initialising the destination).
-template <int J> __device__ __forceinline__ int rowbcast_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, true);
-}
-template <int J> __device__ __forceinline__ double rowbcast(double v) {
-    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
-}
-template <int J> __device__ __forceinline__ float rowbcast(float v) {
-    return __int_as_float(rowbcast_i<J>(__float_as_int(v)));
-}
 
 // √ of a pivot the caller has checked positive and finite: IEEE sqrt
 // correctly rounded (f32: formed in f64, rounded once, as pow_half). A pivot
@@ -1227,8 +1186,6 @@ __global__ __launch_bounds__(256) void csr_cols_past_rhs(int64_t n, const int64_
 // 64 x 64 matrix-vector product (MF_I or MB_I) in one wave, against the N*b
 // dependent adds of the reference order (band_backward_reg).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double fma_t(double a, double b, double c) { return __fma_rn(a, b, c); }
-__device__ __forceinline__ float fma_t(float a, float b, float c) { return __fmaf_rn(a, b, c); }
 
 // M[q * 64 + l] layouts (one 64 x 64 matrix per block, 4096 elements):
 //   G[I]  = Linv_I[l][q]   (forward:  u[l] = sum_q Linv[l][q] r[q])
@@ -1320,18 +1277,31 @@ __global__ __launch_bounds__(256) void blk_prep(int64_t n, int64_t b, int64_t ld
 // (nb64 * 64 each), flags[col * nb64 + I] = 1 once block I of Y is final
 // (write-through stores, drained, then a relaxed agent-scope flag; sc1 loads
 // on the reading side: MI355X_MICROARCH.md "Valid forms", row 1).
+// One band (segment) of a blk_trsv launch: its factor (rows [0, n) of the
+// band at CB), blk_prep's Linv and coupling blocks, the right-hand sides
+// (column j at rhs + j * rhs_stride) and the padded solution (column j at
+// Y + j * nb64 * 64) with its per-block flags (column j at flags + j * nb64).
+template <typename T>
+struct TrsvSeg {
+    const T* CB;
+    int64_t n;
+    const T* Minv;
+    const T* Madj;
+    const T* rhs;
+    int64_t rhs_stride;
+    T* Y;
+    int* flags;
+};
+
 template <typename T, bool FWD>
-__global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld, const T* __restrict__ CB,
-                                                const T* __restrict__ Minv, const T* __restrict__ Madj,
-                                                const T* __restrict__ rhs, int64_t rhs_stride, T* __restrict__ Y,
-                                                int* __restrict__ flags, int* __restrict__ ticket,
-                                                int* __restrict__ status, int64_t k) {
+__global__ __launch_bounds__(256) void blk_trsv(int64_t b, int64_t ld, const TrsvSeg<T>* __restrict__ segs, int nseg,
+                                                int64_t nb64max, int* __restrict__ ticket, int* __restrict__ status,
+                                                int64_t k) {
     __shared__ T red[4][64];
     __shared__ T rv[64];
     __shared__ int64_t tk;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t nb64 = (n + 63) / 64, NP = nb64 * 64, pad_off = n * ld;
     auto wait_flag = [&](const int* f) {
         long long spins = 0;
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -1346,11 +1316,23 @@ __global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld
         if (threadIdx.x == 0) tk = atomicAdd(ticket, 1);
         __syncthreads();
         const int64_t t = tk;
-        if (t >= nb64 * k) break;
-        const int64_t col = t % k, step = t / k;
+        if (t >= nb64max * k * nseg) break;
+        // tickets: step s of every (segment, column) in turn
+        const int64_t step = t / (k * nseg), col = t % k;
+        const TrsvSeg<T> sg = segs[(t / k) % nseg];
+        const int64_t n = sg.n, nb64 = (n + 63) / 64, NP = nb64 * 64;
+        if (step >= nb64) {
+            __syncthreads();
+            continue;
+        }
+        const T* const CB = sg.CB;
+        const T* const Minv = sg.Minv;
+        const T* const Madj = sg.Madj;
+        const T* const rhs = sg.rhs;
+        const int64_t rhs_stride = sg.rhs_stride;
         const int64_t I = FWD ? step : nb64 - 1 - step, i0 = I * 64, i = i0 + lane;
-        T* Yc = Y + col * NP;
-        int* fl = flags + col * nb64;
+        T* Yc = sg.Y + col * NP;
+        int* fl = sg.flags + col * nb64;
         const bool has_adj = FWD ? I > 0 : I + 1 < nb64;
         // x-independent operands first: this wave's slice of Linv, wave 0's coupling matrix
         T minv[16], madj[64];
@@ -1377,10 +1359,13 @@ __global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int64_t j = J * 64 + 16 * w + q;
-                // L[i][j] (FWD) or L[j][i]: in the band and the matrix, else a zero of the padding
+                // L[i][j] (FWD) or L[j][i] in the band and the segment, else zero (the
+                // load reads element 0, the select drops it: past a segment's end
+                // the band holds the next rows' values, not padding)
                 const bool ok = FWD ? (i < n) & (i - j <= b) : (j < n) & (j - i <= b);
                 const int64_t idx = FWD ? j * ld + (i - j) : i * ld + (j - i);
-                lv[q] = CB[ok ? idx : pad_off];
+                const T lw = CB[idx & -(int64_t)ok];
+                lv[q] = ok ? lw : (T)0;
             }
             wait_flag(&fl[J]);
             const T v = ld_sc1(&Yc[J * 64 + lane]);
@@ -1440,266 +1425,24 @@ __global__ __launch_bounds__(256) void blk_trsv(int64_t n, int64_t b, int64_t ld
 // L are exact zeros (every product there has an out-of-band factor), so tiles
 // read zeros outside the band and write only inside it.
 // ---------------------------------------------------------------------------
-// tiles in LDS: rows padded to 65 elements (row-strided accesses hit distinct banks)
-constexpr int TLD = 65;
 
-// LDS pointers that keep their address space across a call
-template <typename T> using lds_t = __attribute__((address_space(3))) T;
-// the f64 MFMA 16x16x4 accumulator
-typedef double bsm_d4 __attribute__((ext_vector_type(4)));
-
-// 1/sqrt(x): the hardware estimate and one Newton step (its error squared
-// once): a short dependent chain for the blocked factor's pivots (two steps:
-// 317 against 311 ms at C5, x error 8.8e-11 against 9.7e-11)
-__device__ __forceinline__ double rsqrt_nr1(double x) {
-    const double y = __builtin_amdgcn_rsq(x);
-    const double h = __fma_rn(-x * y, y, 1.0);
-    return __fma_rn(0.5 * y, h, y);
-}
-__device__ __forceinline__ float rsqrt_nr(float x) {
-    float y = __builtin_amdgcn_rsqf(x);
-    const float h = __fmaf_rn(-x * y, y, 1.0f);
-    return __fmaf_rn(0.5f * y, h, y);
-}
-__device__ __forceinline__ float rsqrt_nr1(float x) { return rsqrt_nr(x); }
-
-// Block (p2, p1), p1 < p2, of Linv on one wave (f64 MFMA 16x16x4):
-// Linv[p2][p1] = -Di[p2] sum_{q = p1}^{p2 - 1} L[p2][q] Linv[q][p1],
-// from row blocks < p2 of Linv already in Q (Q[c * TLD + r] = Linv[r][c]).
+// One band (segment) of a blk_chol launch: rows [0, n) of the band at CB
+// (CB[k * ld + d] = A[k + d][k]), its Dinv blocks and flags. Several segments
+// (the interiors of solve(order="partitioned"), §4.9) are factored by one
+// launch, their tickets interleaved block column by block column.
 template <typename T>
-__device__ __forceinline__ void blk_linv_block(const lds_t<T>* P, lds_t<T>* Q, const lds_t<T>* Di, int p2, int p1,
-                                               int l) {
-    const int m = l & 15, kq = l >> 4;
-    bsm_d4 t = {0.0, 0.0, 0.0, 0.0};
-    for (int qb = p1; qb < p2; ++qb) {
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-            const int k = 16 * qb + 4 * k4 + kq;
-            t = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(16 * p2 + m) * TLD + k],
-                                                     (double)Q[(16 * p1 + m) * TLD + k], t, 0, 0, 0);
-        }
-    }
-    bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4)
-        o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)Di[p2 * 256 + m * 16 + 4 * k4 + kq], t[k4], o, 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) Q[(16 * p1 + m) * TLD + 16 * p2 + kq + 4 * q] = (T)o[q];
-}
-
-// Q's diagonal block p = Di[p] (Di[p][row][col] -> Q[col * TLD + row]), one wave
-template <typename T>
-__device__ __forceinline__ void blk_linv_diag(lds_t<T>* Q, const lds_t<T>* Di, int p, int l) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int e = l + 64 * u, row = e >> 4, col = e & 15;
-        Q[(16 * p + col) * TLD + 16 * p + row] = Di[p * 256 + e];
-    }
-}
-
-// Factor AND invert the 64 x 64 tile S (P[r * TLD + c], lower part) on all
-// four waves, by 16-column panels p (columns c0 = 16p ...):
-//   1. wave 0 factors the 16 x 16 diagonal block (lane r & 15 = row, pivots
-//      and L[j][t] by DPP row broadcast: no LDS, no barrier) and inverts it
-//      into Di[p];
-//   2. the rows below: L[i][c0 + j] = sum_t S[i][c0 + t] Di[p][j][t];
-//   3. the trailing lower part: S[i][j] -= sum_t L[i][c0 + t] L[j][c0 + t].
-// Steps 2 and 3 are 16 x 16 blocks on f64 MFMA, one block per wave at a time.
-// Linv by row blocks: row block p - 1 on waves 1-3 while wave 0 factors
-// block p, the last one at the end. rd[r] = 1 / L[r][r].
-// Every thread of the workgroup must call it (barriers inside).
-// Progressive publication (dpub): Linv's row block
-// p - 1 is complete once wave 0 has factored block p; wave 3, idle in the rows
-// below and the trailing update from panel 1 on, stores it to dpub (this
-// tile's Dinv, dpub[s * 64 + l] = Linv[l][s]) and raises rbf[p - 1] when the
-// stores have drained, one panel later. The next diagonal tile forms the
-// matching column block of its sub-diagonal tile and that block's update
-// while this factor runs (blk_chol): only row block 3 is left on the
-// chain. Row block 3 goes out with the tile's flag, as before.
-template <typename T>
-__device__ __forceinline__ void blk_publish_rowblock(const lds_t<T>* Q, T* __restrict__ dpub, int c, int lane) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int i = lane + 64 * u, s = i >> 4, j = i & 15;
-        st_sc1(&dpub[s * 64 + 16 * c + j], (T)Q[s * TLD + 16 * c + j]);
-    }
-}
-__device__ __forceinline__ void blk_publish_flag(int* rbf, int c, int lane) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&rbf[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+struct CholSeg {
+    T* CB;
+    int64_t n;
+    T* Dinv;     // nb64 * 4096
+    int* flags;  // nb64 * DM
+    int* rbf;    // 4 * nb64
+};
 
 template <typename T>
-__device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
-                                                int* status, int tid, unsigned long long* tdbg,
-                                                T* __restrict__ dpub, int* rbf, int* pflag) {
-    long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
-    asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    bool pd = true;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) Q[(tid >> 2) * TLD + 16 * (tid & 3) + u] = (T)0;  // rows of Linv^T
-    for (int p = 0; p < 4; ++p) {
-        const int c0 = 16 * p;
-        const long long t0 = tdbg ? clock64() : 0;
-        if (dpub && w == 3 && p >= 2) blk_publish_flag(rbf, p - 2, tid & 63);  // row block p - 2, stored a panel ago
-        if (w > 0) {
-            // while wave 0 factors block p: Linv's row block p - 1 (its blocks
-            // need row blocks < p - 1, Di[p - 1] and L's columns < p - 1, all
-            // complete) and diagonal block p - 1
-            if (p >= 2 && w - 1 < p - 1) blk_linv_block<T>(P, Q, Di, p - 1, w - 1, tid & 63);
-            if (p >= 1 && w == 3) blk_linv_diag<T>(Q, Di, p - 1, tid & 63);
-        } else {
-            const int r = tid & 15;
-            T dv[16], rps[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) dv[j] = P[(c0 + r) * TLD + c0 + j];
-            // The factor and the block's inverse in one pass. Step t: the pivot,
-            // column t of L (l, lane j: L[j][t]), the trailing update of the
-            // rows below by L[j][t] broadcast from lane j; and, with the same
-            // broadcasts, x[t] = Linv[t][r] of lane r's inverse column and its
-            // terms in the later rows' sums (acc[j] += L[j][t] x[t]): the FMAs
-            // of the row-by-row inverse, in the same order per row, so the
-            // same bits, with no second pass and no second set of broadcasts.
-            // The next pivot is lane t+1's own update fma(-l, l, dv[t+1]) (its
-            // broadcast of l is its own l): the pivot chain skips that broadcast.
-            T x[16], acc[16];
-#pragma unroll
-            for (int q2 = 0; q2 < 16; ++q2) acc[q2] = (T)0;
-            T nxt = dv[0];
-            auto step = [&]<int t>(std::integral_constant<int, t>) __attribute__((always_inline)) {
-                const T piv = rowbcast<t>(nxt);
-                pd = pd & (piv > (T)0) & (piv < (T)INFINITY);
-                const T rp = rsqrt_nr1(piv);
-                rps[t] = rp;
-                const T l = dv[t] * rp;  // lane t: the pivot's square root
-                dv[t] = l;
-                x[t] = ((t == r ? (T)1 : (T)0) - acc[t]) * rp;
-                if constexpr (t < 15) nxt = fma_t(-l, l, dv[t + 1]);
-                [&]<int... js>(std::integer_sequence<int, js...>) __attribute__((always_inline)) {
-                    (([&] {
-                         const T bl = rowbcast<t + 1 + js>(l);
-                         dv[t + 1 + js] = fma_t(-l, bl, dv[t + 1 + js]);
-                         acc[t + 1 + js] = fma_t(bl, x[t], acc[t + 1 + js]);
-                     }()),
-                     ...);
-                }(std::make_integer_sequence<int, 15 - t>{});
-            };
-            [&]<int... ts>(std::integer_sequence<int, ts...>) __attribute__((always_inline)) {
-                (step(std::integral_constant<int, ts>{}), ...);
-            }(std::make_integer_sequence<int, 16>{});
-#pragma unroll
-            for (int j = 0; j < 16; ++j) P[(c0 + r) * TLD + c0 + j] = j <= r ? dv[j] : (T)0;
-#pragma unroll
-            for (int q2 = 0; q2 < 16; ++q2) Di[p * 256 + q2 * 16 + r] = x[q2];  // Di[p][row][col]
-#pragma unroll
-            for (int t = 0; t < 16; ++t) rd[c0 + t] = rps[t];
-        }
-        // pflag: the caller's global stores (the sub-diagonal tile) drain on
-        // every wave during block 0's factor; the flag follows the barrier
-        if (pflag && p == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const long long t1 = tdbg ? clock64() : 0;
-        if (pflag && p == 0 && tid == 192) __hip_atomic_store(pflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (dpub && w == 3 && p >= 1) blk_publish_rowblock<T>(Q, dpub, p - 1, tid & 63);
-        // 2. rows below the block, one 16-row block per wave on f64 MFMA
-        //    16x16x4: L[pb][p] = S[pb][p] Di[p]^T (read and written by the same wave)
-        const int l = tid & 63, m = l & 15, kq = l >> 4;
-        if (w < 3 - p) {
-            const int r0 = 16 * (p + 1 + w);
-            bsm_d4 o = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) {
-                const int k = 4 * k4 + kq;
-                o = __builtin_amdgcn_mfma_f64_16x16x4f64((double)P[(r0 + m) * TLD + c0 + k],
-                                                         (double)Di[p * 256 + m * 16 + k], o, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) P[(r0 + kq + 4 * q) * TLD + c0 + m] = (T)o[q];
-        }
-        __syncthreads();
-        const long long t2 = tdbg ? clock64() : 0;
-        // 3. the trailing lower part by 16 x 16 blocks (pi, pj), p < pj <= pi:
-        //    S[pi][pj] -= L[pi][p] L[pj][p]^T, blocks dealt to the waves in turn
-        const int nbk = 3 - p;
-        for (int bk = w; bk < nbk * (nbk + 1) / 2; bk += 4) {
-            int pi = 0, pj = bk;  // bk -> (pi, pj), pj <= pi, both relative to p + 1
-            while (pj > pi) pj -= ++pi;
-            const int i0 = 16 * (p + 1 + pi), j0 = 16 * (p + 1 + pj);
-            bsm_d4 o;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = (double)P[(i0 + kq + 4 * q) * TLD + j0 + m];
-#pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) {
-                const int k = 4 * k4 + kq;
-                o = __builtin_amdgcn_mfma_f64_16x16x4f64(-(double)P[(i0 + m) * TLD + c0 + k],
-                                                         (double)P[(j0 + m) * TLD + c0 + k], o, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) P[(i0 + kq + 4 * q) * TLD + j0 + m] = (T)o[q];
-        }
-        __syncthreads();
-        if (tdbg) {
-            const long long t3 = clock64();
-            ta += t1 - t0;
-            tb += t2 - t1;
-            tc += t3 - t2;
-        }
-    }
-    // Linv's last row block and diagonal block
-    if (w < 3) {
-        blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
-    } else {
-        if (dpub) blk_publish_flag(rbf, 2, tid & 63);
-        blk_linv_diag<T>(Q, Di, 3, tid & 63);
-    }
-    __syncthreads();
-    if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
-    if (tdbg && tid == 0) {
-        __hip_atomic_fetch_add(&tdbg[17], (unsigned long long)ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&tdbg[18], (unsigned long long)tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&tdbg[19], (unsigned long long)tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// X[cb][q] (element (row 16w + (lane >> 4) + 4q, column 16cb + (lane & 15)) of
-// a 64 x 64 tile) += (NEG ? -1 : 1) * sum_k AT[k][row] * B[k][col], one
-// v_mfma_f64_16x16x4 per 16 x 16 block and 4 k: wave w forms rows 16w..16w+15
-// (A operand: lane l holds A[l & 15][l >> 4]; B: B[l >> 4][l & 15]). Two LDS
-// reads per 4 x 16 x 16 FMAs instead of eight per 16 on the VALU. f32 tiles
-// are carried in f64.
-// TRI_B: B[k][c] = 0 for k > c (B = Linv^T), so column block cb stops at k = 16cb + 15.
-template <typename T, bool NEG, bool TRI_B = false>
-__device__ __forceinline__ void mfma_tile(const lds_t<T>* AT, const lds_t<T>* B, T (&X)[4][4], int w, int lane) {
-    bsm_d4 c[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) c[cb][q] = (double)X[cb][q];
-    const int kq = lane >> 4, m = lane & 15;
-#pragma unroll
-    for (int k4 = 0; k4 < 16; ++k4) {
-        const int k = 4 * k4 + kq;
-        double a = (double)AT[k * TLD + 16 * w + m];
-        if (NEG) a = -a;
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-            if (!TRI_B || k4 < 4 * (cb + 1))
-                c[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)B[k * TLD + 16 * cb + m], c[cb], 0, 0, 0);
-        if ((k4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // operand loads of 4 k-steps in flight, not all 16
-    }
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[cb][q] = (T)c[cb][q];
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
-                                                T* __restrict__ Dinv, int* __restrict__ flags,
-                                                int* __restrict__ ticket, int* __restrict__ status,
-                                                unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg,
-                                                int* __restrict__ rbf) {
+__global__ __launch_bounds__(256) void blk_chol(int64_t b, int64_t ld, const CholSeg<T>* __restrict__ segs, int nseg,
+                                                int64_t nb64max, int* __restrict__ ticket, int* __restrict__ status,
+                                                unsigned long long* __restrict__ dbg, unsigned long long* __restrict__ tdbg) {
     __shared__ T PT[64][TLD];  // PT[t][r] = L_{I,J}[r][t], later S^T / the tile
     __shared__ T QT[64][TLD];  // QT[t][c] = L_{K,J}[c][t], later Linv^T
     __shared__ T AT[64][TLD];  // L_{K,K-1}^T as its column blocks form
@@ -1709,7 +1452,13 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
     __shared__ int64_t tk;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t nb64 = (n + 63) / 64, DM = (63 + b) / 64 + 1;  // tiles per block column (incl. diagonal)
+    const int64_t DM = (63 + b) / 64 + 1;  // tiles per block column (incl. diagonal)
+    // the current ticket's segment
+    int64_t n = 0, nb64 = 0;
+    T* CB = nullptr;
+    T* Dinv = nullptr;
+    int* flags = nullptr;
+    int* rbf = nullptr;
     auto wait_flag = [&](const int* f) {
         long long spins = 0;
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -1776,8 +1525,22 @@ __global__ __launch_bounds__(256) void blk_chol(int64_t n, int64_t b, int64_t ld
         if (dbg && tid == 0) __hip_atomic_fetch_max(&dbg[0], (unsigned long long)t0, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_SYSTEM);
         const int64_t t = t0;
-        if (t >= nb64 * DM) break;
-        const int64_t K = t / DM, d = t % DM, I = K + d;
+        if (t >= nb64max * DM * nseg) break;
+        // tickets: block column K of every segment in turn, tiles d within it
+        const int64_t K = t / (DM * nseg), d = t % DM, I = K + d;
+        {
+            const int sg = (int)((t / DM) % nseg);
+            n = segs[sg].n;
+            CB = segs[sg].CB;
+            Dinv = segs[sg].Dinv;
+            flags = segs[sg].flags;
+            rbf = segs[sg].rbf;
+            nb64 = (n + 63) / 64;
+        }
+        if (K >= nb64) {
+            __syncthreads();
+            continue;
+        }
         int* fl = flags + K * DM;
         // no such tile (past the matrix or the band), or the sub-diagonal tile
         // (K + 1, K), which diagonal tile K + 1's workgroup forms
@@ -2442,8 +2205,12 @@ int band_factor_blocked(const bsm_csr* a, Band& bd, DBuf& dinv, hipStream_t s) {
         BSM_HIP_TRY(hipMemsetAsync(tdb.p, 0, 48 * sizeof(unsigned long long), s));
     }
     g_blk_phase = "blk_chol launch";
-    blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(n, bd.b, bd.ld, bd.cb.as<T>(), dinv.as<T>(), flags, tix, st, hdbg,
-                                                tdb.as<unsigned long long>(), rbf);
+    const CholSeg<T> seg{bd.cb.as<T>(), n, dinv.as<T>(), flags, rbf};
+    DBuf segd;
+    BSM_TRY(segd.alloc(sizeof(seg)));
+    BSM_HIP_TRY(hipMemcpyAsync(segd.p, &seg, sizeof(seg), hipMemcpyHostToDevice, s));
+    blk_chol<T><<<(unsigned)grid, 256, 0, s>>>(bd.b, bd.ld, segd.as<CholSeg<T>>(), 1, nb64, tix, st, hdbg,
+                                                tdb.as<unsigned long long>());
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("cholesky", s);
     blk_watchdog(s, "blk_chol", hdbg, (long long)(nb64 * DM), grid, tdb.as<unsigned long long>());
@@ -2723,15 +2490,19 @@ int solve_dispatch_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void*
             BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "blk_trsv does not fit a CU");
             uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
             if (grid > nb64 * k) grid = nb64 * k;
-            blk_trsv<T, true><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), g.as<T>(),
-                                                            mf.as<T>(), bc.as<T>(), (int64_t)n, yp.as<T>(), ff,
+            const TrsvSeg<T> sg[2] = {
+                {bd.cb.as<T>(), (int64_t)n, g.as<T>(), mf.as<T>(), bc.as<T>(), (int64_t)n, yp.as<T>(), ff},
+                {bd.cb.as<T>(), (int64_t)n, h.as<T>(), mb.as<T>(), yp.as<T>(), (int64_t)NP, xp.as<T>(), fb}};
+            DBuf sgd;
+            BSM_TRY(sgd.alloc(sizeof(sg)));
+            BSM_HIP_TRY(hipMemcpyAsync(sgd.p, sg, sizeof(sg), hipMemcpyHostToDevice, s));
+            blk_trsv<T, true><<<(unsigned)grid, 256, 0, s>>>(bd.b, bd.ld, sgd.as<TrsvSeg<T>>(), 1, (int64_t)nb64,
                                                             tix, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
             stage_mark("forward", s);
             blk_watchdog(s, "blk_trsv forward", nullptr, (long long)(nb64 * k), (long long)grid);
-            blk_trsv<T, false><<<(unsigned)grid, 256, 0, s>>>((int64_t)n, bd.b, bd.ld, bd.cb.as<T>(), h.as<T>(),
-                                                             mb.as<T>(), yp.as<T>(), (int64_t)NP, xp.as<T>(), fb,
-                                                             tix + 1, st, (int64_t)k);
+            blk_trsv<T, false><<<(unsigned)grid, 256, 0, s>>>(bd.b, bd.ld, sgd.as<TrsvSeg<T>>() + 1, 1,
+                                                             (int64_t)nb64, tix + 1, st, (int64_t)k);
             BSM_HIP_TRY(hipGetLastError());
             stage_mark("backward", s);
             blk_watchdog(s, "blk_trsv backward", nullptr, (long long)(nb64 * k), (long long)grid);

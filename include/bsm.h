@@ -172,6 +172,25 @@ int bsm_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_col
  * arguments, errors and panics as bsm_solve. This build's addition. */
 int bsm_solve_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
                       void* const* x_cols);
+/* solve (lib.rs:11-24) by a nested-dissection multifrontal Cholesky of
+ * P A P^T: P from recursive BFS level-set bisection of A's graph (host), the
+ * separator tree's dense fronts factored level by level on the device. x is
+ * NOT bit-exact with the reference (another elimination order) but within its
+ * f64 tolerance (1e-6 relative, BASELINE.json north_star). A is its lower
+ * triangle (j <= i) mirrored, as cholesky_decomp reads it; rows must have
+ * strictly increasing columns, and a pivot <= 0 (not SPD) -> BSM_ERR_UNSUPPORTED.
+ * Same arguments and panics as bsm_solve. This build's addition. */
+int bsm_solve_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
+                 void* const* x_cols);
+/* The analysis of bsm_solve_nd alone, on a host pattern (row_ptr n+1, col_idx
+ * row_ptr[n]); no device use (tests, diagnostics). Writes perm (n entries,
+ * perm[new] = old) when non-null; *n_nodes and *st_len always; when cap >=
+ * *n_nodes and st_cap >= *st_len, the tree in post-order as 8 int64 per node
+ * (start, end, parent, level, slot, m, offset into st, 0) and every node's m
+ * front rows (new indices, ascending) into st. This build's addition. */
+int bsm_nd_analyse(uint64_t n, const uint64_t* row_ptr, const uint64_t* col_idx, uint64_t leaf,
+                   int64_t* perm, int64_t* nodes, uint64_t cap, uint64_t* n_nodes, int64_t* st,
+                   uint64_t st_cap, uint64_t* st_len);
 
 /* ---- device-level entry points (HBM pointers, async on `stream`) --------- */
 /* Synthetic CSR generator (bsm_synth.h recipe): rows [row0, row0+rows) of a
