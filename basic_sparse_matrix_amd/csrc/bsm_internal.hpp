@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -232,6 +233,10 @@ struct bsm_csr {
     // cached row-block x column-panel copy (kernels_tiled.hip), same mutex
     mutable bsm_tiled* tiled = nullptr;
     mutable bool tiled_tried = false;
+    // solve(order="nd")'s plan (kernels_nd.hip): the pattern's ordering, tree
+    // and device index arrays, built on first use (the pattern is immutable),
+    // same mutex; released with the handle
+    mutable std::shared_ptr<void> nd_plan;
     // row_ptr / col / vals from the result cache (csr_alloc): their block
     // capacities, 0 = plain hipMalloc (bsm_csr_free hipFrees those)
     size_t cache_cap[3] = {0, 0, 0};

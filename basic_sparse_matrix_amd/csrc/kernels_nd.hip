@@ -455,89 +455,167 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
     L.ext_off.push_back((int64_t)L.ext.size());
 }
 
-template <typename T>
-int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
-    stage_reset(s);
-    const int64_t N = (int64_t)n;
+// A pattern's plan, device side: one allocation holding the node
+// descriptors, front rows, their places in the parents, pinv / owner, the
+// level lists, tiles and extend tasks, and perm; plus the per-level offsets
+// the launches need. Cached on the handle (bsm_csr::nd_plan) unless
+// BSM_ND_CACHE=0: the pattern of a finalised Csr never changes.
+struct NdCached {
+    int64_t leaf = 0;
+    int32_t nn = 0, n_levels = 0;
+    std::vector<int64_t> tiles_off, lvl_off, ext_off;
+    int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
+    size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_perm = 0;
+    size_t n_tiles = 0, n_ext = 0;
+    double ms_graph = 0, ms_order = 0, ms_symbolic = 0;
+    DBuf plan;
+};
+
+// The calling thread's page-locked staging buffer (grown on demand, kept for
+// the thread's later plans): the pattern's download and the plan's upload
+// are direct DMA (~30 MB each at C5) instead of pageable copies.
+int pinned_staging(size_t bytes, char** out) {
+    thread_local char* buf = nullptr;
+    thread_local size_t cap = 0;
+    if (cap < bytes) {
+        if (buf) (void)hipHostFree(buf);
+        buf = nullptr;
+        cap = 0;
+        const size_t want = std::max(bytes, cap * 2);
+        BSM_HIP_TRY(hipHostMalloc((void**)&buf, want, hipHostMallocDefault));
+        cap = want;
+    }
+    *out = buf;
+    return BSM_OK;
+}
+
+int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
+    const int64_t N = (int64_t)a->rows;
     // A's pattern to the host for the analysis
-    std::vector<int64_t> rp((size_t)N + 1);
-    std::vector<int32_t> cl((size_t)a->nnz);
-    BSM_HIP_TRY(hipMemcpyAsync(rp.data(), a->row_ptr, (size_t)(N + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    char* stg = nullptr;
+    const size_t rp_bytes = ((size_t)(N + 1) * sizeof(int64_t) + 255) / 256 * 256;
+    BSM_TRY(pinned_staging(rp_bytes + (size_t)a->nnz * sizeof(int32_t), &stg));
+    const int64_t* rp = (const int64_t*)stg;
+    const int32_t* cl = (const int32_t*)(stg + rp_bytes);
+    BSM_HIP_TRY(hipMemcpyAsync(stg, a->row_ptr, (size_t)(N + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     if (a->nnz)
-        BSM_HIP_TRY(hipMemcpyAsync(cl.data(), a->col, (size_t)a->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipMemcpyAsync(stg + rp_bytes, a->col, (size_t)a->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
     stage_mark("nd_pattern_d2h", s);
-    const char* le = getenv("BSM_ND_LEAF");
     const char* te = getenv("BSM_ND_THREADS");
-    const int64_t leaf = le ? atoll(le) : 256;
-    int threads = te ? atoi(te) : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    const int threads = te ? atoi(te) : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
     NdPlan P;
-    const int arc = nd_analyse(N, rp.data(), cl.data(), leaf, threads, P);
+    const int arc = nd_analyse(N, rp, cl, leaf, threads, P);
     BSM_REQUIRE(arc == 0, BSM_ERR_UNSUPPORTED,
                 "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
     NdLayout L;
     nd_layout(P, L);
+    C.leaf = leaf;
+    C.nn = (int32_t)L.dev.size();
+    C.n_levels = P.n_levels;
+    C.tiles_off = L.tiles_off;
+    C.lvl_off = L.lvl_off;
+    C.ext_off = L.ext_off;
+    C.f_elems = L.f_elems;
+    C.dinv_elems = L.dinv_elems;
+    C.n_flags = L.n_flags;
+    C.vtot = L.vtot;
+    C.n_tiles = L.tiles.size();
+    C.n_ext = L.ext.size();
+    C.ms_graph = P.ms_graph;
+    C.ms_order = P.ms_order;
+    C.ms_symbolic = P.ms_symbolic;
+    for (const auto& d : L.dev) C.max_front = std::max<int64_t>(C.max_front, d.ld);
     stage_mark("nd_analyse", s);
-    if (getenv("BSM_ND_TRACE")) {
-        int64_t mx = 0;
-        for (const auto& d : L.dev) mx = std::max<int64_t>(mx, d.ld);
-        fprintf(stderr,
-                "[bsm nd] n %lld nodes %zu levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms; fronts "
-                "%.3f GB (largest %lld), tiles %zu, extend columns %zu\n",
-                (long long)N, L.dev.size(), P.n_levels, P.ms_graph, P.ms_order, P.ms_symbolic,
-                (double)L.f_elems * sizeof(T) * 1e-9, (long long)mx, L.tiles.size(), L.ext.size());
-    }
-    // device plan: one upload of the packed arrays
-    const int32_t nn = (int32_t)L.dev.size();
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-    const size_t o_dev = 0, o_st = o_dev + al(L.dev.size() * sizeof(NdDev)),
-                 o_ri = o_st + al(L.st.size() * 4), o_pinv = o_ri + al(L.ri.size() * 4),
-                 o_owner = o_pinv + al(L.pinv.size() * 4), o_lvl = o_owner + al(L.owner.size() * 4),
-                 o_tiles = o_lvl + al(L.lvl_nodes.size() * 4), o_ext = o_tiles + al(L.tiles.size() * sizeof(int4)),
-                 o_perm = o_ext + al(L.ext.size() * sizeof(int2)), total = o_perm + al((size_t)N * 8);
-    std::vector<char> hp(total);
+    C.o_dev = 0;
+    C.o_st = C.o_dev + al(L.dev.size() * sizeof(NdDev));
+    C.o_ri = C.o_st + al(L.st.size() * 4);
+    C.o_pinv = C.o_ri + al(L.ri.size() * 4);
+    C.o_owner = C.o_pinv + al(L.pinv.size() * 4);
+    C.o_lvl = C.o_owner + al(L.owner.size() * 4);
+    C.o_tiles = C.o_lvl + al(L.lvl_nodes.size() * 4);
+    C.o_ext = C.o_tiles + al(L.tiles.size() * sizeof(int4));
+    C.o_perm = C.o_ext + al(L.ext.size() * sizeof(int2));
+    const size_t total = C.o_perm + al((size_t)N * 8);
+    char* hp = nullptr;
+    BSM_TRY(pinned_staging(total, &hp));  // the pattern is no longer needed
     auto put = [&](size_t o, const void* p, size_t b) {
-        if (b) memcpy(hp.data() + o, p, b);
+        if (b) memcpy(hp + o, p, b);
     };
-    put(o_dev, L.dev.data(), L.dev.size() * sizeof(NdDev));
-    put(o_st, L.st.data(), L.st.size() * 4);
-    put(o_ri, L.ri.data(), L.ri.size() * 4);
-    put(o_pinv, L.pinv.data(), L.pinv.size() * 4);
-    put(o_owner, L.owner.data(), L.owner.size() * 4);
-    put(o_lvl, L.lvl_nodes.data(), L.lvl_nodes.size() * 4);
-    put(o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
-    put(o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
-    put(o_perm, P.perm.data(), (size_t)N * 8);
-    DBuf plan;
-    BSM_TRY(plan.alloc(total));
-    BSM_HIP_TRY(hipMemcpyAsync(plan.p, hp.data(), total, hipMemcpyHostToDevice, s));
-    char* pb = plan.as<char>();
-    const NdDev* d_nodes = (const NdDev*)(pb + o_dev);
-    const int32_t* d_st = (const int32_t*)(pb + o_st);
-    const int32_t* d_ri = (const int32_t*)(pb + o_ri);
-    const int32_t* d_pinv = (const int32_t*)(pb + o_pinv);
-    const int32_t* d_owner = (const int32_t*)(pb + o_owner);
-    const int32_t* d_lvl = (const int32_t*)(pb + o_lvl);
-    const int4* d_tiles = (const int4*)(pb + o_tiles);
-    const int2* d_ext = (const int2*)(pb + o_ext);
-    const int64_t* d_perm = (const int64_t*)(pb + o_perm);
+    put(C.o_dev, L.dev.data(), L.dev.size() * sizeof(NdDev));
+    put(C.o_st, L.st.data(), L.st.size() * 4);
+    put(C.o_ri, L.ri.data(), L.ri.size() * 4);
+    put(C.o_pinv, L.pinv.data(), L.pinv.size() * 4);
+    put(C.o_owner, L.owner.data(), L.owner.size() * 4);
+    put(C.o_lvl, L.lvl_nodes.data(), L.lvl_nodes.size() * 4);
+    put(C.o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
+    put(C.o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
+    put(C.o_perm, P.perm.data(), (size_t)N * 8);
+    BSM_TRY(C.plan.alloc(total));
+    BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
+    stage_mark("nd_upload", s);
+    return BSM_OK;
+}
+
+template <typename T>
+int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
+    stage_reset(s);
+    const int64_t N = (int64_t)n;
+    const char* le = getenv("BSM_ND_LEAF");
+    const char* ce = getenv("BSM_ND_CACHE");
+    const int64_t leaf = le ? atoll(le) : 256;
+    const bool cache = !(ce && atoi(ce) == 0);
+    std::shared_ptr<NdCached> pc;
+    if (cache) {
+        std::lock_guard<std::mutex> lk(a->plan_mu);
+        auto c = std::static_pointer_cast<NdCached>(a->nd_plan);
+        if (c && c->leaf == leaf) pc = c;
+    }
+    if (pc) {
+        stage_mark("nd_plan_cached", s);
+    } else {
+        pc = std::make_shared<NdCached>();
+        BSM_TRY(nd_build_plan(a, leaf, s, *pc));
+        if (cache) {
+            std::lock_guard<std::mutex> lk(a->plan_mu);
+            a->nd_plan = pc;
+        }
+    }
+    const NdCached& C = *pc;
+    if (getenv("BSM_ND_TRACE"))
+        fprintf(stderr,
+                "[bsm nd] n %lld nodes %d levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms; fronts "
+                "%.3f GB (largest %lld), tiles %zu, extend columns %zu\n",
+                (long long)N, C.nn, C.n_levels, C.ms_graph, C.ms_order, C.ms_symbolic,
+                (double)C.f_elems * sizeof(T) * 1e-9, (long long)C.max_front, C.n_tiles, C.n_ext);
+    char* pb = C.plan.as<char>();
+    const NdDev* d_nodes = (const NdDev*)(pb + C.o_dev);
+    const int32_t* d_st = (const int32_t*)(pb + C.o_st);
+    const int32_t* d_ri = (const int32_t*)(pb + C.o_ri);
+    const int32_t* d_pinv = (const int32_t*)(pb + C.o_pinv);
+    const int32_t* d_owner = (const int32_t*)(pb + C.o_owner);
+    const int32_t* d_lvl = (const int32_t*)(pb + C.o_lvl);
+    const int4* d_tiles = (const int4*)(pb + C.o_tiles);
+    const int2* d_ext = (const int2*)(pb + C.o_ext);
+    const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
     // numeric storage
     DBuf fr, dv, fl;
-    BSM_TRY(fr.alloc((size_t)L.f_elems * sizeof(T)));
-    BSM_TRY(dv.alloc((size_t)std::max<int64_t>(L.dinv_elems, 1) * sizeof(T)));
-    const size_t nfl = (size_t)L.n_flags + (size_t)P.n_levels + 2;
+    BSM_TRY(fr.alloc((size_t)C.f_elems * sizeof(T)));
+    BSM_TRY(dv.alloc((size_t)std::max<int64_t>(C.dinv_elems, 1) * sizeof(T)));
+    const size_t nfl = (size_t)C.n_flags + (size_t)C.n_levels + 2;
     BSM_TRY(fl.alloc(nfl * sizeof(int)));
-    BSM_HIP_TRY(hipMemsetAsync(fr.p, 0, (size_t)L.f_elems * sizeof(T), s));
+    BSM_HIP_TRY(hipMemsetAsync(fr.p, 0, (size_t)C.f_elems * sizeof(T), s));
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* d_flags = fl.as<int>();
-    int* d_tickets = d_flags + L.n_flags;
-    int* d_status = d_tickets + P.n_levels;
+    int* d_tickets = d_flags + C.n_flags;
+    int* d_status = d_tickets + C.n_levels;
     T* F = fr.as<T>();
-    stage_mark("nd_upload", s);
     nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals), d_pinv,
                                                      d_owner, d_nodes, d_st, F);
     BSM_HIP_TRY(hipGetLastError());
-    nd_pad_pivots<T><<<(unsigned)nn, 64, 0, s>>>(d_nodes, F);
+    nd_pad_pivots<T><<<(unsigned)C.nn, 64, 0, s>>>(d_nodes, F);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("nd_assemble", s);
     int dev = 0, cus = 0, per_cu = 0;
@@ -545,8 +623,8 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nd_factor<T>, 256, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "nd_factor does not fit a CU");
-    for (int32_t lv = 0; lv < P.n_levels; ++lv) {
-        const int64_t t0 = L.tiles_off[(size_t)lv], nt = L.tiles_off[(size_t)lv + 1] - t0;
+    for (int32_t lv = 0; lv < C.n_levels; ++lv) {
+        const int64_t t0 = C.tiles_off[(size_t)lv], nt = C.tiles_off[(size_t)lv + 1] - t0;
         if (nt > 0) {
             const int64_t grid = std::min<int64_t>(nt, (int64_t)cus * per_cu);
             nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
@@ -554,7 +632,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             BSM_HIP_TRY(hipGetLastError());
         }
         for (int sl = 0; sl < 2; ++sl) {
-            const int64_t e0 = L.ext_off[(size_t)(2 * lv + sl)], ne = L.ext_off[(size_t)(2 * lv + sl) + 1] - e0;
+            const int64_t e0 = C.ext_off[(size_t)(2 * lv + sl)], ne = C.ext_off[(size_t)(2 * lv + sl) + 1] - e0;
             if (ne <= 0) continue;
             nd_extend<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext + e0, ne, d_ri, F);
             BSM_HIP_TRY(hipGetLastError());
@@ -564,23 +642,23 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     if (k > 0) {
         DBuf bpb, vb;
         BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T)));
-        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(L.vtot, 1) * k * sizeof(T)));
+        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T)));
         nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
                                                        bpb.as<T>());
         BSM_HIP_TRY(hipGetLastError());
-        for (int32_t lv = 0; lv < P.n_levels; ++lv) {
-            const int64_t o = L.lvl_off[(size_t)lv], c = L.lvl_off[(size_t)lv + 1] - o;
+        for (int32_t lv = 0; lv < C.n_levels; ++lv) {
+            const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
             if (c <= 0) continue;
             nd_forward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
-                                                                        vb.as<T>(), L.vtot, F, dv.as<T>(), d_ri);
+                                                                        vb.as<T>(), C.vtot, F, dv.as<T>(), d_ri);
             BSM_HIP_TRY(hipGetLastError());
         }
         stage_mark("nd_forward", s);
-        for (int32_t lv = P.n_levels - 1; lv >= 0; --lv) {
-            const int64_t o = L.lvl_off[(size_t)lv], c = L.lvl_off[(size_t)lv + 1] - o;
+        for (int32_t lv = C.n_levels - 1; lv >= 0; --lv) {
+            const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
             if (c <= 0) continue;
             nd_backward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
-                                                                         vb.as<T>(), L.vtot, F, dv.as<T>(), d_st);
+                                                                         vb.as<T>(), C.vtot, F, dv.as<T>(), d_st);
             BSM_HIP_TRY(hipGetLastError());
         }
         stage_mark("nd_backward", s);

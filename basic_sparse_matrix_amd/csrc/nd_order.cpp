@@ -30,6 +30,7 @@ double ms_since(Clock::time_point t0) {
 // the undirected graph of A: an edge {i, j} per stored lower entry j < i
 struct Graph {
     int64_t n = 0;
+    int64_t band = 0;  // max i - j over the stored lower entries
     std::vector<int64_t> xadj;
     std::vector<int32_t> adj;
 };
@@ -45,6 +46,7 @@ bool build_graph(int64_t n, const int64_t* rp, const int32_t* col, Graph& g) {
             if (j < i) {
                 ++g.xadj[i + 1];
                 ++g.xadj[j + 1];
+                g.band = std::max(g.band, i - j);
             }
         }
     for (int64_t i = 0; i < n; ++i) g.xadj[i + 1] += g.xadj[i];
@@ -74,6 +76,7 @@ struct Bisect {
     int64_t leaf;
     int par_depth;
     std::vector<int32_t> mark, lvl, seen;
+    int64_t band = 0;  // max |i - j| over the edges (natural order)
     std::deque<TNode> tree;
     std::mutex mu;
     std::atomic<int32_t> stamp{0};
@@ -90,6 +93,14 @@ struct Bisect {
     TNode& node(int32_t i) {  // deque: references survive later emplace_back
         std::lock_guard<std::mutex> l(mu);
         return tree[(size_t)i];
+    }
+
+    // v itself if tagged `tag`, else a neighbour tagged `tag`, else -1 (search)
+    int32_t near_in(int32_t v, int32_t tag) const {
+        if (v < 0 || mark[v] == tag) return v;
+        for (int64_t e = g.xadj[v]; e < g.xadj[v + 1]; ++e)
+            if (mark[g.adj[e]] == tag) return g.adj[e];
+        return -1;
     }
 
     // BFS from s over the vertices tagged `tag`, appended to order; levels in lvl
@@ -112,14 +123,33 @@ struct Bisect {
         }
     }
 
-    void run(std::vector<int32_t> verts, int32_t id, int depth) {
+    // hint >= 0: a vertex of the part to root the level structure at (no
+    // search for a far vertex); else the first BFS finds one
+    void run(std::vector<int32_t> verts, int32_t id, int depth, int32_t hint) {
         if ((int64_t)verts.size() <= leaf) {
             node(id).own = std::move(verts);
             return;
         }
         std::vector<int32_t> order, A, B, S;
+        if (depth == 0 && band > 0 && (int64_t)verts.size() >= 8 * band) {
+            // a narrow band in the natural order (a mesh numbered row by row):
+            // any band consecutive indices separate those below from those
+            // above, so the root's cut needs no BFS (the two of a 1M-vertex
+            // part are the largest serial step of the bisection)
+            const int64_t n = (int64_t)verts.size(), lo = (n - band) / 2, hi = lo + band;
+            for (int64_t v = 0; v < n; ++v) {
+                if (v < lo) A.push_back((int32_t)v);
+                else if (v >= hi) B.push_back((int32_t)v);
+            }
+            for (int64_t v = lo; v < hi; ++v) {
+                bool beyond = false;  // a separator vertex with no neighbour above joins A
+                for (int64_t e = g.xadj[v]; e < g.xadj[v + 1] && !beyond; ++e) beyond = g.adj[e] >= hi;
+                (beyond ? S : A).push_back((int32_t)v);
+            }
+            std::sort(A.begin(), A.end());
+        } else {
         order.reserve(verts.size());
-        bfs(verts[0], id, stamp++, order);
+        bfs(hint >= 0 ? hint : verts[0], id, stamp++, order);
         if (order.size() < verts.size()) {
             // disconnected: whole components to the smaller side, no separator
             const int32_t sid = stamp++;
@@ -140,9 +170,11 @@ struct Bisect {
         } else {
             // level structure from a far vertex (the last one reached), its
             // middle level the separator
-            const int32_t u = order.back();
-            order.clear();
-            bfs(u, id, stamp++, order);
+            if (hint < 0) {
+                const int32_t u = order.back();
+                order.clear();
+                bfs(u, id, stamp++, order);
+            }
             const int32_t D = lvl[order.back()];
             if (D < 2) {  // no level to cut at (a clique-like part): one dense front
                 node(id).own = std::move(verts);
@@ -175,6 +207,12 @@ struct Bisect {
                 }
             }
         }
+        }
+        // the children's roots: the separator's first vertex reached (an end
+        // of the cut, so the next cut runs across this one); without a
+        // separator, a search
+        int32_t ha = -1, hb = -1;
+        if (!S.empty() && !(depth == 0 && order.empty())) ha = hb = S.front();
         const int32_t ka = new_node(), kb = new_node();
         for (int32_t v : A) mark[v] = ka;
         for (int32_t v : B) mark[v] = kb;
@@ -185,13 +223,17 @@ struct Bisect {
             me.kid[0] = ka;
             me.kid[1] = kb;
         }
+        if (ha >= 0) {  // a separator vertex is no longer in the parts: its neighbour there
+            ha = near_in(ha, ka);
+            hb = near_in(hb, kb);
+        }
         if (depth < par_depth) {
-            std::thread t([&, ka] { run(std::move(A), ka, depth + 1); });
-            run(std::move(B), kb, depth + 1);
+            std::thread t([&, ka, ha] { run(std::move(A), ka, depth + 1, ha); });
+            run(std::move(B), kb, depth + 1, hb);
             t.join();
         } else {
-            run(std::move(A), ka, depth + 1);
-            run(std::move(B), kb, depth + 1);
+            run(std::move(A), ka, depth + 1, ha);
+            run(std::move(B), kb, depth + 1, hb);
         }
     }
 };
@@ -218,7 +260,8 @@ int nd_analyse(int64_t n, const int64_t* row_ptr, const int32_t* col, int64_t le
     {
         std::vector<int32_t> all((size_t)n);
         for (int64_t i = 0; i < n; ++i) all[(size_t)i] = (int32_t)i;
-        bs.run(std::move(all), root, 0);
+        bs.band = g.band;
+        bs.run(std::move(all), root, 0, -1);
     }
 
     // post-order numbering: kid 0's subtree, kid 1's, then the node's own vertices
@@ -325,7 +368,9 @@ extern "C" int bsm_nd_analyse(uint64_t n, const uint64_t* row_ptr, const uint64_
         cl[(size_t)e] = (int32_t)col_idx[e];
     }
     bsm::NdPlan P;
-    if (bsm::nd_analyse((int64_t)n, rp.data(), cl.data(), (int64_t)leaf, 4, P) != 0) return BSM_ERR_UNSUPPORTED;
+    const char* te = getenv("BSM_ND_THREADS");
+    if (bsm::nd_analyse((int64_t)n, rp.data(), cl.data(), (int64_t)leaf, te ? atoi(te) : 4, P) != 0)
+        return BSM_ERR_UNSUPPORTED;
     *n_nodes = P.nodes.size();
     uint64_t total = 0;
     for (const auto& x : P.nodes) total += x.st.size();
