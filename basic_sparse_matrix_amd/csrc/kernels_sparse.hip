@@ -1017,6 +1017,96 @@ struct CsrGuard {  // frees a half-built output on error paths
     bsm_csr* release() { bsm_csr* r = m; m = nullptr; return r; }
 };
 
+// ---- add / sub, rows of moderate length: one wave per row -------------------
+// When no row has more than WROW_CAP entries on its two sides together (the
+// handles' analysed max row lengths say so, no device round trip), each row
+// is one 64-lane workgroup: the wave stages the row's two sides in LDS
+// (coalesced), lane 0 runs the reference's two-pointer merge (merge_range,
+// sparse.rs:493-532) out of LDS and writes the kept outputs at the row's
+// upper-bound slot (arp[r] + brp[r]); a scan of the counts and a copy place
+// them. One host sync per call (the result's nnz), against the count / long
+// row / piece pipeline's five (§6b: the fixed cost of ss_add at e <= 200k).
+constexpr int WROW_CAP = 2048;
+
+template <typename T, bool SUB>
+__global__ __launch_bounds__(64) void addsub_wave(const int64_t* __restrict__ arp, const int32_t* __restrict__ acol,
+                                                  const T* __restrict__ av, const int64_t* __restrict__ brp,
+                                                  const int32_t* __restrict__ bcol, const T* __restrict__ bv,
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ tcol,
+                                                  T* __restrict__ tval) {
+    __shared__ int32_t sc[WROW_CAP];
+    __shared__ T sv[WROW_CAP];
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t a0 = arp[r], la = arp[r + 1] - a0, b0 = brp[r], lb = brp[r + 1] - b0;
+    for (int64_t i = lane; i < la; i += 64) {
+        sc[i] = acol[a0 + i];
+        sv[i] = av[a0 + i];
+    }
+    for (int64_t i = lane; i < lb; i += 64) {
+        sc[la + i] = bcol[b0 + i];
+        sv[la + i] = bv[b0 + i];
+    }
+    __syncthreads();
+    if (lane == 0) {
+        const int64_t base = a0 + b0;
+        int32_t n = 0;
+        merge_range<T, SUB>(0, la, la, la + lb, sc, sv, sc, sv, [&](int32_t c, T v) {
+            if (Arith<T>::nz(v)) {
+                tcol[base + n] = c;
+                tval[base + n] = v;
+                ++n;
+            }
+        });
+        cnt[r] = n;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void addsub_place(const int64_t* __restrict__ arp, const int64_t* __restrict__ brp,
+                                                   const int64_t* __restrict__ orp, const int32_t* __restrict__ tcol,
+                                                   const T* __restrict__ tval, int32_t* __restrict__ ocol,
+                                                   T* __restrict__ ov) {
+    const int64_t r = blockIdx.x, src = arp[r] + brp[r], dst = orp[r], n = orp[r + 1] - dst;
+    for (int64_t i = threadIdx.x; i < n; i += 64) {
+        ocol[dst + i] = tcol[src + i];
+        ov[dst + i] = tval[src + i];
+    }
+}
+
+int addsub_wave_path(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr** out, hipStream_t s) {
+    const uint64_t rows = a->rows, ub = a->nnz + b->nnz;
+    CsrGuard g;
+    DBuf cnt, orp, ws, tcol, tval;
+    auto run = [&]<typename T, bool SUB>() -> int {
+        BSM_TRY(cnt.alloc(rows * sizeof(int32_t), s));
+        BSM_TRY(orp.alloc((rows + 1) * sizeof(int64_t), s));
+        BSM_TRY(ws.alloc(scan_workspace_bytes(rows), s));
+        BSM_TRY(tcol.alloc((ub + 1) * sizeof(int32_t), s));
+        BSM_TRY(tval.alloc((ub + 1) * sizeof(T), s));
+        addsub_wave<T, SUB><<<(unsigned)rows, 64, 0, s>>>(a->row_ptr, a->col, static_cast<const T*>(a->vals),
+                                                         b->row_ptr, b->col, static_cast<const T*>(b->vals),
+                                                         cnt.as<int32_t>(), tcol.as<int32_t>(), tval.as<T>());
+        BSM_HIP_TRY(hipGetLastError());
+        BSM_TRY(exclusive_scan_i32_to_i64(cnt.as<int32_t>(), orp.as<int64_t>(), rows, ws.p, ws.bytes, s));
+        // the output at the nnz(a) + nnz(b) bound: its count arrives with the call's one sync
+        BSM_TRY(csr_alloc(&g.m, a->dtype, rows, a->cols, ub));
+        BSM_HIP_TRY(hipMemcpyAsync(g.m->row_ptr, orp.p, (rows + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        addsub_place<T><<<(unsigned)rows, 64, 0, s>>>(a->row_ptr, b->row_ptr, orp.as<int64_t>(), tcol.as<int32_t>(),
+                                                      tval.as<T>(), g.m->col, static_cast<T*>(g.m->vals));
+        BSM_HIP_TRY(hipGetLastError());
+        int64_t nnz = 0;
+        BSM_HIP_TRY(read_dev(&nnz, orp.as<int64_t>() + rows, sizeof(int64_t), s));  // syncs the stream
+        g.m->nnz = (uint64_t)nnz;
+        return BSM_OK;
+    };
+    BSM_TRY(dispatch_dtype(a->dtype, [&]<typename T>() -> int {
+        return sub ? run.template operator()<T, true>() : run.template operator()<T, false>();
+    }));
+    *out = g.release();
+    return BSM_OK;
+}
+
 }  // namespace
 
 int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr** out, hipStream_t s) {
@@ -1026,6 +1116,13 @@ int sparse_addsub_dispatch(const bsm_csr* a, const bsm_csr* b, bool sub, bsm_csr
     BSM_REQUIRE(a->rows > 0, BSM_ERR_PANIC,
                 "%s on a matrix with 0 rows: the reference's row loop never terminates (sparse.rs:%s)",
                 sub ? "sub_sparse" : "add_sparse", sub ? "593-596" : "533-537");
+    // every row short enough for one wave (the operands' analysed longest
+    // rows; a device-built operand not yet analysed takes the general path);
+    // BSM_SS_WAVE=0: the general path always (A/B)
+    const bool wave_ok = !getenv("BSM_SS_WAVE") || atoi(getenv("BSM_SS_WAVE")) != 0;
+    if (wave_ok && a->analysed && b->analysed && a->max_row_len + b->max_row_len <= (uint64_t)WROW_CAP &&
+        (a->nnz + b->nnz) * (sizeof(int32_t) + dtype_size(a->dtype)) <= (1ull << 30))
+        return addsub_wave_path(a, b, sub, out, s);
     const uint64_t rows = a->rows;
     DBuf cnt, lflag, lpos, ws;
     CsrGuard g;

@@ -230,6 +230,11 @@ int create_streams(bsm_multi* c) {
                 const int in_xcd = linear ? b % per_xcd : b / 8;
                 (in_xcd < keep ? mm : mc)[b / 32] |= 1u << (b % 32);
             }
+            // NOTE: hipExtStreamCreateWithCUMask takes no flags, so these two
+            // streams are BLOCKING with respect to the null stream (the
+            // unmasked ones below are hipStreamNonBlocking): null-stream work
+            // (pageable copies, hipMemset without a stream) serialises against
+            // them. The round-4 CU-mask A/B ran this way.
             BSM_HIP_TRY(hipExtStreamCreateWithCUMask(&c->compute[i], (uint32_t)mc.size(), mc.data()));
             BSM_HIP_TRY(hipExtStreamCreateWithCUMask(&c->comm[i], (uint32_t)mm.size(), mm.data()));
         } else {

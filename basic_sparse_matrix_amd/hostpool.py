@@ -109,13 +109,14 @@ class HostPool:
                     if cap <= m.cap <= cap + cap // 4 + _HUGE and (best is None or m.cap < self._free[best].cap):
                         best = i
                 m = self._free.pop(best) if best is not None else None
+                if m is not None:  # out of the free bytes before the queued give-backs trim to `keep`
+                    self._free_bytes -= m.cap
             finally:
                 self._busy = False
                 pending, self._pending = self._pending, []
                 for p in pending:
                     self._give_back(p)
             if m is not None:
-                self._free_bytes -= m.cap
                 self.hits += 1
                 return m
             self.misses += 1

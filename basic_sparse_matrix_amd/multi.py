@@ -39,6 +39,8 @@ PLAN_KEYS = ("total", "tiled_count", "tiled_scan", "tiled_alloc", "tiled_write",
 def partition_rows(row_ptr, pieces: int) -> np.ndarray:
     """bsm_partition_rows: the piece bounds the library uses (host only)."""
     rp = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+    if rp.size == 0:  # row_ptr holds rows + 1 entries: empty is not a matrix (rows would wrap to 2^64 - 1)
+        raise ValueError("partition_rows: row_ptr must hold rows + 1 entries, got an empty array")
     out = np.empty(pieces + 1, dtype=np.uint64)
     _lib.check(_lib.load().bsm_partition_rows(_lib.ptr(rp), rp.size - 1, pieces, _lib.ptr(out)))
     return out

@@ -324,7 +324,8 @@ int bsm_multi_create_rank(const void* id, int world, int rank, int device, bsm_m
 int bsm_multi_create_external(int world, int rank, int device, bsm_multi** out);
 int bsm_multi_is_external(const bsm_multi* ctx, int* external);
 /* The piece bounds the multi-GPU path uses (host only, no device needed):
- * bounds[0..pieces] for row_ptr[0..rows]. */
+ * bounds[0..pieces] for row_ptr[0..rows]. row_ptr must hold rows + 1 entries
+ * (it is not validated against anything: rows is trusted). */
 int bsm_partition_rows(const uint64_t* row_ptr, uint64_t rows, uint32_t pieces, uint64_t* bounds);
 /* world size, devices driven by this process, global rank of the first one */
 int bsm_multi_info(const bsm_multi* ctx, int* world, int* n_local, int* first_rank);

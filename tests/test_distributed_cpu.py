@@ -131,6 +131,15 @@ def _worker(rank, world, port, chunks, rows, kind, result_q):
     dist.destroy_process_group()
 
 
+def test_partition_rows_rejects_empty_row_ptr():
+    """row_ptr holds rows + 1 entries; an empty array is refused in Python
+    (the C entry point trusts rows)."""
+    from basic_sparse_matrix_amd.multi import partition_rows as lib_partition
+
+    with pytest.raises(ValueError):
+        lib_partition(np.zeros(0, dtype=np.uint64), 4)
+
+
 @pytest.mark.parametrize("world,chunks,rows,kind", [
     (2, 1, 997, 1), (2, 3, 997, 1), (3, 1, 601, 1), (3, 4, 1000, 1),
     (3, 2, 600, 0),   # equal pieces

@@ -72,9 +72,15 @@ def unsorted_random(rng, e, rows, cols, dtype, seed_shift=0):
 DTYPES = [np.float64, np.float32, np.int32, np.uint32, np.int64, np.uint64]
 
 
+@pytest.mark.parametrize("path", ["wave", "general"])
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("kind", ["sorted", "unsorted"])
-def test_add_sub_vs_oracle(orc, dtype, kind):
+def test_add_sub_vs_oracle(orc, monkeypatch, dtype, kind, path):
+    """Both add/sub paths: one wave per row when every row fits one wave's
+    LDS (addsub_wave, the default for such operands), and the general
+    count / long-row / piece pipeline (BSM_SS_WAVE=0)."""
+    if path == "general":
+        monkeypatch.setenv("BSM_SS_WAVE", "0")
     rng = np.random.default_rng(11)
     if kind == "sorted":
         a, b = sorted_random(rng, 120, 90, 0.1, dtype), sorted_random(rng, 120, 90, 0.1, dtype)
@@ -83,6 +89,35 @@ def test_add_sub_vs_oracle(orc, dtype, kind):
     assert_csr_bits(a.add_sparse(b), *orc.add_sparse(arrays(a), arrays(b)))
     assert_csr_bits(a.sub_sparse(b), *orc.sub_sparse(arrays(a), arrays(b)))
     assert_csr_bits(b.sub_sparse(a), *orc.sub_sparse(arrays(b), arrays(a)))
+
+
+@pytest.mark.parametrize("path", ["wave", "general"])
+@pytest.mark.parametrize("dtype", [np.float64, np.uint32, np.int64])
+def test_add_sub_moderate_unsorted_rows(orc, monkeypatch, dtype, path):
+    """Rows of 0 to 1,000 entries per side (the wave path's range, up to its
+    2,048-entry cap together) with unsorted and repeated columns: the merge's
+    every branch (greater, less, equal, one side exhausted) inside one wave's
+    LDS, and rows with zero results dropped."""
+    if path == "general":
+        monkeypatch.setenv("BSM_SS_WAVE", "0")
+    rng = np.random.default_rng(23)
+    rows, cols = 400, 300
+
+    def make():
+        lens = rng.integers(0, 1001, rows)
+        lens[:3] = [0, 1000, 1]
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        ci = rng.integers(0, cols, int(rp[-1])).astype(np.uint64)
+        if np.dtype(dtype).kind == "f":
+            v = rng.integers(-2, 3, int(rp[-1])).astype(dtype)  # zeros and exact cancellations
+        else:
+            v = rng.integers(1, 4, int(rp[-1])).astype(dtype)
+        return Csr.from_csr_arrays((rows, cols), rp, ci, v)
+
+    a, b = make(), make()
+    for op, ref in [(Csr.add_sparse, orc.add_sparse), (Csr.sub_sparse, orc.sub_sparse)]:
+        assert_csr_bits(op(a, b), *ref(arrays(a), arrays(b)))
+        assert_csr_bits(op(b, a), *ref(arrays(b), arrays(a)))
 
 
 def test_sub_exact_cancellation(orc):
