@@ -738,6 +738,17 @@ Dense<T> solve_blocked(Csr<T> a, Dense<T> b) {
     return detail::run_solver<T>(bsm_solve_blocked, a, b);
 }
 
+/// solve by a nested-dissection multifrontal factor of P A P^T (bsm_solve_nd;
+/// this build's addition): within the f64 tolerance, not bit-exact; the
+/// ordering plan is cached on the device handle; same errors/panics.
+template <class T>
+    requires std::is_floating_point_v<T>
+Dense<T> solve_nd(Csr<T> a, Dense<T> b) {
+    if (a.get_dims().rows != a.get_dims().cols)
+        throw Panic("called `Result::unwrap()` on an `Err` value: NonSquareMatrix");
+    return detail::run_solver<T>(bsm_solve_nd, a, b);
+}
+
 }  // namespace bsm
 
 #endif  // BSM_HPP

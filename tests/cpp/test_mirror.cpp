@@ -377,6 +377,14 @@ GPU_TEST(solve_poisson_f64_vs_band_oracle) {
         den += ex[i] * ex[i];
     }
     CHECK(std::sqrt(num / den) < 1e-10);
+    // the nested-dissection solve: the same tolerance
+    auto xn = bsm::solve_nd(a, Dense<double>::from_data({b}));
+    num = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const double e = xn.get_col(0)[i] - ex[i];
+        num += e * e;
+    }
+    CHECK(std::sqrt(num / den) < 1e-10);
 }
 
 int main(int argc, char** argv) {
