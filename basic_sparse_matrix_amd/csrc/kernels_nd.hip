@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 //     K < npt, I >  K: L_IK = S L_KK^-T                    (flag)
 //     K >= npt       : U_IK = S (the update block, for nd_extend)
 template <typename T>
-__global__ __launch_bounds__(256) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
+__global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
                                                  int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
                                                  int* __restrict__ flags, int* __restrict__ ticket,
                                                  int* __restrict__ status) {
@@ -127,14 +127,16 @@ __global__ __launch_bounds__(256) void nd_factor(const NdDev* __restrict__ nodes
         const int64_t ld = nd.ld;
         T* const Fn = F + nd.foff;
         int* const fl = flags + nd.flag_off;
-        // X[t][r] = L[64 I2 + r][64 J + t] (sc1: other workgroups wrote it)
-        auto stage = [&](T (*X)[TLD], int I2, int J) {
-            T v[16];
+        // tile (I2, J) of L into registers (sc1: other workgroups wrote it),
+        // then X[t][r] = L[64 I2 + r][64 J + t] in LDS
+        auto load = [&](T (&v)[16], int I2, int J) {
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int e = tid + 256 * u, r = e & 63, c = e >> 6;
                 v[u] = ld_sc1(&Fn[(int64_t)(64 * J + c) * ld + 64 * I2 + r]);
             }
+        };
+        auto store = [&](T (*X)[TLD], const T (&v)[16]) {
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int e = tid + 256 * u;
@@ -147,12 +149,22 @@ __global__ __launch_bounds__(256) void nd_factor(const NdDev* __restrict__ nodes
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 acc[cb][q] = Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q];
+        // left-looking products, software-pipelined: the loads of block
+        // column J + 1 are in flight during column J's MFMAs
+        // left-looking products (two workgroups per CU: __launch_bounds__
+        // (256, 2) keeps the VGPRs at 128; at 136 the occupancy query gave one
+        // and the C5 factor took 8.5 instead of 5.7 ms)
         const int Jn = K < npt ? K : npt;
         for (int J = 0; J < Jn; ++J) {
             wait_flag(&fl[I * npt + J]);
             if (I != K) wait_flag(&fl[K * npt + J]);
-            stage(PT, I, J);
-            if (I != K) stage(QT, K, J);
+            T va[16];
+            load(va, I, J);
+            store(PT, va);
+            if (I != K) {
+                load(va, K, J);
+                store(QT, va);
+            }
             __syncthreads();
             mfma_tile<T, true>(PTl, I != K ? QTl : PTl, acc, w, lane);
             __syncthreads();
@@ -249,14 +261,17 @@ __global__ __launch_bounds__(256) void nd_scatter(int64_t n, int64_t k, const in
 // node's pivots of bp plus its children's update vectors; per pivot tile K
 // y_K = Dinv_K v_K, then v_I -= L_IK y_K below. v (at V + voff) ends as y
 // over the pivots and the update vector u over the front rows. V is read and
-// written write-through (rows change hands between threads).
+// written write-through (rows change hands between threads). Every product's
+// loads are issued together (unrolled): a loop of load, wait, FMA is one
+// L2 round trip per term, 64 per tile step.
 template <typename T>
 __global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ nodes, const int32_t* __restrict__ lvl,
                                                   int64_t n, const T* __restrict__ bp, T* __restrict__ V, int64_t vtot,
                                                   const T* __restrict__ F, const T* __restrict__ Dinv,
                                                   const int32_t* __restrict__ ri) {
     __shared__ T vk[64], yk[64];
-    const int tid = threadIdx.x;
+    __shared__ T part[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const NdDev& nd = nodes[lvl[blockIdx.x]];
     const int64_t col = blockIdx.y;
     T* const v = V + col * vtot + nd.voff;
@@ -283,22 +298,41 @@ __global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ node
     for (int K = 0; K < nd.npt; ++K) {
         if (tid < 64) vk[tid] = ld_sc1(&v[64 * K + tid]);
         __syncthreads();
+        {  // y_K = Dinv_K v_K: wave wv sums terms q in [16 wv, 16 wv + 16)
+            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096 + 16 * wv * 64 + lane;
+            T gv[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) gv[j] = g[j * 64];
+            T y0 = (T)0, y1 = (T)0;
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                y0 = fma_t(gv[j], vk[16 * wv + j], y0);
+                y1 = fma_t(gv[j + 1], vk[16 * wv + j + 1], y1);
+            }
+            part[wv][lane] = y0 + y1;
+        }
+        __syncthreads();
         if (tid < 64) {
-            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096;
-            T y = (T)0;
-            for (int q = 0; q < 64; ++q) y = fma_t(g[q * 64 + tid], vk[q], y);
+            const T y = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
             yk[tid] = y;
             st_sc1(&v[64 * K + tid], y);
         }
         __syncthreads();
         for (int r = 64 * (K + 1) + tid; r < fp; r += 256) {
             const T* lc = Fn + (int64_t)64 * K * ld + r;
-            T s0 = (T)0, s1 = (T)0;
-            for (int t = 0; t < 64; t += 2) {
-                s0 = fma_t(lc[(int64_t)t * ld], yk[t], s0);
-                s1 = fma_t(lc[(int64_t)(t + 1) * ld], yk[t + 1], s1);
+            T lv[64];
+#pragma unroll
+            for (int t = 0; t < 64; ++t) lv[t] = lc[(int64_t)t * ld];
+            const T vr = ld_sc1(&v[r]);
+            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+            for (int t = 0; t < 64; t += 4) {
+                s0 = fma_t(lv[t], yk[t], s0);
+                s1 = fma_t(lv[t + 1], yk[t + 1], s1);
+                s2 = fma_t(lv[t + 2], yk[t + 2], s2);
+                s3 = fma_t(lv[t + 3], yk[t + 3], s3);
             }
-            st_sc1(&v[r], ld_sc1(&v[r]) - (s0 + s1));
+            st_sc1(&v[r], vr - ((s0 + s1) + (s2 + s3)));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -315,6 +349,7 @@ __global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nod
                                                    const int32_t* __restrict__ st) {
     __shared__ T red[64][65];
     __shared__ T zk[64];
+    __shared__ T part[4][64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const NdDev& nd = nodes[lvl[blockIdx.x]];
     const int64_t col = blockIdx.y;
@@ -326,33 +361,59 @@ __global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nod
     const T* const Fn = F + nd.foff;
     const int64_t ld = nd.ld;
     for (int K = nd.npt - 1; K >= 0; --K) {
+        // column sums below the tile: wave wv takes columns 16 wv .. 16 wv + 15,
+        // lanes the rows, two rows per lane in flight
         T acc[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) acc[c] = (T)0;
         const T* lc = Fn + (int64_t)(64 * K + 16 * wv) * ld;
-        for (int r = 64 * (K + 1) + lane; r < fp; r += 64) {
-            const T wr = ld_sc1(&w[r]);
+        int r = 64 * (K + 1) + lane;
+        for (; r + 64 < fp; r += 128) {
+            const T w0 = ld_sc1(&w[r]), w1 = ld_sc1(&w[r + 64]);
+            T l0[16], l1[16];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = fma_t(lc[(int64_t)c * ld + r], wr, acc[c]);
+            for (int c = 0; c < 16; ++c) {
+                l0[c] = lc[(int64_t)c * ld + r];
+                l1[c] = lc[(int64_t)c * ld + r + 64];
+            }
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma_t(l1[c], w1, fma_t(l0[c], w0, acc[c]));
+        }
+        if (r < fp) {
+            const T w0 = ld_sc1(&w[r]);
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma_t(lc[(int64_t)c * ld + r], w0, acc[c]);
         }
 #pragma unroll
         for (int c = 0; c < 16; ++c) red[16 * wv + c][lane] = acc[c];
         __syncthreads();
         if (tid < 64) {
-            T s0 = (T)0, s1 = (T)0;
-            for (int l = 0; l < 64; l += 2) {
+            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+            for (int l = 0; l < 64; l += 4) {
                 s0 += red[tid][l];
                 s1 += red[tid][l + 1];
+                s2 += red[tid][l + 2];
+                s3 += red[tid][l + 3];
             }
-            zk[tid] = ld_sc1(&w[64 * K + tid]) - (s0 + s1);
+            zk[tid] = ld_sc1(&w[64 * K + tid]) - ((s0 + s1) + (s2 + s3));
         }
         __syncthreads();
-        if (tid < 64) {
-            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096 + (int64_t)tid * 64;
-            T x = (T)0;
-            for (int q = 0; q < 64; ++q) x = fma_t(g[q], zk[q], x);  // Linv[q][tid] = Dinv[tid * 64 + q]
-            st_sc1(&w[64 * K + tid], x);
+        {  // x_K = Dinv_K^T z: Linv[q][l] = Dinv[l * 64 + q]; wave wv sums q in [16 wv, 16 wv + 16)
+            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096 + (int64_t)lane * 64 + 16 * wv;
+            T gv[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) gv[j] = g[j];
+            T x0 = (T)0, x1 = (T)0;
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                x0 = fma_t(gv[j], zk[16 * wv + j], x0);
+                x1 = fma_t(gv[j + 1], zk[16 * wv + j + 1], x1);
+            }
+            part[wv][lane] = x0 + x1;
         }
+        __syncthreads();
+        if (tid < 64) st_sc1(&w[64 * K + tid], (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -467,7 +528,7 @@ struct NdCached {
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_perm = 0;
     size_t n_tiles = 0, n_ext = 0;
-    double ms_graph = 0, ms_order = 0, ms_symbolic = 0;
+    double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
 };
 
@@ -508,8 +569,10 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     const int arc = nd_analyse(N, rp, cl, leaf, threads, P);
     BSM_REQUIRE(arc == 0, BSM_ERR_UNSUPPORTED,
                 "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
+    const auto tl0 = host_now();
     NdLayout L;
     nd_layout(P, L);
+    C.ms_layout = ms_since(tl0);
     C.leaf = leaf;
     C.nn = (int32_t)L.dev.size();
     C.n_levels = P.n_levels;
@@ -538,6 +601,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.o_ext = C.o_tiles + al(L.tiles.size() * sizeof(int4));
     C.o_perm = C.o_ext + al(L.ext.size() * sizeof(int2));
     const size_t total = C.o_perm + al((size_t)N * 8);
+    const auto tp0 = host_now();
     char* hp = nullptr;
     BSM_TRY(pinned_staging(total, &hp));  // the pattern is no longer needed
     auto put = [&](size_t o, const void* p, size_t b) {
@@ -552,6 +616,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     put(C.o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
     put(C.o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
+    C.ms_pack = ms_since(tp0);
     BSM_TRY(C.plan.alloc(total));
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
@@ -586,9 +651,9 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const NdCached& C = *pc;
     if (getenv("BSM_ND_TRACE"))
         fprintf(stderr,
-                "[bsm nd] n %lld nodes %d levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms; fronts "
-                "%.3f GB (largest %lld), tiles %zu, extend columns %zu\n",
-                (long long)N, C.nn, C.n_levels, C.ms_graph, C.ms_order, C.ms_symbolic,
+                "[bsm nd] n %lld nodes %d levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms, layout "
+                "%.1f ms, packing %.1f ms; fronts %.3f GB (largest %lld), tiles %zu, extend columns %zu\n",
+                (long long)N, C.nn, C.n_levels, C.ms_graph, C.ms_order, C.ms_symbolic, C.ms_layout, C.ms_pack,
                 (double)C.f_elems * sizeof(T) * 1e-9, (long long)C.max_front, C.n_tiles, C.n_ext);
     char* pb = C.plan.as<char>();
     const NdDev* d_nodes = (const NdDev*)(pb + C.o_dev);

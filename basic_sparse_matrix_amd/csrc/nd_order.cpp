@@ -77,6 +77,7 @@ struct Bisect {
     int par_depth;
     std::vector<int32_t> mark, lvl, seen;
     int64_t band = 0;  // max |i - j| over the edges (natural order)
+    bool band_hints = true;
     std::deque<TNode> tree;
     std::mutex mu;
     std::atomic<int32_t> stamp{0};
@@ -131,6 +132,7 @@ struct Bisect {
             return;
         }
         std::vector<int32_t> order, A, B, S;
+        int32_t ha = -1, hb = -1;  // the children's BFS roots (-1: search for a far vertex)
         if (depth == 0 && band > 0 && (int64_t)verts.size() >= 8 * band) {
             // a narrow band in the natural order (a mesh numbered row by row):
             // any band consecutive indices separate those below from those
@@ -147,6 +149,13 @@ struct Bisect {
                 (beyond ? S : A).push_back((int32_t)v);
             }
             std::sort(A.begin(), A.end());
+            // the halves' BFS roots: their first and last indices (a mesh's
+            // far corners, where the search for a far vertex would also end
+            // up), without that search's BFS
+            if (band_hints) {
+                ha = 0;
+                hb = (int32_t)(n - 1);
+            }
         } else {
         order.reserve(verts.size());
         bfs(hint >= 0 ? hint : verts[0], id, stamp++, order);
@@ -211,8 +220,7 @@ struct Bisect {
         // the children's roots: the separator's first vertex reached (an end
         // of the cut, so the next cut runs across this one); without a
         // separator, a search
-        int32_t ha = -1, hb = -1;
-        if (!S.empty() && !(depth == 0 && order.empty())) ha = hb = S.front();
+        if (!order.empty() && !S.empty()) ha = hb = S.front();
         const int32_t ka = new_node(), kb = new_node();
         for (int32_t v : A) mark[v] = ka;
         for (int32_t v : B) mark[v] = kb;
@@ -261,6 +269,8 @@ int nd_analyse(int64_t n, const int64_t* row_ptr, const int32_t* col, int64_t le
         std::vector<int32_t> all((size_t)n);
         for (int64_t i = 0; i < n; ++i) all[(size_t)i] = (int32_t)i;
         bs.band = g.band;
+        const char* bh = getenv("BSM_ND_BANDHINT");
+        bs.band_hints = !(bh && atoi(bh) == 0);
         bs.run(std::move(all), root, 0, -1);
     }
 
