@@ -84,8 +84,9 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 }
 
 // Partial Cholesky of the fronts of one level. tiles[t] = (node, I, K):
-// column-major order across the level's fronts (K, then node, then I), so a
-// tile only waits on tiles of earlier tickets. Tile (I, K), I >= K:
+// column-major order across the level's fronts (K; the diagonal tiles of all
+// fronts, then the tiles below them), so a tile only waits on tiles of
+// earlier tickets. Tile (I, K), I >= K:
 //     S = F_IK - sum_{J < min(K, npt)} L_IJ L_KJ^T
 //     K < npt, I == K: L_KK = chol(S), Dinv_K = L_KK^-1   (flag)
 //     K < npt, I >  K: L_IK = S L_KK^-T                    (flag)
@@ -496,12 +497,17 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
         L.tiles_off.push_back((int64_t)L.tiles.size());
         int32_t kmax = 0;
         for (int32_t i : lv) kmax = std::max(kmax, L.dev[(size_t)i].nt);
-        for (int32_t K = 0; K < kmax; ++K)
+        // column K of every front: the diagonal tiles first, then the tiles
+        // below (which wait for their diagonal tile's inverse), so the
+        // waiting tiles' diagonals are well under way when they are taken
+        for (int32_t K = 0; K < kmax; ++K) {
+            for (int32_t i : lv)
+                if (K < L.dev[(size_t)i].nt) L.tiles.push_back(make_int4(i, K, K, 0));
             for (int32_t i : lv) {
                 const NdDev& d = L.dev[(size_t)i];
-                for (int32_t I = K; I < d.nt; ++I)
-                    if (K < d.nt) L.tiles.push_back(make_int4(i, I, K, 0));
+                for (int32_t I = K + 1; I < d.nt; ++I) L.tiles.push_back(make_int4(i, I, K, 0));
             }
+        }
         for (int s = 0; s < 2; ++s) {
             L.ext_off.push_back((int64_t)L.ext.size());
             for (int32_t i : lv) {
