@@ -10,8 +10,10 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -74,16 +76,16 @@ struct TNode {
 struct Bisect {
     const Graph& g;
     int64_t leaf;
-    int par_depth;
     std::vector<int32_t> mark, lvl, seen;
     int64_t band = 0;  // max |i - j| over the edges (natural order)
     bool band_hints = true;
+    bool trace = false;
     std::deque<TNode> tree;
     std::mutex mu;
     std::atomic<int32_t> stamp{0};
 
-    Bisect(const Graph& g_, int64_t leaf_, int par_depth_)
-        : g(g_), leaf(leaf_), par_depth(par_depth_), mark((size_t)g_.n, 0), lvl((size_t)g_.n, 0),
+    Bisect(const Graph& g_, int64_t leaf_)
+        : g(g_), leaf(leaf_), mark((size_t)g_.n, 0), lvl((size_t)g_.n, 0),
           seen((size_t)g_.n, -1) {}
 
     int32_t new_node() {
@@ -126,11 +128,23 @@ struct Bisect {
 
     // hint >= 0: a vertex of the part to root the level structure at (no
     // search for a far vertex); else the first BFS finds one
-    void run(std::vector<int32_t> verts, int32_t id, int depth, int32_t hint) {
+    struct Task {
+        std::vector<int32_t> verts;
+        int32_t id;
+        int depth;
+        int32_t hint;
+    };
+
+    // One part: a leaf, or a separator and two child parts for the pool.
+    void split(Task& tk, std::vector<Task>& out) {
+        std::vector<int32_t>& verts = tk.verts;
+        const int32_t id = tk.id, hint = tk.hint;
+        const int depth = tk.depth;
         if ((int64_t)verts.size() <= leaf) {
             node(id).own = std::move(verts);
             return;
         }
+        const auto tr0 = Clock::now();
         std::vector<int32_t> order, A, B, S;
         int32_t ha = -1, hb = -1;  // the children's BFS roots (-1: search for a far vertex)
         if (depth == 0 && band > 0 && (int64_t)verts.size() >= 8 * band) {
@@ -148,7 +162,6 @@ struct Bisect {
                 for (int64_t e = g.xadj[v]; e < g.xadj[v + 1] && !beyond; ++e) beyond = g.adj[e] >= hi;
                 (beyond ? S : A).push_back((int32_t)v);
             }
-            std::sort(A.begin(), A.end());
             // the halves' BFS roots: their first and last indices (a mesh's
             // far corners, where the search for a far vertex would also end
             // up), without that search's BFS
@@ -221,6 +234,7 @@ struct Bisect {
         // of the cut, so the next cut runs across this one); without a
         // separator, a search
         if (!order.empty() && !S.empty()) ha = hb = S.front();
+        if (trace && depth < 5) fprintf(stderr, "[nd bisect] depth %d part %zu: split %.2f ms\n", depth, verts.size(), ms_since(tr0));
         const int32_t ka = new_node(), kb = new_node();
         for (int32_t v : A) mark[v] = ka;
         for (int32_t v : B) mark[v] = kb;
@@ -235,14 +249,52 @@ struct Bisect {
             ha = near_in(ha, ka);
             hb = near_in(hb, kb);
         }
-        if (depth < par_depth) {
-            std::thread t([&, ka, ha] { run(std::move(A), ka, depth + 1, ha); });
-            run(std::move(B), kb, depth + 1, hb);
-            t.join();
-        } else {
-            run(std::move(A), ka, depth + 1, ha);
-            run(std::move(B), kb, depth + 1, hb);
-        }
+        out.push_back(Task{std::move(A), ka, depth + 1, ha});
+        out.push_back(Task{std::move(B), kb, depth + 1, hb});
+    }
+
+    // The parts on `threads` workers sharing one LIFO queue (depth first
+    // per worker; an idle worker takes the newest waiting part), so the
+    // uneven subtrees of the lower levels balance: fixed subtree-per-thread
+    // left the last thread 3x behind the first.
+    void run_pool(Task root, int threads) {
+        std::vector<Task> q;
+        std::mutex qm;
+        std::condition_variable cv;
+        size_t pending = 1;  // queued + being split
+        q.push_back(std::move(root));
+        auto worker = [&] {
+            std::vector<Task> kids;
+            for (;;) {
+                Task tk;
+                {
+                    std::unique_lock<std::mutex> lk(qm);
+                    cv.wait(lk, [&] { return !q.empty() || pending == 0; });
+                    if (q.empty()) return;  // pending == 0: done
+                    tk = std::move(q.back());
+                    q.pop_back();
+                }
+                kids.clear();
+                split(tk, kids);
+                // keep one child here (no queue round trip), publish the rest
+                while (!kids.empty()) {
+                    std::unique_lock<std::mutex> lk(qm);
+                    for (size_t i = 1; i < kids.size(); ++i) q.push_back(std::move(kids[i]));
+                    pending += kids.size() - 1;
+                    if (kids.size() > 1) cv.notify_all();
+                    lk.unlock();
+                    Task next = std::move(kids[0]);
+                    kids.clear();
+                    split(next, kids);
+                }
+                std::unique_lock<std::mutex> lk(qm);
+                if (--pending == 0) cv.notify_all();
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto& t : pool) t.join();
     }
 };
 
@@ -261,9 +313,7 @@ int nd_analyse(int64_t n, const int64_t* row_ptr, const int32_t* col, int64_t le
 
     // bisection tree
     t0 = Clock::now();
-    int par_depth = 0;
-    while ((1 << par_depth) < threads) ++par_depth;
-    Bisect bs(g, leaf, par_depth);
+    Bisect bs(g, leaf);
     const int32_t root = bs.new_node();
     {
         std::vector<int32_t> all((size_t)n);
@@ -271,7 +321,9 @@ int nd_analyse(int64_t n, const int64_t* row_ptr, const int32_t* col, int64_t le
         bs.band = g.band;
         const char* bh = getenv("BSM_ND_BANDHINT");
         bs.band_hints = !(bh && atoi(bh) == 0);
-        bs.run(std::move(all), root, 0, -1);
+        const char* tt = getenv("BSM_ND_TRACE");
+        bs.trace = tt && atoi(tt) == 2;
+        bs.run_pool({std::move(all), root, 0, -1}, threads);
     }
 
     // post-order numbering: kid 0's subtree, kid 1's, then the node's own vertices
