@@ -178,6 +178,36 @@ def test_nd_deterministic(orc, g):
     assert rel_err(x0, ex) < 1e-10
 
 
+def poisson3d(g):
+    """7-point Laplacian on a g^3 grid (natural order, band g^2), diagonal 6.5."""
+    n = g ** 3
+    idx = np.arange(n).reshape(g, g, g)
+    rows, cols, vals = [idx.ravel()], [idx.ravel()], [np.full(n, 6.5)]
+    for ax in range(3):
+        a = np.take(idx, range(g - 1), axis=ax).ravel()
+        b = np.take(idx, range(1, g), axis=ax).ravel()
+        rows += [a, b]
+        cols += [b, a]
+        vals += [np.full(a.size, -1.0), np.full(a.size, -1.0)]
+    r, c, v = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    o = np.lexsort((c, r))
+    r, c, v = r[o], c[o], v[o]
+    rp = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n))]).astype(np.uint64)
+    return rp, c.astype(np.uint64), v
+
+
+@pytest.mark.parametrize("g", [8, 20])
+def test_nd_poisson3d_vs_oracle(orc, g):
+    """A 3-D mesh (separators ~ n^(2/3): larger fronts per level than 2-D)."""
+    rp, ci, v = poisson3d(g)
+    n = g ** 3
+    b = orc.gen_x_cols(1012, n, 2)
+    x = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
+    ex = orc.solve(n, rp, ci, v, b, band=True)
+    for j in range(2):
+        assert rel_err(x.get_col(j), ex[j]) < 1e-10, j
+
+
 @pytest.mark.slow
 def test_c5_nd_poisson_1m_f64_properties(orc, golden_c5):
     """C5 (N = 1M): within 1e-6 relative (BASELINE.json) of the band
