@@ -277,7 +277,8 @@ template <typename T, int M, int RP>  // RP rows per wave: 16 / RP waves
 __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t b, int64_t ld, T* __restrict__ CB,
                                                     T* __restrict__ R, int* __restrict__ fprog,
                                                     int* __restrict__ status, int* __restrict__ ticket,
-                                                    int64_t n_tiles, unsigned long long* __restrict__ trace) {
+                                                    int64_t n_tiles, unsigned long long* __restrict__ trace,
+                                                    int delay) {
     using A = Arith<T>;
     constexpr int CS = 64 + 64 * M;
     constexpr int C5_NT = 64 * (16 / RP);
@@ -573,6 +574,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
         if (tid < 64) {
             diag_factor16x<T, 1>(dacc, dA, dacc, xl, i0, n, b, ld, CB, R, status, c);
             mark(false, 13);
+            for (int q = delay; q < 0; ++q) __builtin_amdgcn_s_sleep(127);  // stress: wave 0 arrives last
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (c == 0) {
                 if (!store_waves || (atomicAdd(&s_arr, C5_W0) & 0xff) == C5_NSW) {
@@ -596,6 +598,7 @@ __global__ __launch_bounds__(64 * (16 / RP)) void band_chol5(int64_t n, int64_t 
             // store wave raises the flag, or completion if wave 0 has already
             // arrived (MI355X_MICROARCH.md "Valid forms": per-wave arrival).
             const int k0 = i0 - C4_TB;
+            for (int q = 0; q < delay; ++q) __builtin_amdgcn_s_sleep(127);  // stress: the stores land late
             for (int e = tid - 64; e < C4_TB * C4_TB; e += C5_NT - 64) {
                 const int t = e >> 4, rw = e & 15, d = i0 + rw - k0 - t;
                 if (d <= ib && i0 + rw < n) st_sc1(&CB[(int64_t)(k0 + t) * ld + d], hist2[(I - 1) & 1][t][rw]);
@@ -1795,8 +1798,14 @@ int launch_chol5(Band& bd, int* fprog, int* status, hipStream_t s, unsigned long
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > n_tiles) grid = n_tiles;
     if (grid < 1) grid = 1;
+    // BSM_CHOL5_DELAY=d (stress tests only): every row-block's store waves
+    // sleep d x 127 x 64 cycles before storing the last tile (d < 0: wave 0
+    // sleeps -d times that before its drain), so completion must wait for the
+    // late side whichever it is (tests/test_gpu_solver.py)
+    const char* de = getenv("BSM_CHOL5_DELAY");
+    const int delay = de ? std::max(-64, std::min(64, atoi(de))) : 0;
     band_chol5<T, M, RP><<<(unsigned)grid, C5_NT, 0, s>>>(bd.n, bd.b, bd.ld, bd.cb.as<T>(), bd.r.as<T>(), fprog, status,
-                                                         status + 1, n_tiles, trace);
+                                                         status + 1, n_tiles, trace, delay);
     BSM_HIP_TRY(hipGetLastError());
     return BSM_OK;
 }

@@ -169,6 +169,23 @@ def test_poisson_cholesky_bandwidths_vs_oracle(orc, dtype, g):
     assert_csr_exact(A.cholesky_decomp(), *expect)
 
 
+@pytest.mark.parametrize("delay", [8, -8])
+@pytest.mark.parametrize("dtype,g", [(np.float64, 100), (np.float32, 63)])
+def test_chol5_completion_with_late_waves_vs_oracle(orc, monkeypatch, dtype, g, delay):
+    """a row-block is complete only when wave 0's factor AND
+    the store waves' last-tile stores have landed. BSM_CHOL5_DELAY makes one
+    side late in every row-block (d > 0: the store waves sleep ~d x 8k cycles
+    before storing; d < 0: wave 0 before its drain), so a completion raised by
+    the early side alone would let the next row-blocks read stale rows. The
+    factor must still equal the band oracle bit for bit."""
+    monkeypatch.setenv("BSM_CHOL5_DELAY", str(delay))
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    v = v.astype(dtype)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    assert_csr_exact(A.cholesky_decomp(), *orc.cholesky(n, n, rp, ci, v, band=True))
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_forward_helper_prefixes_vs_oracle(orc, dtype):
     """Bandwidth 200 > FW3_NEAR: the default forward solve takes the far
