@@ -240,6 +240,11 @@ struct bsm_csr {
     // row_ptr / col / vals from the result cache (csr_alloc): their block
     // capacities, 0 = plain hipMalloc (bsm_csr_free hipFrees those)
     size_t cache_cap[3] = {0, 0, 0};
+    // small mul_dense results: a host copy written by the same kernel as the
+    // device arrays (row_ptr int64 [rows + 1], cols int32 [nnz], values
+    // [nnz]); bsm_csr_download serves it without touching the device. The
+    // device arrays never change after creation, so it cannot go stale.
+    std::unique_ptr<char[]> host_copy;
 };
 
 
@@ -283,7 +288,8 @@ int exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, uint64_t n, void*
                               uint64_t ws_bytes, hipStream_t s);  // out has n+1 entries
 int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
-                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s);
+                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s,
+                  uint64_t max_row_len = UINT64_MAX);  // the longest row, when known (kernel choice)
 // nnz-balanced integer SpMM for skewed rows (zeroes y; row_nnz may be null)
 bool spmm_wants_split(int dtype, uint64_t k, uint64_t max_row_len);
 int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
@@ -316,6 +322,15 @@ int tiled_spmm(const bsm_tiled* t, const void* x, void* y, int32_t* row_nnz, boo
 void tiled_destroy(bsm_tiled* t);
 int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const int64_t* out_rp,
                      int32_t* out_col, void* out_vals, hipStream_t s);
+// Small results (rows <= SMALL_OUT_ROWS, rows x k <= SMALL_OUT_CAP): the
+// row-count scan and the compaction in one workgroup, which also writes the
+// result into `host` (page-locked: row_ptr int64 [rows + 1], then cols int32
+// [cap] at small_col_bytes alignment, then values [cap]); kernels_spmm.hip.
+constexpr uint64_t SMALL_OUT_ROWS = 8192;
+constexpr uint64_t SMALL_OUT_CAP = 131072;
+inline size_t small_col_bytes(uint64_t cap) { return (cap * sizeof(int32_t) + 15) / 16 * 16; }
+int compact_small_dispatch(int dtype, uint64_t rows, uint64_t k, const int32_t* nz, const void* y, int64_t* out_rp,
+                           int32_t* out_col, void* out_vals, void* host, uint64_t cap, hipStream_t s);
 int pack_cols_to_rowmajor(int dtype, uint64_t n, uint64_t k, const void* colmajor, void* rowmajor,
                           hipStream_t s);
 int unpack_rowmajor_to_cols(int dtype, uint64_t n, uint64_t k, const void* rowmajor,

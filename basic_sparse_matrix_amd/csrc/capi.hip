@@ -359,6 +359,37 @@ void* pinned(size_t bytes) {
     return h.buf;
 }
 
+// BSM_SMALL_OUT=0: small mul_dense results take the scan + compaction
+// launches and the download copies (A/B)
+static bool small_out_enabled() {
+    const char* e = getenv("BSM_SMALL_OUT");
+    return !e || atoi(e) != 0;
+}
+
+// Page-locked destination of the small results' host copy (compact_small):
+// one per thread, reused by the thread's next small call (the result handle
+// keeps its own copy). *dev: the buffer's device address.
+static void* pinned_result(size_t bytes, void** dev) {
+    static thread_local PinnedHolder h;
+    static thread_local void* h_dev = nullptr;
+    if (bytes > h.cap) {
+        if (h.buf) (void)hipHostFree(h.buf);
+        h.buf = h_dev = nullptr;
+        h.cap = 0;
+        const size_t want = std::max<size_t>(bytes, 1 << 20);
+        if (hipHostMalloc(&h.buf, want, hipHostMallocDefault) != hipSuccess ||
+            hipHostGetDevicePointer(&h_dev, h.buf, 0) != hipSuccess) {
+            if (h.buf) (void)hipHostFree(h.buf);
+            h.buf = h_dev = nullptr;
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        h.cap = want;
+    }
+    *dev = h_dev;
+    return h.buf;
+}
+
 // Per-call temporaries of small calls (the uploaded X, Y, row counts, scan
 // workspace) come from a per-thread grow-only device arena: no hipMalloc /
 // hipFree per call (hipFree waits for the device). Calls larger than
@@ -558,7 +589,8 @@ int spmm_launch_locked(const bsm_csr* a, uint64_t k, bool allow_tiled, const voi
     if (w && a->plan_usable && a->plan_cols == w)
         return spmm_panelled(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, w,
                              a->plan_seg, s);
-    return spmm_dispatch(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, false, s);
+    return spmm_dispatch(a->dtype, a->rows, a->cols, a->nnz, a->row_ptr, a->col, a->vals, k, x, y, nz, false, s,
+                         a->max_row_len);
 }
 
 // mul_dense core on device operands: Y = A X, then compaction into a Csr.
@@ -599,11 +631,21 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
         BSM_TRY(spmm_prepare_locked(a, k, 0, reserve, s, nullptr));
         BSM_TRY(spmm_launch_locked(a, k, true, x_dev, yp, nz, s));
     }
+    // the smallest results (C1): scan + compaction in one workgroup that also
+    // writes the host copy bsm_csr_download serves (compact_small)
+    const bool arena = small && yp != y.p;
+    char* host = nullptr;
+    void* host_dev = nullptr;
+    if (arena && k > 0 && rows > 0 && rows <= SMALL_OUT_ROWS && rows * k <= SMALL_OUT_CAP &&
+        small_out_enabled())
+        host = static_cast<char*>(pinned_result((rows + 1) * sizeof(int64_t) + small_col_bytes(rows * k) +
+                                                    rows * k * es,
+                                                &host_dev));
     const size_t wsb = ws.p ? ws.bytes : ws_b;
-    BSM_TRY(exclusive_scan_i32_to_i64(nz, out_rp.as<int64_t>(), rows, wsp, wsb, s));
+    if (!host) BSM_TRY(exclusive_scan_i32_to_i64(nz, out_rp.as<int64_t>(), rows, wsp, wsb, s));
     int64_t out_nnz = 0;
-    if (!small || yp == y.p) BSM_HIP_TRY(read_dev(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t), s));
-    const uint64_t cap = small && yp != y.p ? rows * k : (uint64_t)out_nnz;
+    if (!arena) BSM_HIP_TRY(read_dev(&out_nnz, out_rp.as<int64_t>() + rows, sizeof(int64_t), s));
+    const uint64_t cap = arena ? rows * k : (uint64_t)out_nnz;
     r = new bsm_csr();
     r->dtype = a->dtype;
     r->device = a->device;
@@ -625,8 +667,26 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
     r->analysed = true;
     r->rows_sorted = true;
     r->max_row_len = k;  // a bound: at most k entries per output row
-    rc = compact_dispatch(a->dtype, rows, k, yp, r->row_ptr, r->col, r->vals, s);
-    if (rc == BSM_OK && small && yp != y.p) {  // nnz with the one synchronisation of the call
+    if (host) {
+        rc = compact_small_dispatch(a->dtype, rows, k, nz, yp, r->row_ptr, r->col, r->vals, host_dev, cap, s);
+        if (rc == BSM_OK) {
+            hipError_t e = hipStreamSynchronize(s);  // the call's one synchronisation
+            if (e != hipSuccess) {
+                set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
+                rc = BSM_ERR_HIP;
+            }
+        }
+        if (rc == BSM_OK) {
+            out_nnz = reinterpret_cast<const int64_t*>(host)[rows];
+            const size_t rp_b = (rows + 1) * sizeof(int64_t), col_b = (size_t)out_nnz * sizeof(int32_t);
+            r->host_copy.reset(new char[rp_b + col_b + (size_t)out_nnz * es]);
+            std::memcpy(r->host_copy.get(), host, rp_b + col_b);
+            std::memcpy(r->host_copy.get() + rp_b + col_b, host + rp_b + small_col_bytes(cap), (size_t)out_nnz * es);
+        }
+    } else {
+        rc = compact_dispatch(a->dtype, rows, k, yp, r->row_ptr, r->col, r->vals, s);
+    }
+    if (rc == BSM_OK && arena && !host) {  // nnz with the one synchronisation of the call
         hipError_t e = read_dev(&out_nnz, r->row_ptr + rows, sizeof(int64_t), s);
         if (e != hipSuccess) {
             set_error("read nnz: %s", hipGetErrorString(e));
@@ -634,7 +694,7 @@ static int mul_dense_device(const bsm_csr* a, uint64_t k, const void* x_dev, bsm
         }
     }
     r->nnz = (uint64_t)out_nnz;
-    if (rc == BSM_OK) {
+    if (rc == BSM_OK && !host) {
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
             set_error("hipStreamSynchronize: %s", hipGetErrorString(e));
@@ -773,6 +833,16 @@ int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, voi
     BSM_TRY(ctx_stream(&s));
     const size_t es = dtype_size(m->dtype);
     const size_t rp_b = (m->rows + 1) * sizeof(int64_t), col_b = m->nnz * sizeof(int32_t), val_b = m->nnz * es;
+    if (m->host_copy) {  // a small mul_dense result: its host copy, no device work
+        const int64_t* rp64 = reinterpret_cast<const int64_t*>(m->host_copy.get());
+        const int32_t* c32 = reinterpret_cast<const int32_t*>(m->host_copy.get() + rp_b);
+        if (row_ptr)
+            for (uint64_t r = 0; r <= m->rows; ++r) row_ptr[r] = (uint64_t)rp64[r];
+        if (col_idx)
+            for (uint64_t e = 0; e < m->nnz; ++e) col_idx[e] = (uint64_t)c32[e];
+        if (vals && val_b) std::memcpy(vals, m->host_copy.get() + rp_b + col_b, val_b);
+        return BSM_OK;
+    }
     // page-locked destinations (bsm_host_register): direct DMA, no host copies
     // (row_ptr may be a small pageable array: its copy is tiny either way)
     // (up to 128M entries: the widened columns need an nnz x 8 B device temporary)
@@ -885,7 +955,8 @@ int bsm_csr_mul_vector(const bsm_csr* a, const void* rhs, uint64_t rhs_len, void
     }
     if (rc == BSM_OK)
         rc = spmm_dispatch(src->dtype, src->rows, src->cols, src->nnz, src->row_ptr, src->col,
-                           src->vals, 1, x.p, y.p, nullptr, true, s);
+                           src->vals, 1, x.p, y.p, nullptr, true, s,
+                           src->analysed ? src->max_row_len : UINT64_MAX);
     if (rc == BSM_OK && out_len) {
         hipError_t e = hipMemcpyAsync(out, y.p, out_len * es, hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) { set_error("D2H: %s", hipGetErrorString(e)); rc = BSM_ERR_HIP; }

@@ -951,6 +951,7 @@ int spmv_items() {
     return (v == 2 || v == 8) ? v : 4;
 }
 constexpr uint64_t SHORT_ROW_AVG = 24;  // nnz/rows at or below: four rows per wave
+constexpr uint64_t SPMV_THREAD_ROWS = 16384, SPMV_THREAD_MAX_LEN = 48;  // spmv_thread's shapes
 constexpr uint64_t SPMV_ROWS_AVG = 12;  // k = 1, nnz/rows at or below: spmv_rows (one chunk per workgroup)
 int spmm_variant() {
     const char* e = getenv("BSM_SPMM_VARIANT");
@@ -960,7 +961,7 @@ int spmm_variant() {
 template <typename T>
 int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* col,
                 const T* vals, uint64_t k, const T* x, T* y, int32_t* row_nnz, bool neg_init,
-                hipStream_t s) {
+                hipStream_t s, uint64_t max_row_len) {
     if (rows == 0) return BSM_OK;
     // short rows on average (C2: 10): the rows-blocked SpMV; BSM_SPMV_VARIANT=1
     // forces the nnz-balanced spmv_stream (A/B)
@@ -979,6 +980,11 @@ int launch_spmm(uint64_t rows, uint64_t nnz, const int64_t* rp, const int32_t* c
         else if (svv == 5)
             spmv_wave<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
         else if (svv == 6)
+            spmv_thread<T, 12><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
+        else if (svv == 0 && rows <= SPMV_THREAD_ROWS && max_row_len <= SPMV_THREAD_MAX_LEN)
+            // few short rows (C1: 1,024 x ~10): latency-bound, one thread per
+            // row has the fewest dependent round trips (4.5 against 6.4 us at
+            // C1, profiles/r05_z_*)
             spmv_thread<T, 12><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
         else  // default (C2: 111 us against 117-167 for the others, scripts/perf/spmv_variants.py)
             spmv_wave<T, 8><<<(unsigned)blocks, 256, 0, s>>>(r, rp, col, vals, x, y, row_nnz, neg_init);
@@ -1195,12 +1201,12 @@ int spmm_split_dispatch(int dtype, uint64_t rows, uint64_t nnz, const int64_t* r
 
 int spmm_dispatch(int dtype, uint64_t rows, uint64_t n_cols, uint64_t nnz, const int64_t* rp,
                   const int32_t* col, const void* vals, uint64_t k, const void* x, void* y,
-                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s) {
+                  int32_t* row_nnz, bool neg_zero_init, hipStream_t s, uint64_t max_row_len) {
     (void)n_cols;
     return dispatch_dtype(dtype, [&]<typename T>() {
         return launch_spmm<T>(rows, nnz, rp, col, static_cast<const T*>(vals), k,
                               static_cast<const T*>(x), static_cast<T*>(y), row_nnz,
-                              neg_zero_init, s);
+                              neg_zero_init, s, max_row_len);
     });
 }
 
@@ -1303,6 +1309,109 @@ int compact_dispatch(int dtype, uint64_t rows, uint64_t k, const void* y, const 
                                                            static_cast<const T*>(y), out_rp, out_col,
                                                            static_cast<T*>(out_vals));
         }
+        BSM_HIP_TRY(hipGetLastError());
+        return BSM_OK;
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Small results (C1: 1,024 rows x 1 column): the row-count scan and the
+// compaction in ONE workgroup, writing the result twice -- into its device
+// arrays and into a page-locked host copy -- so that the call's one
+// synchronisation also delivers what bsm_csr_download returns (no scan
+// launch, no compaction launch, no read-back of nnz, no download copies).
+// Offsets live in LDS (rows <= SMALL_OUT_ROWS). Same entries, same order as
+// scan + compact_k1 / compact_seg: the row's nonzero columns ascending.
+// ---------------------------------------------------------------------------
+constexpr int SMALL_OUT_THREADS = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(SMALL_OUT_THREADS) void compact_small(int64_t rows, int k, const int32_t* __restrict__ nz,
+                                                                   const T* __restrict__ Y, int64_t* __restrict__ out_rp,
+                                                                   int32_t* __restrict__ out_col, T* __restrict__ out_val,
+                                                                   int64_t* __restrict__ h_rp, int32_t* __restrict__ h_col,
+                                                                   T* __restrict__ h_val) {
+    using A = Arith<T>;
+    __shared__ int32_t off[SMALL_OUT_ROWS];
+    __shared__ int32_t wsum[SMALL_OUT_THREADS / WAVE];
+    const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+    const int R = (int)((rows + SMALL_OUT_THREADS - 1) / SMALL_OUT_THREADS);
+    const int r0 = t * R, r1 = (int)min<int64_t>(rows, (int64_t)r0 + R);
+    int local = 0;
+    for (int r = r0; r < r1; ++r) local += nz[r];
+    int incl = local;  // wave inclusive scan, then the waves' totals
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == WAVE - 1) wsum[w] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < SMALL_OUT_THREADS / WAVE; ++q) {
+        before += q < w ? wsum[q] : 0;
+        total += wsum[q];
+    }
+    int ex = before + incl - local;
+    for (int r = r0; r < r1; ++r) {
+        off[r] = ex;
+        out_rp[r] = ex;
+        h_rp[r] = ex;
+        ex += nz[r];
+    }
+    if (t == 0) {
+        out_rp[rows] = total;
+        h_rp[rows] = total;
+    }
+    __syncthreads();
+    if (k == 1) {
+        for (int r = t; r < rows; r += SMALL_OUT_THREADS) {
+            const T v = Y[r];
+            if (A::nz(v)) {
+                const int p = off[r];
+                out_col[p] = 0;
+                out_val[p] = v;
+                h_col[p] = 0;
+                h_val[p] = v;
+            }
+        }
+        return;
+    }
+    for (int r = w; r < rows; r += SMALL_OUT_THREADS / WAVE) {  // one wave per row, lanes over columns
+        int base = off[r];
+        for (int j0 = 0; j0 < k; j0 += WAVE) {
+            const int j = j0 + lane;
+            const T v = j < k ? Y[(int64_t)r * k + j] : A::zero();
+            const bool keep = j < k && A::nz(v);
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const int p = base + __popcll(m & lanemask_lt(lane));
+                out_col[p] = j;
+                out_val[p] = v;
+                h_col[p] = j;
+                h_val[p] = v;
+            }
+            base += __popcll(m);
+        }
+    }
+}
+
+int compact_small_dispatch(int dtype, uint64_t rows, uint64_t k, const int32_t* nz, const void* y, int64_t* out_rp,
+                           int32_t* out_col, void* out_vals, void* host, uint64_t cap, hipStream_t s) {
+    BSM_REQUIRE(rows <= (uint64_t)SMALL_OUT_ROWS && k > 0 && rows * k <= SMALL_OUT_CAP && cap >= rows * k,
+                BSM_ERR_INVALID, "compact_small: %llu x %llu is not a small result", (unsigned long long)rows,
+                (unsigned long long)k);
+    const size_t es = dtype_size(dtype);
+    char* h = static_cast<char*>(host);
+    int64_t* h_rp = reinterpret_cast<int64_t*>(h);
+    int32_t* h_col = reinterpret_cast<int32_t*>(h + (rows + 1) * sizeof(int64_t));
+    void* h_val = h + (rows + 1) * sizeof(int64_t) + small_col_bytes(cap);
+    (void)es;
+    return dispatch_dtype(dtype, [&]<typename T>() {
+        compact_small<T><<<1, SMALL_OUT_THREADS, 0, s>>>((int64_t)rows, (int)k, nz, static_cast<const T*>(y), out_rp,
+                                                         out_col, static_cast<T*>(out_vals), h_rp, h_col,
+                                                         static_cast<T*>(h_val));
         BSM_HIP_TRY(hipGetLastError());
         return BSM_OK;
     });

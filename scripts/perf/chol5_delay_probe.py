@@ -1,6 +1,7 @@
 """Wall time of cholesky_decomp (band_chol5) at several BSM_CHOL5_DELAY
 values: shows that the stress knob the completion tests use really slows the
 late side (tests/test_gpu_solver.py::test_chol5_completion_with_late_waves_vs_oracle)."""
+import argparse
 import json
 import os
 import sys
@@ -25,7 +26,9 @@ def poisson2d(g):
     return n, np.cumsum(rp).astype(np.uint64), np.array(cols, np.uint64), np.array(vals)
 
 
-g = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+ap = argparse.ArgumentParser()
+ap.add_argument("g", type=int, nargs="?", default=100)
+g = ap.parse_args().g
 n, rp, ci, v = poisson2d(g)
 A = Csr.from_csr_arrays((n, n), rp, ci, v)
 A.cholesky_decomp()  # warm

@@ -88,10 +88,11 @@ def test_c1_public_api_bit_exact(orc):
     assert np.array_equal(comp.vals[:comp.nnz()].cpu().numpy().view(np.uint64), ev.view(np.uint64))
 
 
-@pytest.mark.parametrize("variant", ["0", "1"])  # spmv_rows (default for short rows) / spmv_stream
+# default / spmv_stream / spmv_wave / spmv_thread (the default for few short rows)
+@pytest.mark.parametrize("variant", ["0", "1", "5", "6"])
 def test_spmv_variants_ragged_rows_bit_exact(orc, monkeypatch, variant):
     """k = 1 on ragged rows (empty rows, rows longer than a workgroup's LDS
-    chunk) through both SpMV kernels, bit-exact."""
+    chunk) through every SpMV kernel, bit-exact."""
     from basic_sparse_matrix_amd import Csr, Dense
 
     monkeypatch.setenv("BSM_SPMV_VARIANT", variant)

@@ -127,6 +127,45 @@ def test_mul_dense_random_parity(orc, dtype, k):
     assert_csr_bits(got, *oracle_mul_dense(orc, a, x_cols))
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.int32])
+@pytest.mark.parametrize("rows,k", [(1, 1), (1024, 1), (1500, 3), (8192, 16), (8193, 1), (4096, 32), (2048, 64),
+                                    (1000, 131)])
+def test_small_result_host_copy_and_device_arrays(orc, monkeypatch, dtype, rows, k):
+    """Small results (rows <= 8192, rows x k <= 131,072; C1's shape) are
+    scanned and compacted by one workgroup that writes the result's device
+    arrays AND the host copy bsm_csr_download then serves. Both must equal
+    the oracle: the host copy through the download, the device arrays through
+    a device transpose of the result handle (transpose results have no host
+    copy). The shapes straddle both limits; BSM_SMALL_OUT=0 (scan +
+    compaction launches, download copies) gives the same bits."""
+    import ctypes
+
+    from basic_sparse_matrix_amd import _lib
+
+    dt = np.dtype(dtype)
+    vk = orc.VAL_SMALLINT  # exact zero sums too (dropped entries)
+    n_cols = 300
+    rp, ci, v = orc.gen_csr(40 + rows + k, rows, n_cols, kind=orc.ROWLEN_UNIFORM, a=0, b=9, value_kind=vk, dtype=dt)
+    a = Csr.from_csr_arrays((rows, n_cols), rp, ci, v)
+    x_cols = orc.gen_x_cols(41 + k, n_cols, k, value_kind=vk, dtype=dt)
+    exp = oracle_mul_dense(orc, a, x_cols)
+    assert_csr_bits(a.mul_dense(Dense.from_columns(x_cols)), *exp)
+
+    lib = _lib.load()
+    h, t = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.check(lib.bsm_csr_mul_dense(a._device().handle, k, n_cols, _lib.ptr_array(x_cols), ctypes.byref(h)))
+    r = _lib.DeviceCsr(h.value)
+    assert r.nnz == int(exp[0][-1])
+    _lib.check(lib.bsm_csr_transpose(r.handle, ctypes.byref(t)))
+    trp, tci, tv = _lib.DeviceCsr(t.value).download()
+    ert, ect, evt = orc.transpose(rows, k, *exp)
+    assert np.array_equal(trp, ert) and np.array_equal(tci, ect)
+    assert np.array_equal(tv.view(np.uint8), np.asarray(evt, dt).view(np.uint8))
+
+    monkeypatch.setenv("BSM_SMALL_OUT", "0")
+    assert_csr_bits(a.mul_dense(Dense.from_columns(x_cols)), *exp)
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_mul_dense_k32_kernel_variants(orc, monkeypatch, variant):
     """Every k = 32 f64 kernel (BSM_SPMM_VARIANT: row-wave, one row per wave
