@@ -110,7 +110,7 @@ template <typename T>
 __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
                                                  int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
                                                  int* __restrict__ flags, int* __restrict__ ticket,
-                                                 int* __restrict__ status) {
+                                                 int* __restrict__ status, int pad_skip) {
     __shared__ T PT[64][TLD];
     __shared__ T QT[64][TLD];
     __shared__ T rd[64];
@@ -191,8 +191,11 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
 #pragma unroll
                 for (int q = 0; q < 4; ++q) PT[rb + 4 * q][16 * cb + cm] = acc[cb][q];
             __syncthreads();
+            // the panels holding real pivots (the front's last pivot tile may
+            // end in identity padding: blk_diag_panels skips those panels)
+            const int rem = nd.np - 64 * K;
             blk_diag_panels<T>(PTl, QTl, (lds_t<T>*)Di, (lds_t<T>*)Tb, (lds_t<T>*)rd, status, tid, nullptr, nullptr,
-                               nullptr, nullptr);
+                               nullptr, nullptr, rem >= 64 || !pad_skip ? 4 : (rem + 15) / 16);
             __syncthreads();
             T* const dk = Dinv + nd.dinv_off + (int64_t)K * 4096;
 #pragma unroll
@@ -551,6 +554,14 @@ struct NdCached {
     size_t n_tiles = 0, n_ext = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
+    // The numeric storage (fronts, inverse diagonal tiles, flags) stays with
+    // the cached plan for the handle's next solve: hipFree of the 5.6 GB of
+    // fronts and hipMalloc again cost ~0.9 ms of a C5 solve's 11.4
+    // (profiles/r05_q_*). One solve at a time uses them (num_mu; a concurrent
+    // solve on the same handle allocates its own). BSM_ND_KEEP=0: freed after
+    // every solve.
+    std::mutex num_mu;
+    DBuf fr, dv, fl;
 };
 
 // The calling thread's page-locked staging buffer (grown on demand, kept for
@@ -669,7 +680,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             a->nd_plan = pc;
         }
     }
-    const NdCached& C = *pc;
+    NdCached& C = *pc;
     if (getenv("BSM_ND_TRACE"))
         fprintf(stderr,
                 "[bsm nd] n %lld nodes %d levels %d: graph %.1f ms, bisection %.1f ms, symbolic %.1f ms, layout "
@@ -686,12 +697,19 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int4* d_tiles = (const int4*)(pb + C.o_tiles);
     const int2* d_ext = (const int2*)(pb + C.o_ext);
     const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
-    // numeric storage
-    DBuf fr, dv, fl;
-    BSM_TRY(fr.alloc((size_t)C.f_elems * sizeof(T)));
-    BSM_TRY(dv.alloc((size_t)std::max<int64_t>(C.dinv_elems, 1) * sizeof(T)));
+    // numeric storage: the plan's own buffers when this solve may hold them
+    const char* ke = getenv("BSM_ND_KEEP");
+    std::unique_lock<std::mutex> num_lock(C.num_mu, std::defer_lock);
+    const bool keep = cache && !(ke && atoi(ke) == 0) && num_lock.try_lock();
+    DBuf own_fr, own_dv, own_fl;
+    DBuf& fr = keep ? C.fr : own_fr;
+    DBuf& dv = keep ? C.dv : own_dv;
+    DBuf& fl = keep ? C.fl : own_fl;
+    const size_t fr_b = (size_t)C.f_elems * sizeof(T), dv_b = (size_t)std::max<int64_t>(C.dinv_elems, 1) * sizeof(T);
     const size_t nfl = (size_t)C.n_flags + (size_t)C.n_levels + 2;
-    BSM_TRY(fl.alloc(nfl * sizeof(int)));
+    if (fr.bytes != fr_b) BSM_TRY(fr.alloc(fr_b));  // a plan serves one dtype per handle; sizes match after
+    if (dv.bytes != dv_b) BSM_TRY(dv.alloc(dv_b));
+    if (fl.bytes != nfl * sizeof(int)) BSM_TRY(fl.alloc(nfl * sizeof(int)));
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* d_flags = fl.as<int>();
     int* d_tickets = d_flags + C.n_flags;
@@ -712,12 +730,15 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nd_factor<T>, 256, 0));
     BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "nd_factor does not fit a CU");
+    // BSM_ND_PAD_SKIP=0: diagonal tiles factor their padding panels too (A/B; same bits)
+    const char* pse = getenv("BSM_ND_PAD_SKIP");
+    const int pad_skip = !(pse && atoi(pse) == 0);
     for (int32_t lv = 0; lv < C.n_levels; ++lv) {
         const int64_t t0 = C.tiles_off[(size_t)lv], nt = C.tiles_off[(size_t)lv + 1] - t0;
         if (nt > 0) {
             const int64_t grid = std::min<int64_t>(nt, (int64_t)cus * per_cu);
             nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                        d_tickets + lv, d_status);
+                                                        d_tickets + lv, d_status, pad_skip);
             BSM_HIP_TRY(hipGetLastError());
         }
         for (int sl = 0; sl < 2; ++sl) {
@@ -729,9 +750,9 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     }
     stage_mark("nd_factor", s);
     if (k > 0) {
-        DBuf bpb, vb;
-        BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T)));
-        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T)));
+        DBuf bpb, vb;  // from the thread's cache of temporaries (no hipFree per solve)
+        BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T), s));
+        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T), s));
         nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
                                                        bpb.as<T>());
         BSM_HIP_TRY(hipGetLastError());

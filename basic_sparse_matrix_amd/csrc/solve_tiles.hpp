@@ -143,17 +143,26 @@ __device__ __forceinline__ void blk_publish_flag(int* rbf, int c, int lane) {
     if (lane == 0) __hip_atomic_store(&rbf[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+//
+// npan < 4 (the nested-dissection fronts' last pivot tile, whose pivots past
+// np are padding: identity rows and columns, zero elsewhere): only panels
+// p < npan hold real pivots. A padding panel's factor, rows below, trailing
+// update and Linv blocks would produce exactly the identity and zeros it
+// already holds (pivot 1: rsqrt 1, L 1, x 1; products with zero rows leave
+// S's bits), so they are skipped and Q's padding diagonal set to 1: the same
+// bits in ~npan / 4 of the time. Uniform across the workgroup (the barriers).
 template <typename T>
 __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<T>* Di, lds_t<T>* Tb, lds_t<T>* rd,
                                                 int* status, int tid, unsigned long long* tdbg,
-                                                T* __restrict__ dpub, int* rbf, int* pflag) {
+                                                T* __restrict__ dpub, int* rbf, int* pflag, int npan = 4) {
     long long ta = 0, tb = 0, tc = 0;  // BSM_BLK_DEBUG: wave 0's block, the rows below, the trailing update
     asm volatile("" : "+v"(tid));  // opaque: keep the per-step masks out of the ticket loop
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     bool pd = true;
 #pragma unroll
     for (int u = 0; u < 16; ++u) Q[(tid >> 2) * TLD + 16 * (tid & 3) + u] = (T)0;  // rows of Linv^T
-    for (int p = 0; p < 4; ++p) {
+    npan = __builtin_amdgcn_readfirstlane(npan);
+    for (int p = 0; p < npan; ++p) {
         const int c0 = 16 * p;
         const long long t0 = tdbg ? clock64() : 0;
         if (dpub && w == 3 && p >= 2) blk_publish_flag(rbf, p - 2, tid & 63);  // row block p - 2, stored a panel ago
@@ -260,12 +269,18 @@ __device__ __forceinline__ void blk_diag_panels(lds_t<T>* P, lds_t<T>* Q, lds_t<
             tc += t3 - t2;
         }
     }
-    // Linv's last row block and diagonal block
-    if (w < 3) {
-        blk_linv_block<T>(P, Q, Di, 3, w, tid & 63);
-    } else {
+    // Linv's last row block and diagonal block (of the real panels)
+    const int pl = npan - 1;
+    if (w < pl) {
+        blk_linv_block<T>(P, Q, Di, pl, w, tid & 63);
+    } else if (w == 3) {
         if (dpub) blk_publish_flag(rbf, 2, tid & 63);
-        blk_linv_diag<T>(Q, Di, 3, tid & 63);
+        blk_linv_diag<T>(Q, Di, pl, tid & 63);
+    }
+    if (tid < 64 - 16 * npan) {  // the padding pivots: Linv's diagonal 1 (the rest of Q is zero), rd 1
+        const int c = 16 * npan + tid;
+        Q[c * TLD + c] = (T)1;
+        rd[c] = (T)1;
     }
     __syncthreads();
     if (w == 0 && (tid & 63) == 0 && !pd) atomicOr(status, ST_NOT_PD);
