@@ -258,6 +258,38 @@ __global__ __launch_bounds__(256) void nd_extend(const NdDev* __restrict__ nodes
     for (int a = b + lane; a < c.m; a += 64) dst[rc[a]] += src[a];
 }
 
+// Both children of a parent in one launch: task (c0, b0, c1, b1) adds column
+// b0 of child c0's update block, then column b1 of child c1's, into the SAME
+// parent column (ri[b0] of c0 == ri[b1] of c1; -1: that child has none), in
+// that order, on one wave: the same sums in the same order as a slot-0 launch
+// followed by a slot-1 launch, and the tasks of a launch own distinct parent
+// columns. The second child's loads are write-through (the first child's
+// stores came from other lanes of this wave) after the wave's stores drain.
+template <typename T>
+__global__ __launch_bounds__(256) void nd_extend2(const NdDev* __restrict__ nodes, const int4* __restrict__ tasks,
+                                                  int64_t ntasks, const int32_t* __restrict__ ri, T* __restrict__ F) {
+    const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (task >= ntasks) return;
+    const int lane = threadIdx.x & 63;
+    const int4 tk = tasks[task];
+    auto add = [&](int ci, int b, bool coherent) {
+        const NdDev& c = nodes[ci];
+        const NdDev& p = nodes[c.parent];
+        const int32_t* rc = ri + c.st_off;
+        const T* src = F + c.foff + (int64_t)(c.np_pad + b) * c.ld + c.np_pad;
+        T* dst = F + p.foff + (int64_t)rc[b] * p.ld;
+        for (int a = b + lane; a < c.m; a += 64) {
+            T* d = dst + rc[a];
+            *d = (coherent ? ld_sc1(d) : *d) + src[a];
+        }
+    };
+    if (tk.x >= 0) add(tk.x, tk.y, false);
+    if (tk.z >= 0) {
+        if (tk.x >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        add(tk.z, tk.w, tk.x >= 0);
+    }
+}
+
 // right-hand sides into the new order: bp[col * n + q] = b[perm[q] * k + col] (b row-major n x k)
 template <typename T>
 __global__ __launch_bounds__(256) void nd_gather(int64_t n, int64_t k, const int64_t* __restrict__ perm,
@@ -448,6 +480,8 @@ struct NdLayout {
     std::vector<int4> tiles;
     std::vector<int2> ext;
     std::vector<int64_t> tiles_off, lvl_off, ext_off;  // per level (ext: per level and slot)
+    std::vector<int4> ext2;                             // nd_extend2's tasks (both slots)
+    std::vector<int64_t> ext2_off;                      // per level
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
 };
 
@@ -534,10 +568,43 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
                 for (int32_t b = 0; b < L.dev[(size_t)i].m; ++b) L.ext.push_back(make_int2(i, b));
             }
         }
+        // both slots in one launch: a slot-0 child's columns, each paired with
+        // the slot-1 sibling's column landing on the same parent column when
+        // that sibling is on this level too, then the sibling's unpaired ones
+        L.ext2_off.push_back((int64_t)L.ext2.size());
+        if (lv.empty()) continue;
+        const int32_t level = P.nodes[(size_t)lv.front()].level;
+        for (int32_t i : lv) {
+            const NdNode& x = P.nodes[(size_t)i];
+            if (x.parent < 0) continue;
+            const NdNode& px = P.nodes[(size_t)x.parent];
+            const int32_t sib = px.kids[1 - x.slot];
+            const bool pair = sib >= 0 && P.nodes[(size_t)sib].level == level;
+            if (pair && x.slot == 1) continue;  // taken with its slot-0 sibling
+            const int32_t m0 = L.dev[(size_t)i].m;
+            const int32_t* r0 = L.ri.data() + L.dev[(size_t)i].st_off;
+            if (!pair) {
+                for (int32_t b = 0; b < m0; ++b) L.ext2.push_back(make_int4(i, b, -1, -1));
+                continue;
+            }
+            const int32_t m1 = L.dev[(size_t)sib].m;
+            const int32_t* r1 = L.ri.data() + L.dev[(size_t)sib].st_off;
+            std::vector<char> used((size_t)m1, 0);
+            int32_t b1 = 0;
+            for (int32_t b = 0; b < m0; ++b) {  // ri ascending on both sides: one merge walk
+                while (b1 < m1 && r1[b1] < r0[b]) ++b1;
+                const bool hit = b1 < m1 && r1[b1] == r0[b];
+                if (hit) used[(size_t)b1] = 1;
+                L.ext2.push_back(make_int4(i, b, hit ? sib : -1, hit ? b1 : -1));
+            }
+            for (int32_t b = 0; b < m1; ++b)
+                if (!used[(size_t)b]) L.ext2.push_back(make_int4(sib, b, -1, -1));
+        }
     }
     L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
     L.tiles_off.push_back((int64_t)L.tiles.size());
     L.ext_off.push_back((int64_t)L.ext.size());
+    L.ext2_off.push_back((int64_t)L.ext2.size());
 }
 
 // A pattern's plan, device side: one allocation holding the node
@@ -548,9 +615,10 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
 struct NdCached {
     int64_t leaf = 0;
     int32_t nn = 0, n_levels = 0;
-    std::vector<int64_t> tiles_off, lvl_off, ext_off;
+    std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off;
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
-    size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_perm = 0;
+    size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
+           o_perm = 0;
     size_t n_tiles = 0, n_ext = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
@@ -611,6 +679,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.tiles_off = L.tiles_off;
     C.lvl_off = L.lvl_off;
     C.ext_off = L.ext_off;
+    C.ext2_off = L.ext2_off;
     C.f_elems = L.f_elems;
     C.dinv_elems = L.dinv_elems;
     C.n_flags = L.n_flags;
@@ -631,7 +700,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.o_lvl = C.o_owner + al(L.owner.size() * 4);
     C.o_tiles = C.o_lvl + al(L.lvl_nodes.size() * 4);
     C.o_ext = C.o_tiles + al(L.tiles.size() * sizeof(int4));
-    C.o_perm = C.o_ext + al(L.ext.size() * sizeof(int2));
+    C.o_ext2 = C.o_ext + al(L.ext.size() * sizeof(int2));
+    C.o_perm = C.o_ext2 + al(L.ext2.size() * sizeof(int4));
     const size_t total = C.o_perm + al((size_t)N * 8);
     const auto tp0 = host_now();
     char* hp = nullptr;
@@ -647,6 +717,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     put(C.o_lvl, L.lvl_nodes.data(), L.lvl_nodes.size() * 4);
     put(C.o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
     put(C.o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
+    put(C.o_ext2, L.ext2.data(), L.ext2.size() * sizeof(int4));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
     C.ms_pack = ms_since(tp0);
     BSM_TRY(C.plan.alloc(total));
@@ -696,6 +767,10 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int32_t* d_lvl = (const int32_t*)(pb + C.o_lvl);
     const int4* d_tiles = (const int4*)(pb + C.o_tiles);
     const int2* d_ext = (const int2*)(pb + C.o_ext);
+    const int4* d_ext2 = (const int4*)(pb + C.o_ext2);
+    // BSM_ND_EXT_MERGE=0: one extend launch per child slot (A/B; same bits)
+    const char* eme = getenv("BSM_ND_EXT_MERGE");
+    const bool ext_merge = !(eme && atoi(eme) == 0);
     const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
     // numeric storage: the plan's own buffers when this solve may hold them
     const char* ke = getenv("BSM_ND_KEEP");
@@ -741,7 +816,14 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
                                                         d_tickets + lv, d_status, pad_skip);
             BSM_HIP_TRY(hipGetLastError());
         }
-        for (int sl = 0; sl < 2; ++sl) {
+        if (ext_merge) {
+            const int64_t e0 = C.ext2_off[(size_t)lv], ne = C.ext2_off[(size_t)lv + 1] - e0;
+            if (ne > 0) {
+                nd_extend2<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext2 + e0, ne, d_ri, F);
+                BSM_HIP_TRY(hipGetLastError());
+            }
+        }
+        for (int sl = 0; sl < 2 && !ext_merge; ++sl) {
             const int64_t e0 = C.ext_off[(size_t)(2 * lv + sl)], ne = C.ext_off[(size_t)(2 * lv + sl) + 1] - e0;
             if (ne <= 0) continue;
             nd_extend<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext + e0, ne, d_ri, F);

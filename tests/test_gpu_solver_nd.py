@@ -178,14 +178,18 @@ def test_nd_deterministic(orc, g):
     assert rel_err(x0, ex) < 1e-10
 
 
+@pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
-def test_nd_padding_panels_skipped_same_bits(orc, monkeypatch, dtype, leaf):
-    """A front's last pivot tile ends in identity padding when np is not a
-    multiple of 64; its factor skips the padding's 16-column panels, which
-    would only reproduce that identity: x has the same bits as with every
-    panel factored (BSM_ND_PAD_SKIP=0), and a fresh handle per run (no cached
-    plan or buffers shared between the two)."""
+def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
+    """Two shortcuts that must not change a bit, each against its switch set
+    to 0 (a fresh handle per run: no cached plan or buffers shared):
+    * BSM_ND_PAD_SKIP: a front's last pivot tile ends in identity padding
+      when np is not a multiple of 64; its factor skips the padding's
+      16-column panels, which would only reproduce that identity;
+    * BSM_ND_EXT_MERGE: both children's update blocks go into the parent in
+      one launch (child 0's column, then child 1's, on one wave) instead of
+      one launch per child: the same adds in the same order."""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
     g = 90
     n = g * g
@@ -193,7 +197,7 @@ def test_nd_padding_panels_skipped_same_bits(orc, monkeypatch, dtype, leaf):
     v = v.astype(dtype)
     b = orc.gen_x_cols(1013, n, 2, dtype=dtype)
     x_skip = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
-    monkeypatch.setenv("BSM_ND_PAD_SKIP", "0")
+    monkeypatch.setenv(switch, "0")
     x_full = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
     for j in range(2):
         a0, a1 = np.asarray(x_skip.get_col(j)), np.asarray(x_full.get_col(j))
