@@ -112,7 +112,10 @@ int bsm_csr_from_coo(int dtype, uint64_t rows, uint64_t cols, uint64_t n, const 
                      const uint64_t* col, const void* vals, bsm_csr** out);
 int bsm_csr_shape(const bsm_csr* m, uint64_t* rows, uint64_t* cols, uint64_t* nnz,
                   int* dtype);
-/* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz). */
+/* Copy a handle back into caller-allocated host arrays (rows+1, nnz, nnz).
+ * A small bsm_csr_mul_dense result (at most 8,192 rows and 131,072 row x
+ * column slots) carries a host copy written by the same kernel as its device
+ * arrays: its download is a host copy with no device work. */
 int bsm_csr_download(const bsm_csr* m, uint64_t* row_ptr, uint64_t* col_idx, void* vals);
 /* Page-lock (hipHostRegister) / release a caller-owned host range that result
  * arrays are downloaded into again and again (this build's addition; no
