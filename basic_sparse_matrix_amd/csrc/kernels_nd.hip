@@ -390,6 +390,128 @@ __global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ node
     }
 }
 
+// A solve wave waits on a pivot tile of its own front that a running wave
+// publishes within microseconds: ~1 s of polls is a hang (reported as
+// ST_TIMEOUT, not spun on for the factor's ~30 s)
+constexpr long long ND_SOLVE_SPIN_LIMIT = 1ll << 20;
+
+// Forward solve of one level by tile rows: one wave per (node, tile row I,
+// column), taken by ticket in I-major order across the level's fronts (a
+// wave only waits on lower tickets, which are running or done). The wave
+// forms its 64 rows' v (the pivots of bp, then child 0's and child 1's
+// update entries landing in these rows), subtracts L_IK y_K for K < min(I,
+// npt) as each y_K is published (flag per node, column and pivot tile), and,
+// for a pivot tile, forms y_I = Dinv_I v_I and publishes it. Per row the
+// same operations in the same order as nd_forward (one thread per row, the
+// 64-term products in four accumulators; y from four 16-term partials):
+// the same bits, with the fronts' chains of pivot tiles running on as many
+// waves as the front has tile rows instead of one workgroup
+// (BSM_ND_FWD_TILES=0: nd_forward, for the A/B).
+template <typename T>
+__global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__ nodes, const int2* __restrict__ tasks,
+                                                       int64_t ntasks, int k, int64_t n, const T* __restrict__ bp,
+                                                       T* __restrict__ V, int64_t vtot, const T* __restrict__ F,
+                                                       const T* __restrict__ Dinv, const int32_t* __restrict__ ri,
+                                                       int* __restrict__ yflags, int* __restrict__ ticket,
+                                                       int* __restrict__ status) {
+    __shared__ T yk[64];
+    __shared__ T add[2][64];
+    __shared__ int hit[2][64];
+    __shared__ int64_t tk;
+    const int lane = threadIdx.x;
+    for (;;) {
+        if (lane == 0) tk = atomicAdd(ticket, 1);
+        __syncthreads();
+        const int64_t t = __builtin_amdgcn_readfirstlane((int)tk);
+        if (t >= ntasks * k) break;
+        const int2 task = tasks[t / k];
+        const int col = (int)(t % k);
+        const NdDev& nd = nodes[task.x];
+        const int I = task.y;
+        T* const v = V + (int64_t)col * vtot + nd.voff;
+        int* const yf = yflags + (nd.dinv_off / 4096) * k + (int64_t)col * nd.npt;
+        const int r = 64 * I + lane;
+        T val = r < nd.np ? bp[(int64_t)col * n + nd.start + r] : (T)0;
+        // the children's update entries in rows [64 I, 64 I + 64): ri is
+        // ascending, so they are one range of each child's entries
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            hit[sl][lane] = 0;
+            const int kid = sl == 0 ? nd.kid0 : nd.kid1;
+            if (kid < 0) continue;
+            const NdDev& c = nodes[kid];
+            const int32_t* rc = ri + c.st_off;
+            const int32_t lo = lower_bound_i32(rc, c.m, 64 * I), hi = lower_bound_i32(rc, c.m, 64 * I + 64);
+            const T* u = V + (int64_t)col * vtot + c.voff + c.np_pad;
+            __syncthreads();
+            for (int32_t a = lo + lane; a < hi; a += 64) {
+                add[sl][rc[a] - 64 * I] = u[a];
+                hit[sl][rc[a] - 64 * I] = 1;
+            }
+        }
+        __syncthreads();
+        if (nd.kid0 >= 0 && hit[0][lane]) val = val + add[0][lane];
+        if (nd.kid1 >= 0 && hit[1][lane]) val = val + add[1][lane];
+        const T* const lrow = F + nd.foff + r;
+        const int64_t ld = nd.ld;
+        const int Kn = I < nd.npt ? I : nd.npt;
+        for (int K = 0; K < Kn; ++K) {
+            if (lane == 0) {
+                long long spins = 0;
+                while (__hip_atomic_load(&yf[K], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > ND_SOLVE_SPIN_LIMIT) {
+                        atomicOr(status, ST_TIMEOUT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            T lv[64];
+#pragma unroll
+            for (int q = 0; q < 64; ++q) lv[q] = lrow[(int64_t)(64 * K + q) * ld];
+            yk[lane] = ld_sc1(&v[64 * K + lane]);
+            __syncthreads();
+            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+            for (int q = 0; q < 64; q += 4) {
+                s0 = fma_t(lv[q], yk[q], s0);
+                s1 = fma_t(lv[q + 1], yk[q + 1], s1);
+                s2 = fma_t(lv[q + 2], yk[q + 2], s2);
+                s3 = fma_t(lv[q + 3], yk[q + 3], s3);
+            }
+            val = val - ((s0 + s1) + (s2 + s3));
+            __syncthreads();
+        }
+        if (I < nd.npt) {  // y_I = Dinv_I v_I, as nd_forward's four 16-term partials
+            yk[lane] = val;
+            __syncthreads();
+            const T* g = Dinv + nd.dinv_off + (int64_t)I * 4096 + lane;
+            T part[4];
+#pragma unroll
+            for (int wv = 0; wv < 4; ++wv) {
+                T gv[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) gv[j] = g[(16 * wv + j) * 64];
+                T y0 = (T)0, y1 = (T)0;
+#pragma unroll
+                for (int j = 0; j < 16; j += 2) {
+                    y0 = fma_t(gv[j], yk[16 * wv + j], y0);
+                    y1 = fma_t(gv[j + 1], yk[16 * wv + j + 1], y1);
+                }
+                part[wv] = y0 + y1;
+            }
+            st_sc1(&v[r], (part[0] + part[1]) + (part[2] + part[3]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (lane == 0) __hip_atomic_store(&yf[I], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            st_sc1(&v[r], val);
+        }
+        __syncthreads();
+    }
+}
+
 // Backward solve of one level, one workgroup per (node, column): w = y over
 // the pivots, the ancestors' x over the front rows; per pivot tile K from the
 // last, x_K = Dinv_K^T (y_K - L_{>K,K}^T w_{>K}); the pivots' x to xp.
@@ -417,20 +539,24 @@ __global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nod
         T acc[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) acc[c] = (T)0;
+        // rows by tile from the LAST tile down to K + 1 (the front rows, known
+        // from the start, first: nd_backward_tiles sums in this order while
+        // the pivot tiles' x arrive)
         const T* lc = Fn + (int64_t)(64 * K + 16 * wv) * ld;
-        int r = 64 * (K + 1) + lane;
-        for (; r + 64 < fp; r += 128) {
-            const T w0 = ld_sc1(&w[r]), w1 = ld_sc1(&w[r + 64]);
+        const int rlo = 64 * (K + 1);
+        int r = fp - 64 + lane;
+        for (; r - 64 >= rlo; r -= 128) {
+            const T w0 = ld_sc1(&w[r]), w1 = ld_sc1(&w[r - 64]);
             T l0[16], l1[16];
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 l0[c] = lc[(int64_t)c * ld + r];
-                l1[c] = lc[(int64_t)c * ld + r + 64];
+                l1[c] = lc[(int64_t)c * ld + r - 64];
             }
 #pragma unroll
             for (int c = 0; c < 16; ++c) acc[c] = fma_t(l1[c], w1, fma_t(l0[c], w0, acc[c]));
         }
-        if (r < fp) {
+        if (r >= rlo) {
             const T w0 = ld_sc1(&w[r]);
 #pragma unroll
             for (int c = 0; c < 16; ++c) acc[c] = fma_t(lc[(int64_t)c * ld + r], w0, acc[c]);
@@ -471,6 +597,127 @@ __global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nod
     for (int p = tid; p < nd.np; p += 256) xp[col * n + nd.start + p] = ld_sc1(&w[p]);
 }
 
+// Backward solve of one level by pivot tiles: one workgroup per (node, pivot
+// tile K, column), taken by ticket from the fronts' last pivot tiles down (a
+// workgroup only waits on lower tickets). It sums the column products of
+// the rows below tile K as nd_backward does, tile by tile from the last: the
+// front rows (the ancestors' x, read through st) at once, then each pivot
+// tile J > K as its x_J is published (flag per node, column and pivot tile);
+// then x_K = Dinv_K^T (y_K - sums) and its pivots to xp. The same operations
+// in the same order per lane as nd_backward: the same bits
+// (BSM_ND_BWD_TILES=0 for the A/B).
+template <typename T>
+__global__ __launch_bounds__(256) void nd_backward_tiles(const NdDev* __restrict__ nodes,
+                                                         const int2* __restrict__ tasks, int64_t ntasks, int k,
+                                                         int64_t n, T* __restrict__ xp, T* __restrict__ V,
+                                                         int64_t vtot, const T* __restrict__ F,
+                                                         const T* __restrict__ Dinv, const int32_t* __restrict__ st,
+                                                         int* __restrict__ xflags, int* __restrict__ ticket,
+                                                         int* __restrict__ status) {
+    __shared__ T red[64][65];
+    __shared__ T zk[64];
+    __shared__ T part[4][64];
+    __shared__ int tk;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t total = ntasks * k;
+    // Control flow kept simple for the structurizer (a first form, with the
+    // ticket taken at the loop head and a barrier inside an if / else of the
+    // row loop, compiled to a loop whose back edge skipped the ticket: the
+    // workgroup redid its first task forever): the ticket is taken at the
+    // END of each task, both row loops are plain counted loops, and the
+    // flag poll has no break.
+    if (tid == 0) tk = atomicAdd(ticket, 1);
+    __syncthreads();
+    int64_t t = __builtin_amdgcn_readfirstlane(tk);
+    while (t < total) {
+        const int2 task = tasks[t / k];
+        const int col = (int)(t % k);
+        const NdDev& nd = nodes[task.x];
+        const int K = task.y;
+        T* const w = V + (int64_t)col * vtot + nd.voff;
+        int* const xf = xflags + (nd.dinv_off / 4096) * k + (int64_t)col * nd.npt;
+        const int32_t* const sr = st + nd.st_off;
+        const T* const lc = F + nd.foff + (int64_t)(64 * K + 16 * wv) * nd.ld;
+        const int64_t ld = nd.ld;
+        T acc[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = (T)0;
+        // the front rows' tiles, last first: the ancestors' x (0 past the m rows)
+        const int jf = nd.npt > K + 1 ? nd.npt : K + 1;
+        for (int J = nd.nt - 1; J >= jf; --J) {
+            const int r = 64 * J + lane, a = r - nd.np_pad;
+            const T wr = a < nd.m ? xp[(int64_t)col * n + sr[a]] : (T)0;
+            T l[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) l[c] = lc[(int64_t)c * ld + r];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma_t(l[c], wr, acc[c]);
+        }
+        // then the pivot tiles below K, each as its x is published
+        for (int J = nd.npt - 1; J > K; --J) {
+            if (tid == 0) {
+                long long spins = 0;
+                while (__hip_atomic_load(&xf[J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                       spins < ND_SOLVE_SPIN_LIMIT) {
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                }
+                if (spins >= ND_SOLVE_SPIN_LIMIT) atomicOr(status, ST_TIMEOUT);
+            }
+            __syncthreads();
+            const int r = 64 * J + lane;
+            const T wr = ld_sc1(&w[r]);
+            T l[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) l[c] = lc[(int64_t)c * ld + r];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) acc[c] = fma_t(l[c], wr, acc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) red[16 * wv + c][lane] = acc[c];
+        __syncthreads();
+        if (tid < 64) {
+            T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
+#pragma unroll
+            for (int l = 0; l < 64; l += 4) {
+                s0 += red[tid][l];
+                s1 += red[tid][l + 1];
+                s2 += red[tid][l + 2];
+                s3 += red[tid][l + 3];
+            }
+            zk[tid] = ld_sc1(&w[64 * K + tid]) - ((s0 + s1) + (s2 + s3));
+        }
+        __syncthreads();
+        {  // x_K = Dinv_K^T z, as nd_backward
+            const T* g = Dinv + nd.dinv_off + (int64_t)K * 4096 + (int64_t)lane * 64 + 16 * wv;
+            T gv[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) gv[j] = g[j];
+            T x0 = (T)0, x1 = (T)0;
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                x0 = fma_t(gv[j], zk[16 * wv + j], x0);
+                x1 = fma_t(gv[j + 1], zk[16 * wv + j + 1], x1);
+            }
+            part[wv][lane] = x0 + x1;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            const T x = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+            st_sc1(&w[64 * K + tid], x);
+            if (64 * K + tid < nd.np) xp[(int64_t)col * n + nd.start + 64 * K + tid] = x;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_store(&xf[K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tk = atomicAdd(ticket, 1);
+        }
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(tk);
+    }
+}
+
 inline unsigned nd_blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 // the device form of a plan: node descriptors, front rows, tile and task lists
@@ -482,6 +729,10 @@ struct NdLayout {
     std::vector<int64_t> tiles_off, lvl_off, ext_off;  // per level (ext: per level and slot)
     std::vector<int4> ext2;                             // nd_extend2's tasks (both slots)
     std::vector<int64_t> ext2_off;                      // per level
+    std::vector<int2> ftasks;                           // nd_forward_tiles' (node, tile row), I-major
+    std::vector<int64_t> ftask_off;                     // per level
+    std::vector<int2> btasks;                           // nd_backward_tiles' (node, pivot tile), last tiles first
+    std::vector<int64_t> btask_off;                     // per level
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
 };
 
@@ -571,6 +822,16 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
         // both slots in one launch: a slot-0 child's columns, each paired with
         // the slot-1 sibling's column landing on the same parent column when
         // that sibling is on this level too, then the sibling's unpaired ones
+        L.ftask_off.push_back((int64_t)L.ftasks.size());
+        for (int32_t I = 0; I < kmax; ++I)
+            for (int32_t i : lv)
+                if (I < L.dev[(size_t)i].nt) L.ftasks.push_back(make_int2(i, I));
+        L.btask_off.push_back((int64_t)L.btasks.size());
+        int32_t pmax = 0;
+        for (int32_t i : lv) pmax = std::max(pmax, L.dev[(size_t)i].npt);
+        for (int32_t d = 0; d < pmax; ++d)
+            for (int32_t i : lv)
+                if (d < L.dev[(size_t)i].npt) L.btasks.push_back(make_int2(i, L.dev[(size_t)i].npt - 1 - d));
         L.ext2_off.push_back((int64_t)L.ext2.size());
         if (lv.empty()) continue;
         const int32_t level = P.nodes[(size_t)lv.front()].level;
@@ -605,6 +866,8 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
     L.tiles_off.push_back((int64_t)L.tiles.size());
     L.ext_off.push_back((int64_t)L.ext.size());
     L.ext2_off.push_back((int64_t)L.ext2.size());
+    L.ftask_off.push_back((int64_t)L.ftasks.size());
+    L.btask_off.push_back((int64_t)L.btasks.size());
 }
 
 // A pattern's plan, device side: one allocation holding the node
@@ -615,10 +878,10 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
 struct NdCached {
     int64_t leaf = 0;
     int32_t nn = 0, n_levels = 0;
-    std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off;
+    std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off, ftask_off, btask_off;
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
-           o_perm = 0;
+           o_ftask = 0, o_btask = 0, o_perm = 0;
     size_t n_tiles = 0, n_ext = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
@@ -680,6 +943,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.lvl_off = L.lvl_off;
     C.ext_off = L.ext_off;
     C.ext2_off = L.ext2_off;
+    C.ftask_off = L.ftask_off;
+    C.btask_off = L.btask_off;
     C.f_elems = L.f_elems;
     C.dinv_elems = L.dinv_elems;
     C.n_flags = L.n_flags;
@@ -701,7 +966,9 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.o_tiles = C.o_lvl + al(L.lvl_nodes.size() * 4);
     C.o_ext = C.o_tiles + al(L.tiles.size() * sizeof(int4));
     C.o_ext2 = C.o_ext + al(L.ext.size() * sizeof(int2));
-    C.o_perm = C.o_ext2 + al(L.ext2.size() * sizeof(int4));
+    C.o_ftask = C.o_ext2 + al(L.ext2.size() * sizeof(int4));
+    C.o_btask = C.o_ftask + al(L.ftasks.size() * sizeof(int2));
+    C.o_perm = C.o_btask + al(L.btasks.size() * sizeof(int2));
     const size_t total = C.o_perm + al((size_t)N * 8);
     const auto tp0 = host_now();
     char* hp = nullptr;
@@ -718,6 +985,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     put(C.o_tiles, L.tiles.data(), L.tiles.size() * sizeof(int4));
     put(C.o_ext, L.ext.data(), L.ext.size() * sizeof(int2));
     put(C.o_ext2, L.ext2.data(), L.ext2.size() * sizeof(int4));
+    put(C.o_ftask, L.ftasks.data(), L.ftasks.size() * sizeof(int2));
+    put(C.o_btask, L.btasks.data(), L.btasks.size() * sizeof(int2));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
     C.ms_pack = ms_since(tp0);
     BSM_TRY(C.plan.alloc(total));
@@ -768,6 +1037,8 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int4* d_tiles = (const int4*)(pb + C.o_tiles);
     const int2* d_ext = (const int2*)(pb + C.o_ext);
     const int4* d_ext2 = (const int4*)(pb + C.o_ext2);
+    const int2* d_ftask = (const int2*)(pb + C.o_ftask);
+    const int2* d_btask = (const int2*)(pb + C.o_btask);
     // BSM_ND_EXT_MERGE=0: one extend launch per child slot (A/B; same bits)
     const char* eme = getenv("BSM_ND_EXT_MERGE");
     const bool ext_merge = !(eme && atoi(eme) == 0);
@@ -838,19 +1109,60 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
                                                        bpb.as<T>());
         BSM_HIP_TRY(hipGetLastError());
+        // Levels with fewer (node, column) pairs than CUs run their solves by
+        // tiles (nd_forward_tiles / nd_backward_tiles: a front's chain of pivot
+        // tiles on many waves), the others one workgroup per pair (nd_forward /
+        // nd_backward: less bookkeeping per front). Same bits either way.
+        // BSM_ND_FWD_TILES / BSM_ND_BWD_TILES = 0: never, 1: every level.
+        const char* fte = getenv("BSM_ND_FWD_TILES");
+        const char* bte = getenv("BSM_ND_BWD_TILES");
+        const int fwd_mode = fte ? atoi(fte) : 2, bwd_mode = bte ? atoi(bte) : 2;
+        auto by_tiles = [&](int mode, int64_t pairs) { return mode == 1 || (mode == 2 && pairs < cus); };
+        const int64_t n_pf = (C.dinv_elems / 4096) * (int64_t)k;  // flags per pass: one per node, column, pivot tile
+        DBuf tfl;
+        const size_t n_tf = 2 * (size_t)n_pf + 2 * (size_t)C.n_levels;  // forward flags, backward flags, tickets
+        BSM_TRY(tfl.alloc(n_tf * sizeof(int), s));
+        BSM_HIP_TRY(hipMemsetAsync(tfl.p, 0, n_tf * sizeof(int), s));
+        int* const d_yf = tfl.as<int>();
+        int* const d_xf = d_yf + n_pf;
+        int* const d_ftk = d_xf + n_pf;
+        int* const d_btk = d_ftk + C.n_levels;
+        int fper = 0, bper = 0;
+        BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&fper, nd_forward_tiles<T>, 64, 0));
+        BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bper, nd_backward_tiles<T>, 256, 0));
+        BSM_REQUIRE(fper >= 1 && bper >= 1, BSM_ERR_UNSUPPORTED, "nd solve kernels do not fit a CU");
+        const int64_t fwd_grid = (int64_t)cus * fper, bwd_grid = (int64_t)cus * bper;
         for (int32_t lv = 0; lv < C.n_levels; ++lv) {
             const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
             if (c <= 0) continue;
-            nd_forward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
-                                                                        vb.as<T>(), C.vtot, F, dv.as<T>(), d_ri);
+            if (by_tiles(fwd_mode, c * (int64_t)k)) {
+                const int64_t f0 = C.ftask_off[(size_t)lv], nf = C.ftask_off[(size_t)lv + 1] - f0;
+                const int64_t grid = std::min<int64_t>(nf * (int64_t)k, fwd_grid);
+                if (grid <= 0) continue;  // fronts without rows (no pivots, no front rows)
+                nd_forward_tiles<T><<<(unsigned)grid, 64, 0, s>>>(d_nodes, d_ftask + f0, nf, (int)k, N, bpb.as<T>(),
+                                                                  vb.as<T>(), C.vtot, F, dv.as<T>(), d_ri, d_yf,
+                                                                  d_ftk + lv, d_status);
+            } else {
+                nd_forward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
+                                                                            vb.as<T>(), C.vtot, F, dv.as<T>(), d_ri);
+            }
             BSM_HIP_TRY(hipGetLastError());
         }
         stage_mark("nd_forward", s);
         for (int32_t lv = C.n_levels - 1; lv >= 0; --lv) {
             const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
             if (c <= 0) continue;
-            nd_backward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
-                                                                         vb.as<T>(), C.vtot, F, dv.as<T>(), d_st);
+            if (by_tiles(bwd_mode, c * (int64_t)k)) {
+                const int64_t b0 = C.btask_off[(size_t)lv], nb = C.btask_off[(size_t)lv + 1] - b0;
+                const int64_t grid = std::min<int64_t>(nb * (int64_t)k, bwd_grid);
+                if (grid <= 0) continue;  // no pivots on this level
+                nd_backward_tiles<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_btask + b0, nb, (int)k, N,
+                                                                    bpb.as<T>(), vb.as<T>(), C.vtot, F, dv.as<T>(),
+                                                                    d_st, d_xf, d_btk + lv, d_status);
+            } else {
+                nd_backward<T><<<dim3((unsigned)c, (unsigned)k), 256, 0, s>>>(d_nodes, d_lvl + o, N, bpb.as<T>(),
+                                                                             vb.as<T>(), C.vtot, F, dv.as<T>(), d_st);
+            }
             BSM_HIP_TRY(hipGetLastError());
         }
         stage_mark("nd_backward", s);

@@ -178,7 +178,7 @@ def test_nd_deterministic(orc, g):
     assert rel_err(x0, ex) < 1e-10
 
 
-@pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE"])
+@pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -189,7 +189,17 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
       16-column panels, which would only reproduce that identity;
     * BSM_ND_EXT_MERGE: both children's update blocks go into the parent in
       one launch (child 0's column, then child 1's, on one wave) instead of
-      one launch per child: the same adds in the same order."""
+      one launch per child: the same adds in the same order;
+    * BSM_ND_FWD_TILES: the forward solve by tile rows (one wave per node,
+      tile row and column, pivot tiles' y published by flags) instead of one
+      workgroup per node and column: per row the same operations in the
+      same order;
+    * BSM_ND_BWD_TILES: the backward solve by pivot tiles (one workgroup per
+      node, pivot tile and column; the front rows' products first, then each
+      pivot tile's as its x arrives) instead of one workgroup per node and
+      column, which sums its rows in that same tile order.
+    (At this size every level has fewer fronts than CUs, so the default runs
+    the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
     g = 90
     n = g * g
