@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void nd_scatter(int64_t n, int64_t k, const in
 // loads are issued together (unrolled): a loop of load, wait, FMA is one
 // L2 round trip per term, 64 per tile step.
 template <typename T>
-__global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ nodes, const int32_t* __restrict__ lvl,
+__global__ __launch_bounds__(256, 4) void nd_forward(const NdDev* __restrict__ nodes, const int32_t* __restrict__ lvl,
                                                   int64_t n, const T* __restrict__ bp, T* __restrict__ V, int64_t vtot,
                                                   const T* __restrict__ F, const T* __restrict__ Dinv,
                                                   const int32_t* __restrict__ ri) {
@@ -370,18 +370,25 @@ __global__ __launch_bounds__(256) void nd_forward(const NdDev* __restrict__ node
         }
         __syncthreads();
         for (int r = 64 * (K + 1) + tid; r < fp; r += 256) {
+            // the row's 64 terms in two halves of 32 loads in flight: at 226
+            // VGPRs (all 64 at once) two workgroups fit a CU, at <= 128 four
+            // (the leaf level is latency bound: 7,699 fronts at C5); same
+            // accumulators, same order, same bits
             const T* lc = Fn + (int64_t)64 * K * ld + r;
-            T lv[64];
-#pragma unroll
-            for (int t = 0; t < 64; ++t) lv[t] = lc[(int64_t)t * ld];
             const T vr = ld_sc1(&v[r]);
             T s0 = (T)0, s1 = (T)0, s2 = (T)0, s3 = (T)0;
 #pragma unroll
-            for (int t = 0; t < 64; t += 4) {
-                s0 = fma_t(lv[t], yk[t], s0);
-                s1 = fma_t(lv[t + 1], yk[t + 1], s1);
-                s2 = fma_t(lv[t + 2], yk[t + 2], s2);
-                s3 = fma_t(lv[t + 3], yk[t + 3], s3);
+            for (int h = 0; h < 64; h += 32) {
+                T lv[32];
+#pragma unroll
+                for (int t = 0; t < 32; ++t) lv[t] = lc[(int64_t)(h + t) * ld];
+#pragma unroll
+                for (int t = 0; t < 32; t += 4) {
+                    s0 = fma_t(lv[t], yk[h + t], s0);
+                    s1 = fma_t(lv[t + 1], yk[h + t + 1], s1);
+                    s2 = fma_t(lv[t + 2], yk[h + t + 2], s2);
+                    s3 = fma_t(lv[t + 3], yk[h + t + 3], s3);
+                }
             }
             st_sc1(&v[r], vr - ((s0 + s1) + (s2 + s3)));
         }
