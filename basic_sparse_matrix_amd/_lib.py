@@ -107,6 +107,8 @@ SIGNATURES = [
     ("bsm_solve_blocked", _int, [_vp, _u64, _u64, _pp, _pp]),
     ("bsm_solve_nd", _int, [_vp, _u64, _u64, _pp, _pp]),
     ("bsm_nd_analyse", _int, [_u64, _vp, _vp, _u64, _vp, _vp, _u64, _u64p, _vp, _u64, _u64p]),
+    ("bsm_nd_cache_clear", _int, []),
+    ("bsm_nd_cache_info", _int, [_u64p, _u64p, _u64p, _u64p]),
     ("bsm_dev_gen_row_ptr", _int, [_u64, _u64, _u64, _u32, _int, _u32, _u32, _vp, _vp, _u64, _vp]),
     ("bsm_dev_gen_entries", _int, [_int, _u64, _u64, _u64, _u32, _int, _vp, _vp, _vp, _vp]),
     ("bsm_dev_gen_dense", _int, [_int, _u64, _u64, _u64, _u64, _int, _vp, _vp]),
@@ -197,6 +199,18 @@ def stage_times() -> dict:
         key = names.raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
         out[key] = out.get(key, 0.0) + ms[i]
     return out
+
+
+def nd_cache_info() -> dict:
+    """State of solve(order="nd")'s plan cache across handles (bsm_nd_cache_info)."""
+    vals = [ctypes.c_uint64(0) for _ in range(4)]
+    check(load().bsm_nd_cache_info(*[ctypes.byref(v) for v in vals]))
+    return dict(zip(("entries", "kept_bytes", "hits", "misses"), (v.value for v in vals)))
+
+
+def nd_cache_clear() -> None:
+    """Drop every cached nd plan not also held by a live handle (bsm_nd_cache_clear)."""
+    check(load().bsm_nd_cache_clear())
 
 
 def last_error() -> str:

@@ -19,6 +19,7 @@
 // Not bit-exact with the reference (another elimination order, FMA); within
 // the north star's f64 tolerance (tests/test_gpu_solver_nd.py).
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <thread>
 #include <type_traits>
@@ -424,13 +425,17 @@ __global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__
     __shared__ T yk[64];
     __shared__ T add[2][64];
     __shared__ int hit[2][64];
-    __shared__ int64_t tk;
+    __shared__ int tk;
     const int lane = threadIdx.x;
-    for (;;) {
-        if (lane == 0) tk = atomicAdd(ticket, 1);
-        __syncthreads();
-        const int64_t t = __builtin_amdgcn_readfirstlane((int)tk);
-        if (t >= ntasks * k) break;
+    const int64_t total = ntasks * k;
+    // The control-flow shape of nd_backward_tiles (whose first form, with the
+    // ticket at the loop head, compiled to a loop that never took a new
+    // ticket): the ticket is taken at the END of each task, the flag poll has
+    // no break, and no barrier sits inside a branch.
+    if (lane == 0) tk = atomicAdd(ticket, 1);
+    __syncthreads();
+    int64_t t = __builtin_amdgcn_readfirstlane(tk);
+    while (t < total) {
         const int2 task = tasks[t / k];
         const int col = (int)(t % k);
         const NdDev& nd = nodes[task.x];
@@ -441,19 +446,21 @@ __global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__
         T val = r < nd.np ? bp[(int64_t)col * n + nd.start + r] : (T)0;
         // the children's update entries in rows [64 I, 64 I + 64): ri is
         // ascending, so they are one range of each child's entries
+        hit[0][lane] = 0;
+        hit[1][lane] = 0;
+        __syncthreads();
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-            hit[sl][lane] = 0;
             const int kid = sl == 0 ? nd.kid0 : nd.kid1;
-            if (kid < 0) continue;
-            const NdDev& c = nodes[kid];
-            const int32_t* rc = ri + c.st_off;
-            const int32_t lo = lower_bound_i32(rc, c.m, 64 * I), hi = lower_bound_i32(rc, c.m, 64 * I + 64);
-            const T* u = V + (int64_t)col * vtot + c.voff + c.np_pad;
-            __syncthreads();
-            for (int32_t a = lo + lane; a < hi; a += 64) {
-                add[sl][rc[a] - 64 * I] = u[a];
-                hit[sl][rc[a] - 64 * I] = 1;
+            if (kid >= 0) {
+                const NdDev& c = nodes[kid];
+                const int32_t* rc = ri + c.st_off;
+                const int32_t lo = lower_bound_i32(rc, c.m, 64 * I), hi = lower_bound_i32(rc, c.m, 64 * I + 64);
+                const T* u = V + (int64_t)col * vtot + c.voff + c.np_pad;
+                for (int32_t a = lo + lane; a < hi; a += 64) {
+                    add[sl][rc[a] - 64 * I] = u[a];
+                    hit[sl][rc[a] - 64 * I] = 1;
+                }
             }
         }
         __syncthreads();
@@ -465,13 +472,12 @@ __global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__
         for (int K = 0; K < Kn; ++K) {
             if (lane == 0) {
                 long long spins = 0;
-                while (__hip_atomic_load(&yf[K], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                while (__hip_atomic_load(&yf[K], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                       spins < ND_SOLVE_SPIN_LIMIT) {
                     __builtin_amdgcn_s_sleep(1);
-                    if (++spins > ND_SOLVE_SPIN_LIMIT) {
-                        atomicOr(status, ST_TIMEOUT);
-                        break;
-                    }
+                    ++spins;
                 }
+                if (spins >= ND_SOLVE_SPIN_LIMIT) atomicOr(status, ST_TIMEOUT);
             }
             __syncthreads();
             T lv[64];
@@ -490,9 +496,12 @@ __global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__
             val = val - ((s0 + s1) + (s2 + s3));
             __syncthreads();
         }
-        if (I < nd.npt) {  // y_I = Dinv_I v_I, as nd_forward's four 16-term partials
-            yk[lane] = val;
-            __syncthreads();
+        // a pivot tile: y_I = Dinv_I v_I, as nd_forward's four 16-term partials
+        const bool pivot = I < nd.npt;
+        yk[lane] = val;
+        __syncthreads();
+        T out = val;
+        if (pivot) {
             const T* g = Dinv + nd.dinv_off + (int64_t)I * 4096 + lane;
             T part[4];
 #pragma unroll
@@ -508,14 +517,17 @@ __global__ __launch_bounds__(64) void nd_forward_tiles(const NdDev* __restrict__
                 }
                 part[wv] = y0 + y1;
             }
-            st_sc1(&v[r], (part[0] + part[1]) + (part[2] + part[3]));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (lane == 0) __hip_atomic_store(&yf[I], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            st_sc1(&v[r], val);
+            out = (part[0] + part[1]) + (part[2] + part[3]);
+        }
+        st_sc1(&v[r], out);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) {
+            if (pivot) __hip_atomic_store(&yf[I], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tk = atomicAdd(ticket, 1);
         }
         __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(tk);
     }
 }
 
@@ -900,7 +912,103 @@ struct NdCached {
     // every solve.
     std::mutex num_mu;
     DBuf fr, dv, fl;
+    std::atomic<size_t> kept_bytes{0};  // fr + dv + fl, written under num_mu
+    // drop the kept numeric storage unless a solve holds it
+    bool release_numeric() {
+        std::unique_lock<std::mutex> l(num_mu, std::try_to_lock);
+        if (!l.owns_lock()) return false;
+        fr.reset();
+        dv.reset();
+        fl.reset();
+        kept_bytes = 0;
+        return true;
+    }
 };
+
+// ---- the plan cache across handles ------------------------------------------
+// solve(a: Csr<f32>, b) takes `a` by value (src/lib.rs:11): a drop-in caller
+// builds a new Csr, hence a new handle, for every solve, and a plan kept only
+// on the handle is rebuilt every time (the host analysis is ~90 % of a cold
+// C5 solve). So plans are also kept in a library-wide cache keyed by the
+// pattern: (device, n, nnz, leaf) and a 128-bit hash of row_ptr and col
+// computed on the device; a hash hit is confirmed by comparing the pattern
+// with the entry's own copy of it (no false hit on a collision). Bounded:
+// at most BSM_ND_CACHE_ENTRIES entries (default 4, least recently used out)
+// and at most BSM_ND_CACHE_MB of kept numeric storage (default 32768) over
+// the entries no solve is using; bsm_nd_cache_clear drops them all.
+
+__device__ __forceinline__ uint64_t nd_mix64(uint64_t z) {  // SplitMix64's finaliser
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// two sums (mod 2^64) of per-element hashes of (position, value): order-free
+// integer sums, so the key does not depend on the grid
+__global__ __launch_bounds__(256) void nd_pattern_hash(const int64_t* __restrict__ rp, int64_t n1,
+                                                       const int32_t* __restrict__ col, int64_t nnz,
+                                                       unsigned long long* __restrict__ h) {
+    uint64_t s0 = 0, s1 = 0;
+    const int64_t total = n1 + nnz;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const uint64_t x = e < n1 ? (uint64_t)rp[e] : (uint64_t)(uint32_t)col[e - n1];
+        const uint64_t k = (uint64_t)e * 0x9e3779b97f4a7c15ull;
+        s0 += nd_mix64(x ^ k);
+        s1 += nd_mix64(x + k + 0x632be59bd9b4e019ull);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += (uint64_t)__shfl_xor((unsigned long long)s0, o);
+        s1 += (uint64_t)__shfl_xor((unsigned long long)s1, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&h[0], (unsigned long long)s0);
+        atomicAdd(&h[1], (unsigned long long)s1);
+    }
+}
+
+// *diff != 0 when the patterns differ anywhere
+__global__ __launch_bounds__(256) void nd_pattern_diff(const int64_t* __restrict__ rpa, const int64_t* __restrict__ rpb,
+                                                       int64_t n1, const int32_t* __restrict__ ca,
+                                                       const int32_t* __restrict__ cb, int64_t nnz,
+                                                       int* __restrict__ diff) {
+    bool d = false;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n1 + nnz; e += (int64_t)gridDim.x * 256)
+        d |= e < n1 ? rpa[e] != rpb[e] : ca[e - n1] != cb[e - n1];
+    if (__any(d) && (threadIdx.x & 63) == 0) atomicOr(diff, 1);
+}
+
+struct NdKey {
+    int device = 0;
+    int64_t n = 0, leaf = 0;
+    uint64_t nnz = 0, h0 = 0, h1 = 0;
+    bool operator==(const NdKey& o) const {
+        return device == o.device && n == o.n && leaf == o.leaf && nnz == o.nnz && h0 == o.h0 && h1 == o.h1;
+    }
+};
+
+struct NdCacheEntry {
+    NdKey key;
+    uint64_t tick = 0;
+    std::shared_ptr<DBuf> pattern;  // row_ptr (n + 1 int64), then col (nnz int32)
+    std::shared_ptr<NdCached> plan;
+};
+
+struct NdCache {
+    std::mutex mu;
+    std::vector<NdCacheEntry> entries;
+    uint64_t tick = 0, hits = 0, misses = 0;
+};
+
+NdCache& nd_cache() {  // never destroyed: no hipFree after the runtime's teardown at exit
+    static NdCache* c = new NdCache;
+    return *c;
+}
+
+size_t nd_cache_limit(const char* env, size_t dflt) {
+    const char* e = getenv(env);
+    return e ? (size_t)atoll(e) : dflt;
+}
 
 // The calling thread's page-locked staging buffer (grown on demand, kept for
 // the thread's later plans): the pattern's download and the plan's upload
@@ -1003,25 +1111,173 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     return BSM_OK;
 }
 
+size_t nd_pattern_rp_bytes(int64_t n) { return ((size_t)(n + 1) * sizeof(int64_t) + 255) / 256 * 256; }
+
+// the pattern's key (synchronous on s: a ~6M-element pass at C5, ~10 us)
+int nd_pattern_key(const bsm_csr* a, int64_t leaf, hipStream_t s, NdKey& key) {
+    const int64_t n = (int64_t)a->rows, total = n + 1 + (int64_t)a->nnz;
+    key.device = a->device;
+    key.n = n;
+    key.leaf = leaf;
+    key.nnz = a->nnz;
+    DBuf hb;
+    BSM_TRY(hb.alloc(16, s));
+    BSM_HIP_TRY(hipMemsetAsync(hb.p, 0, 16, s));
+    nd_pattern_hash<<<(unsigned)std::min<int64_t>((total + 255) / 256, 4096), 256, 0, s>>>(
+        a->row_ptr, n + 1, a->col, (int64_t)a->nnz, hb.as<unsigned long long>());
+    BSM_HIP_TRY(hipGetLastError());
+    uint64_t h[2] = {0, 0};
+    BSM_HIP_TRY(read_dev(h, hb.p, 16, s));
+    key.h0 = h[0];
+    key.h1 = h[1];
+    const char* hz = getenv("BSM_ND_HASH_ZERO");  // tests: every pattern of one (n, nnz) collides
+    if (hz && atoi(hz) == 1) key.h0 = key.h1 = 0;
+    return BSM_OK;
+}
+
+// Drop kept numeric storage, least recently used first, until the entries'
+// total is at most `budget` bytes; `keep` and storage a running solve holds
+// stay. The caller holds the cache's mutex.
+void nd_cache_trim_locked(NdCache& c, size_t budget, const NdCached* keep) {
+    std::vector<NdCacheEntry*> by_age;
+    size_t total = 0;
+    for (auto& e : c.entries) {
+        total += e.plan->kept_bytes;
+        by_age.push_back(&e);
+    }
+    std::sort(by_age.begin(), by_age.end(), [](auto* x, auto* y) { return x->tick < y->tick; });
+    for (NdCacheEntry* e : by_age) {
+        if (total <= budget) break;
+        if (e->plan.get() == keep) continue;
+        const size_t b = e->plan->kept_bytes;
+        if (b && e->plan->release_numeric()) total -= b;
+    }
+}
+
+void nd_cache_trim(size_t budget, const NdCached* keep) {
+    NdCache& c = nd_cache();
+    std::lock_guard<std::mutex> l(c.mu);
+    nd_cache_trim_locked(c, budget, keep);
+}
+
+// A cached plan for this pattern (confirmed against the entry's copy of the
+// pattern), or null
+int nd_cache_find(const bsm_csr* a, const NdKey& key, hipStream_t s, std::shared_ptr<NdCached>& out) {
+    out.reset();
+    NdCache& c = nd_cache();
+    std::shared_ptr<DBuf> pat;
+    std::shared_ptr<NdCached> plan;
+    {
+        std::lock_guard<std::mutex> l(c.mu);
+        for (auto& e : c.entries)
+            if (e.key == key) {
+                e.tick = ++c.tick;
+                pat = e.pattern;
+                plan = e.plan;
+                break;
+            }
+    }
+    if (plan) {
+        const int64_t n1 = key.n + 1, total = n1 + (int64_t)key.nnz;
+        const char* pb = pat->as<char>();
+        DBuf db;
+        BSM_TRY(db.alloc(4, s));
+        BSM_HIP_TRY(hipMemsetAsync(db.p, 0, 4, s));
+        nd_pattern_diff<<<(unsigned)std::min<int64_t>((total + 255) / 256, 4096), 256, 0, s>>>(
+            a->row_ptr, (const int64_t*)pb, n1, a->col, (const int32_t*)(pb + nd_pattern_rp_bytes(key.n)),
+            (int64_t)key.nnz, db.as<int>());
+        BSM_HIP_TRY(hipGetLastError());
+        int diff = 1;
+        BSM_HIP_TRY(read_dev(&diff, db.p, 4, s));
+        if (!diff) out = plan;
+    }
+    std::lock_guard<std::mutex> l(c.mu);
+    ++(out ? c.hits : c.misses);
+    return BSM_OK;
+}
+
+int nd_cache_insert(const bsm_csr* a, const NdKey& key, const std::shared_ptr<NdCached>& plan, hipStream_t s) {
+    auto pat = std::make_shared<DBuf>();
+    const size_t rpb = nd_pattern_rp_bytes(key.n);
+    BSM_TRY(pat->alloc(rpb + (size_t)key.nnz * sizeof(int32_t)));
+    BSM_HIP_TRY(hipMemcpyAsync(pat->p, a->row_ptr, (size_t)(key.n + 1) * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    if (key.nnz)
+        BSM_HIP_TRY(hipMemcpyAsync(pat->as<char>() + rpb, a->col, (size_t)key.nnz * sizeof(int32_t),
+                                   hipMemcpyDeviceToDevice, s));
+    BSM_HIP_TRY(hipStreamSynchronize(s));  // a lookup on another stream may compare against it next
+    NdCache& c = nd_cache();
+    std::lock_guard<std::mutex> l(c.mu);
+    c.entries.erase(std::remove_if(c.entries.begin(), c.entries.end(),
+                                   [&](const NdCacheEntry& e) { return e.key == key; }),
+                    c.entries.end());
+    NdCacheEntry e;
+    e.key = key;
+    e.tick = ++c.tick;
+    e.pattern = std::move(pat);
+    e.plan = plan;
+    c.entries.push_back(std::move(e));
+    const size_t cap = std::max<size_t>(1, nd_cache_limit("BSM_ND_CACHE_ENTRIES", 4));
+    while (c.entries.size() > cap) {
+        auto old = std::min_element(c.entries.begin(), c.entries.end(),
+                                    [](const NdCacheEntry& x, const NdCacheEntry& y) { return x.tick < y.tick; });
+        c.entries.erase(old);  // a handle still holding the plan keeps it alive
+    }
+    return BSM_OK;
+}
+
+// Numeric storage for a solve: on BSM_ERR_OOM, drop every other cached
+// plan's kept storage and try once more
+int nd_alloc_numeric(DBuf& b, size_t bytes, const NdCached* keep) {
+    if (b.bytes == bytes) return BSM_OK;
+    int rc = b.alloc(bytes);
+    if (rc == BSM_ERR_OOM) {
+        nd_cache_trim(0, keep);
+        rc = b.alloc(bytes);
+    }
+    return rc;
+}
+
+// Waits for the stream when an error return leaves kernels queued that
+// write the kept numeric storage, so no other solve takes that storage
+// (num_mu is released after this guard runs) while they still run.
+struct NdDrainOnError {
+    hipStream_t s;
+    bool armed = false;
+    ~NdDrainOnError() {
+        if (armed) (void)hipStreamSynchronize(s);
+    }
+};
+
 template <typename T>
 int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* x_dev, hipStream_t s) {
     stage_reset(s);
     const int64_t N = (int64_t)n;
     const char* le = getenv("BSM_ND_LEAF");
     const char* ce = getenv("BSM_ND_CACHE");
+    const char* she = getenv("BSM_ND_SHARED");
     const int64_t leaf = le ? atoll(le) : 192;  // C5 leaf sweep: 128 / 192 / 256 / 320 -> 11.9 / 11.4 / 12.3 / 12.5 ms
     const bool cache = !(ce && atoi(ce) == 0);
+    const bool shared = cache && !(she && atoi(she) == 0);  // the cache across handles (BSM_ND_SHARED=0: off)
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);
         auto c = std::static_pointer_cast<NdCached>(a->nd_plan);
         if (c && c->leaf == leaf) pc = c;
     }
+    NdKey key;
     if (pc) {
         stage_mark("nd_plan_cached", s);
     } else {
-        pc = std::make_shared<NdCached>();
-        BSM_TRY(nd_build_plan(a, leaf, s, *pc));
+        if (shared) {
+            BSM_TRY(nd_pattern_key(a, leaf, s, key));
+            BSM_TRY(nd_cache_find(a, key, s, pc));
+            stage_mark(pc ? "nd_plan_shared" : "nd_pattern_key", s);
+        }
+        if (!pc) {
+            pc = std::make_shared<NdCached>();
+            BSM_TRY(nd_build_plan(a, leaf, s, *pc));
+            if (shared) BSM_TRY(nd_cache_insert(a, key, pc, s));
+        }
         if (cache) {
             std::lock_guard<std::mutex> lk(a->plan_mu);
             a->nd_plan = pc;
@@ -1060,9 +1316,32 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     DBuf& fl = keep ? C.fl : own_fl;
     const size_t fr_b = (size_t)C.f_elems * sizeof(T), dv_b = (size_t)std::max<int64_t>(C.dinv_elems, 1) * sizeof(T);
     const size_t nfl = (size_t)C.n_flags + (size_t)C.n_levels + 2;
-    if (fr.bytes != fr_b) BSM_TRY(fr.alloc(fr_b));  // a plan serves one dtype per handle; sizes match after
-    if (dv.bytes != dv_b) BSM_TRY(dv.alloc(dv_b));
-    if (fl.bytes != nfl * sizeof(int)) BSM_TRY(fl.alloc(nfl * sizeof(int)));
+    // a plan serves one dtype per handle; sizes match after the first solve
+    BSM_TRY(nd_alloc_numeric(fr, fr_b, &C));
+    BSM_TRY(nd_alloc_numeric(dv, dv_b, &C));
+    BSM_TRY(nd_alloc_numeric(fl, nfl * sizeof(int), &C));
+    if (keep) C.kept_bytes = fr.bytes + dv.bytes + fl.bytes;
+    // everything that can fail before the first launch: the occupancy
+    // queries and the solves' temporaries (an error return after
+    // the launches would release num_mu under running kernels)
+    int dev = 0, cus = 0, per_cu = 0, fper = 0, bper = 0;
+    BSM_HIP_TRY(hipGetDevice(&dev));
+    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nd_factor<T>, 256, 0));
+    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "nd_factor does not fit a CU");
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&fper, nd_forward_tiles<T>, 64, 0));
+    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bper, nd_backward_tiles<T>, 256, 0));
+    BSM_REQUIRE(fper >= 1 && bper >= 1, BSM_ERR_UNSUPPORTED, "nd solve kernels do not fit a CU");
+    const int64_t n_pf = (C.dinv_elems / 4096) * (int64_t)k;  // flags per pass: one per node, column, pivot tile
+    const size_t n_tf = 2 * (size_t)n_pf + 2 * (size_t)C.n_levels;  // forward flags, backward flags, tickets
+    DBuf bpb, vb, tfl;  // from the thread's cache of temporaries (no hipFree per solve)
+    if (k > 0) {
+        BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T), s));
+        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T), s));
+        BSM_TRY(tfl.alloc(n_tf * sizeof(int), s));
+    }
+    NdDrainOnError drain{s};  // destroyed before num_lock is released
+    drain.armed = true;
     BSM_HIP_TRY(hipMemsetAsync(fl.p, 0, nfl * sizeof(int), s));
     int* d_flags = fl.as<int>();
     int* d_tickets = d_flags + C.n_flags;
@@ -1078,11 +1357,6 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     nd_pad_pivots<T><<<(unsigned)C.nn, 64, 0, s>>>(d_nodes, F);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("nd_assemble", s);
-    int dev = 0, cus = 0, per_cu = 0;
-    BSM_HIP_TRY(hipGetDevice(&dev));
-    BSM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nd_factor<T>, 256, 0));
-    BSM_REQUIRE(per_cu >= 1, BSM_ERR_UNSUPPORTED, "nd_factor does not fit a CU");
     // BSM_ND_PAD_SKIP=0: diagonal tiles factor their padding panels too (A/B; same bits)
     const char* pse = getenv("BSM_ND_PAD_SKIP");
     const int pad_skip = !(pse && atoi(pse) == 0);
@@ -1110,9 +1384,6 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     }
     stage_mark("nd_factor", s);
     if (k > 0) {
-        DBuf bpb, vb;  // from the thread's cache of temporaries (no hipFree per solve)
-        BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T), s));
-        BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T), s));
         nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
                                                        bpb.as<T>());
         BSM_HIP_TRY(hipGetLastError());
@@ -1125,19 +1396,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         const char* bte = getenv("BSM_ND_BWD_TILES");
         const int fwd_mode = fte ? atoi(fte) : 2, bwd_mode = bte ? atoi(bte) : 2;
         auto by_tiles = [&](int mode, int64_t pairs) { return mode == 1 || (mode == 2 && pairs < cus); };
-        const int64_t n_pf = (C.dinv_elems / 4096) * (int64_t)k;  // flags per pass: one per node, column, pivot tile
-        DBuf tfl;
-        const size_t n_tf = 2 * (size_t)n_pf + 2 * (size_t)C.n_levels;  // forward flags, backward flags, tickets
-        BSM_TRY(tfl.alloc(n_tf * sizeof(int), s));
         BSM_HIP_TRY(hipMemsetAsync(tfl.p, 0, n_tf * sizeof(int), s));
         int* const d_yf = tfl.as<int>();
         int* const d_xf = d_yf + n_pf;
         int* const d_ftk = d_xf + n_pf;
         int* const d_btk = d_ftk + C.n_levels;
-        int fper = 0, bper = 0;
-        BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&fper, nd_forward_tiles<T>, 64, 0));
-        BSM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bper, nd_backward_tiles<T>, 256, 0));
-        BSM_REQUIRE(fper >= 1 && bper >= 1, BSM_ERR_UNSUPPORTED, "nd solve kernels do not fit a CU");
         const int64_t fwd_grid = (int64_t)cus * fper, bwd_grid = (int64_t)cus * bper;
         for (int32_t lv = 0; lv < C.n_levels; ++lv) {
             const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
@@ -1179,10 +1442,15 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     int h = 0;
     BSM_HIP_TRY(read_dev(&h, d_status, sizeof(int), s));
     BSM_HIP_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
     stage_mark("nd_copy_out", s);
     BSM_REQUIRE(!(h & ST_TIMEOUT), BSM_ERR_HIP, "nd factor: tile hand-off timed out");
     BSM_REQUIRE(!(h & ST_NOT_PD), BSM_ERR_UNSUPPORTED,
                 "cholesky: matrix is not positive definite (a pivot is <= 0 or not finite)");
+    if (keep && shared) {  // the cached plans' kept storage within its budget (this plan's stays)
+        num_lock.unlock();
+        nd_cache_trim(nd_cache_limit("BSM_ND_CACHE_MB", 32768) << 20, &C);
+    }
     return BSM_OK;
 }
 
@@ -1202,3 +1470,26 @@ int solve_dispatch_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_de
 }
 
 }  // namespace bsm
+
+// ---- C-ABI: the nd plan cache across handles ----
+extern "C" int bsm_nd_cache_clear(void) {
+    bsm::NdCache& c = bsm::nd_cache();
+    std::vector<bsm::NdCacheEntry> gone;
+    {
+        std::lock_guard<std::mutex> l(c.mu);
+        gone.swap(c.entries);
+    }
+    return BSM_OK;  // `gone` frees outside the lock (a handle still holding a plan keeps it)
+}
+
+extern "C" int bsm_nd_cache_info(uint64_t* entries, uint64_t* kept_bytes, uint64_t* hits, uint64_t* misses) {
+    bsm::NdCache& c = bsm::nd_cache();
+    std::lock_guard<std::mutex> l(c.mu);
+    uint64_t kb = 0;
+    for (const auto& e : c.entries) kb += e.plan->kept_bytes;
+    if (entries) *entries = c.entries.size();
+    if (kept_bytes) *kept_bytes = kb;
+    if (hits) *hits = c.hits;
+    if (misses) *misses = c.misses;
+    return BSM_OK;
+}

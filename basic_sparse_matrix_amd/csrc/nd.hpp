@@ -26,7 +26,7 @@ struct NdPlan {
     std::vector<int64_t> pinv;    // pinv[old] = new
     std::vector<NdNode> nodes;    // children before parents (post-order), roots last
     int32_t n_levels = 0;
-    double ms_graph = 0, ms_order = 0, ms_symbolic = 0;
+    double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_bisect = 0;  // ms_order includes ms_bisect
 };
 
 // A's pattern (row_ptr: n + 1 entries, col: row_ptr[n]); the matrix is the

@@ -182,9 +182,29 @@ int bsm_solve_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* cons
  * f64 tolerance (1e-6 relative, BASELINE.json north_star). A is its lower
  * triangle (j <= i) mirrored, as cholesky_decomp reads it; rows must have
  * strictly increasing columns, and a pivot <= 0 (not SPD) -> BSM_ERR_UNSUPPORTED.
- * Same arguments and panics as bsm_solve. This build's addition. */
+ * Same arguments and panics as bsm_solve. This build's addition.
+ * Plans: the analysis of a pattern (ordering, tree, device index arrays) is
+ * kept on the handle AND in a library-wide cache keyed by the pattern (a
+ * 128-bit device hash of row_ptr and col, each hit confirmed by comparing
+ * the pattern itself), because solve takes `a` by value (lib.rs:11) and a
+ * drop-in caller uploads a new handle for every call: a new handle with a
+ * pattern seen before skips the analysis. Retention: after a solve the plan
+ * keeps its numeric storage (the fronts, inverse diagonal tiles and flags:
+ * ~5.6 GB at C5 in f64) for the next solve of that pattern. The cache holds
+ * at most BSM_ND_CACHE_ENTRIES patterns (default 4, least recently used
+ * out) and at most BSM_ND_CACHE_MB of kept storage (default 32768) across
+ * them; an allocation that fails for lack of memory first drops the other
+ * plans' kept storage and retries. bsm_nd_cache_clear releases every cached
+ * plan not also held by a live handle (bsm_csr_free releases the handle's).
+ * Env BSM_ND_CACHE=0: no plan kept anywhere; BSM_ND_SHARED=0: per handle only;
+ * BSM_ND_KEEP=0: numeric storage freed after every solve. */
 int bsm_solve_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
                  void* const* x_cols);
+/* The cross-handle plan cache of bsm_solve_nd: drop every entry, or read its
+ * state (entries, kept numeric bytes, lookups that hit / missed since load).
+ * Any pointer may be NULL. This build's addition. */
+int bsm_nd_cache_clear(void);
+int bsm_nd_cache_info(uint64_t* entries, uint64_t* kept_bytes, uint64_t* hits, uint64_t* misses);
 /* The analysis of bsm_solve_nd alone, on a host pattern (row_ptr n+1, col_idx
  * row_ptr[n]); no device use (tests, diagnostics). Writes perm (n entries,
  * perm[new] = old) when non-null; *n_nodes and *st_len always; when cap >=

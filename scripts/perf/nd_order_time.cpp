@@ -27,6 +27,11 @@ int main(int argc, char** argv) {
         for (auto& x : P.nodes) { int64_t np = x.end - x.start, npp = (np + 63) / 64 * 64, f = npp + x.st.size(), fp = (f + 63) / 64 * 64;
             mem += 8.0 * fp * fp; mx = std::max(mx, fp);
             fl += (double)np * np * np / 3 + (double)np * np * x.st.size() + (double)np * x.st.size() * x.st.size(); }
-        printf("total %.1f ms: graph %.1f order %.1f symbolic %.1f nodes %zu levels %d | fronts %.2f GB max %lld, true flops %.2f GF\n", ms, P.ms_graph, P.ms_order, P.ms_symbolic, P.nodes.size(), P.n_levels, mem / 1e9, (long long)mx, fl / 1e9);
+        uint64_t h = 1469598103934665603ull;  // FNV-1a over perm and every node's (start, end, parent, st)
+        auto mix = [&](int64_t x) { h = (h ^ (uint64_t)x) * 1099511628211ull; };
+        for (int64_t v : P.perm) mix(v);
+        for (auto& x : P.nodes) { mix(x.start); mix(x.end); mix(x.parent); for (int64_t q : x.st) mix(q); }
+        printf("plan %016llx | ", (unsigned long long)h);
+        printf("total %.1f ms: graph %.1f order %.1f (bisect %.1f) symbolic %.1f nodes %zu levels %d | fronts %.2f GB max %lld, true flops %.2f GF\n", ms, P.ms_graph, P.ms_order, P.ms_bisect, P.ms_symbolic, P.nodes.size(), P.n_levels, mem / 1e9, (long long)mx, fl / 1e9);
     }
 }

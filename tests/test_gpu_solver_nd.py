@@ -164,18 +164,118 @@ def test_nd_wide_irregular_graph_residual():
 
 
 @pytest.mark.parametrize("g", [64, 250])
-def test_nd_deterministic(orc, g):
-    """Fixed tile order, fixed child order in the extend-add and the solves:
-    two runs give the same bits."""
+def test_nd_deterministic(orc, monkeypatch, g):
+    """Fixed tile order, fixed child order in the extend-add and the solves,
+    and an analysis whose result does not depend on its threads' timing: two
+    fresh handles with no plan cache anywhere (BSM_ND_CACHE=0: the bisection,
+    symbolic pass and layout run again for each) give the same bits, and so
+    does a third solve through the cached plan."""
     n = g * g
     rp, ci, v = orc.poisson2d(g)
-    A = Csr.from_csr_arrays((n, n), rp, ci, v)
     b = orc.gen_x_cols(1007, n, 1)
-    x0 = np.asarray(solve(A, Dense.from_columns(b), order="nd").get_col(0)).copy()
-    x1 = np.asarray(solve(A, Dense.from_columns(b), order="nd").get_col(0)).copy()
+    monkeypatch.setenv("BSM_ND_CACHE", "0")
+    x0 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0)).copy()
+    x1 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0)).copy()
     assert np.array_equal(x0.view(np.uint8), x1.view(np.uint8))
+    monkeypatch.delenv("BSM_ND_CACHE")
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    solve(A, Dense.from_columns(b), order="nd")
+    x2 = np.asarray(solve(A, Dense.from_columns(b), order="nd").get_col(0)).copy()
+    assert np.array_equal(x0.view(np.uint8), x2.view(np.uint8))
     ex = orc.solve(n, rp, ci, v, b, band=True)[0]
     assert rel_err(x0, ex) < 1e-10
+
+
+def banded_spd(g, offsets):
+    """n = g^2, diagonal 5, -1 on the given off-diagonals (both sides):
+    strictly diagonally dominant, so SPD; sorted columns."""
+    import scipy.sparse as sp
+
+    n = g * g
+    diags = [np.full(n, 5.0)] + [np.full(n - o, -1.0) for o in offsets for _ in (0, 1)]
+    offs = [0] + [s * o for o in offsets for s in (1, -1)]
+    m = sp.diags(diags, offs, shape=(n, n), format="csr")
+    m.sort_indices()
+    return m.indptr.astype(np.uint64), m.indices.astype(np.uint64), m.data.astype(np.float64)
+
+
+def test_nd_plan_shared_across_handles(orc, monkeypatch):
+    """solve takes `a` by value (lib.rs:11): a drop-in caller makes a new
+    handle per call. A new handle with a pattern solved before reuses the
+    library-wide cached plan (a hit, no analysis) and solves ITS values:
+    within the tolerance of the oracle and bit-equal to a solve that builds
+    its own plan (BSM_ND_SHARED=0)."""
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.nd_cache_clear()
+    g = 40
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    b = orc.gen_x_cols(1014, n, 2)
+    i0 = _lib.nd_cache_info()
+    solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
+    i1 = _lib.nd_cache_info()
+    assert i1["entries"] == 1 and i1["misses"] == i0["misses"] + 1 and i1["hits"] == i0["hits"]
+    v2 = 1.5 * v  # same pattern, other values
+    x = solve(Csr.from_csr_arrays((n, n), rp, ci, v2), Dense.from_columns(b), order="nd")
+    i2 = _lib.nd_cache_info()
+    assert i2["hits"] == i1["hits"] + 1 and i2["entries"] == 1 and i2["kept_bytes"] > 0
+    ex = orc.solve(n, rp, ci, v2, b, band=True)
+    for j in range(2):
+        assert rel_err(x.get_col(j), ex[j]) < 1e-10, j
+    monkeypatch.setenv("BSM_ND_SHARED", "0")
+    x_own = solve(Csr.from_csr_arrays((n, n), rp, ci, v2), Dense.from_columns(b), order="nd")
+    assert _lib.nd_cache_info()["hits"] == i2["hits"]
+    for j in range(2):
+        assert np.array_equal(np.asarray(x.get_col(j)).view(np.uint8), np.asarray(x_own.get_col(j)).view(np.uint8))
+
+
+def test_nd_plan_cache_pattern_miss_confirmed(monkeypatch):
+    """Two patterns with the same n and nnz whose keys are forced to collide
+    (BSM_ND_HASH_ZERO=1): the comparison of the patterns themselves rejects
+    the cached plan (a miss, a new analysis), and both solve right."""
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.nd_cache_clear()
+    monkeypatch.setenv("BSM_ND_HASH_ZERO", "1")
+    g = 24
+    n = g * g
+    rp1, ci1, v1 = banded_spd(g, [1, g])
+    rp2, ci2, v2 = banded_spd(g, [2, g - 1])
+    assert ci1.size == ci2.size and not np.array_equal(ci1, ci2)
+    rng = np.random.default_rng(3)
+    b = rng.uniform(-1, 1, n)
+    i0 = _lib.nd_cache_info()
+    for rp, ci, v in ((rp1, ci1, v1), (rp2, ci2, v2), (rp1, ci1, v1)):
+        x = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns([b]), order="nd").get_col(0)
+        a = np.zeros((n, n))
+        a[np.repeat(np.arange(n), np.diff(rp.astype(np.int64))), ci.astype(np.int64)] = v
+        assert rel_err(x, np.linalg.solve(a, b)) < 1e-12
+    i1 = _lib.nd_cache_info()
+    # pattern 1 misses, pattern 2 collides and is rejected (its plan replaces
+    # pattern 1's under the shared key), pattern 1 again is rejected likewise
+    assert i1["misses"] == i0["misses"] + 3 and i1["hits"] == i0["hits"]
+
+
+def test_nd_plan_cache_bounded(orc, monkeypatch):
+    """At most BSM_ND_CACHE_ENTRIES patterns; with BSM_ND_CACHE_MB=0 only the
+    plan just used keeps its numeric storage; bsm_nd_cache_clear empties it."""
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.nd_cache_clear()
+    monkeypatch.setenv("BSM_ND_CACHE_ENTRIES", "2")
+    monkeypatch.setenv("BSM_ND_CACHE_MB", "0")
+    kept = []
+    for g in (20, 21, 22):
+        n = g * g
+        rp, ci, v = orc.poisson2d(g)
+        solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(orc.gen_x_cols(1015, n, 1)), order="nd")
+        info = _lib.nd_cache_info()
+        kept.append(info["kept_bytes"])
+        assert info["entries"] == min(len(kept), 2)
+    assert 0 < kept[-1] < kept[0] + kept[1] + kept[2]
+    _lib.nd_cache_clear()
+    assert _lib.nd_cache_info()["entries"] == 0
 
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES"])
