@@ -99,7 +99,7 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
     for (int d = nd.np + (int)threadIdx.x; d < nd.np_pad; d += 64) F[nd.foff + (int64_t)d * nd.ld + d] = (T)1;
 }
 
-// Partial Cholesky of the fronts of one level. tiles[t] = (node, I, K):
+// Partial Cholesky of the fronts of one level. tiles[t] = (node, I, K, 0):
 // column-major order across the level's fronts (K; the diagonal tiles of all
 // fronts, then the tiles below them), so a tile only waits on tiles of
 // earlier tickets. Tile (I, K), I >= K:
@@ -107,6 +107,12 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 //     K < npt, I == K: L_KK = chol(S), Dinv_K = L_KK^-1   (flag)
 //     K < npt, I >  K: L_IK = S L_KK^-T                    (flag)
 //     K >= npt       : U_IK = S (the update block, for nd_extend)
+// tiles[t] = (node, 0, 0, 1): the whole front of a small node (a few tiles:
+// most of the leaf level) on this workgroup, its tiles in column order one
+// after the other. Its flags are its own (a tile's waits find them set), so
+// it waits on nobody: these tasks follow the tiled fronts' tickets and fill
+// the CUs while those fronts' chains run, without a ticket and a flag
+// hand-off through L2 per tile.
 template <typename T>
 __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
                                                  int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
@@ -117,30 +123,34 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
     __shared__ T rd[64];
     __shared__ T Di[4 * 256];
     __shared__ T Tb[3 * 256];
-    __shared__ int64_t tk;
+    __shared__ int tk;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int rb = 16 * w + (lane >> 4), cm = lane & 15;
     lds_t<T>* const PTl = (lds_t<T>*)&PT[0][0];
     lds_t<T>* const QTl = (lds_t<T>*)&QT[0][0];
+    // the poll has no break (the structurizer's hazard in nd_backward_tiles)
     auto wait_flag = [&](const int* f) {
         long long spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spins <= SPIN_LIMIT) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > SPIN_LIMIT) {
-                if (lane == 0) atomicOr(status, ST_TIMEOUT);
-                return;
-            }
+            ++spins;
         }
+        if (spins > SPIN_LIMIT && lane == 0) atomicOr(status, ST_TIMEOUT);
     };
-    for (;;) {
-        if (tid == 0) tk = atomicAdd(ticket, 1);
-        __syncthreads();
-        const int64_t t = tk;
-        if (t >= ntiles) break;
-        const int4 tl = tiles[t];
-        const NdDev& nd = nodes[tl.x];
-        const int I = tl.y, K = tl.z, npt = nd.npt;
+    // the ticket at the END of each task and counted inner loops (the
+    // control-flow shape of nd_backward_tiles)
+    if (tid == 0) tk = atomicAdd(ticket, 1);
+    __syncthreads();
+    int64_t t = __builtin_amdgcn_readfirstlane(tk);
+    while (t < ntiles) {
+      const int4 tl = tiles[t];
+      const NdDev& nd = nodes[tl.x];
+      const bool whole = tl.w == 1;
+      const int npt = nd.npt, ntf = nd.nt;
+      const int cnt = whole ? ntf * (ntf + 1) / 2 : 1;
+      int I = whole ? 0 : tl.y, K = whole ? 0 : tl.z;
+      for (int jt = 0; jt < cnt; ++jt) {
         const int64_t ld = nd.ld;
         T* const Fn = F + nd.foff;
         int* const fl = flags + nd.flag_off;
@@ -238,6 +248,15 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (K < npt && tid == 0) __hip_atomic_store(&fl[I * npt + K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (++I == ntf) {  // a whole front: the next tile in column order
+            ++K;
+            I = K;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) tk = atomicAdd(ticket, 1);
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(tk);
     }
 }
 
@@ -743,7 +762,8 @@ inline unsigned nd_blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b)
 struct NdLayout {
     std::vector<NdDev> dev;
     std::vector<int32_t> st, ri, pinv, owner, lvl_nodes;
-    std::vector<int4> tiles;
+    std::vector<int4> tiles;   // nd_factor's tasks: tiles of the tiled fronts, then the small fronts whole
+    std::vector<int4> ztiles;  // every front's lower tiles (nd_zero_tiles)
     std::vector<int2> ext;
     std::vector<int64_t> tiles_off, lvl_off, ext_off;  // per level (ext: per level and slot)
     std::vector<int4> ext2;                             // nd_extend2's tasks (both slots)
@@ -755,7 +775,9 @@ struct NdLayout {
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
 };
 
-void nd_layout(const NdPlan& P, NdLayout& L) {
+// small_nt: fronts of at most this many tile rows are one whole-front task
+// of nd_factor (0: every front by tiles)
+void nd_layout(const NdPlan& P, int32_t small_nt, NdLayout& L) {
     const int32_t nn = (int32_t)P.nodes.size();
     L.dev.resize((size_t)nn);
     int64_t st_total = 0;
@@ -819,17 +841,26 @@ void nd_layout(const NdPlan& P, NdLayout& L) {
         L.tiles_off.push_back((int64_t)L.tiles.size());
         int32_t kmax = 0;
         for (int32_t i : lv) kmax = std::max(kmax, L.dev[(size_t)i].nt);
-        // column K of every front: the diagonal tiles first, then the tiles
-        // below (which wait for their diagonal tile's inverse), so the
-        // waiting tiles' diagonals are well under way when they are taken
+        // every front's lower tiles (nd_zero_tiles)
+        for (int32_t i : lv)
+            for (int32_t K = 0; K < L.dev[(size_t)i].nt; ++K)
+                for (int32_t I = K; I < L.dev[(size_t)i].nt; ++I) L.ztiles.push_back(make_int4(i, I, K, 0));
+        // tiled fronts, column K of every front: the diagonal tiles first,
+        // then the tiles below (which wait for their diagonal tile's
+        // inverse), so the waiting tiles' diagonals are well under way when
+        // they are taken; then the small fronts, one task each
+        auto small = [&](int32_t i) { return L.dev[(size_t)i].nt <= small_nt; };
         for (int32_t K = 0; K < kmax; ++K) {
             for (int32_t i : lv)
-                if (K < L.dev[(size_t)i].nt) L.tiles.push_back(make_int4(i, K, K, 0));
+                if (!small(i) && K < L.dev[(size_t)i].nt) L.tiles.push_back(make_int4(i, K, K, 0));
             for (int32_t i : lv) {
                 const NdDev& d = L.dev[(size_t)i];
+                if (small(i)) continue;
                 for (int32_t I = K + 1; I < d.nt; ++I) L.tiles.push_back(make_int4(i, I, K, 0));
             }
         }
+        for (int32_t i : lv)
+            if (small(i)) L.tiles.push_back(make_int4(i, 0, 0, 1));
         for (int s = 0; s < 2; ++s) {
             L.ext_off.push_back((int64_t)L.ext.size());
             for (int32_t i : lv) {
@@ -900,8 +931,9 @@ struct NdCached {
     std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off, ftask_off, btask_off;
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
-           o_ftask = 0, o_btask = 0, o_perm = 0;
-    size_t n_tiles = 0, n_ext = 0;
+           o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0;
+    size_t n_tiles = 0, n_ztiles = 0, n_ext = 0;
+    int32_t small_nt = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
     // The numeric storage (fronts, inverse diagonal tiles, flags) stays with
@@ -980,10 +1012,12 @@ __global__ __launch_bounds__(256) void nd_pattern_diff(const int64_t* __restrict
 
 struct NdKey {
     int device = 0;
+    int32_t small_nt = 0;
     int64_t n = 0, leaf = 0;
     uint64_t nnz = 0, h0 = 0, h1 = 0;
     bool operator==(const NdKey& o) const {
-        return device == o.device && n == o.n && leaf == o.leaf && nnz == o.nnz && h0 == o.h0 && h1 == o.h1;
+        return device == o.device && small_nt == o.small_nt && n == o.n && leaf == o.leaf && nnz == o.nnz &&
+               h0 == o.h0 && h1 == o.h1;
     }
 };
 
@@ -1028,7 +1062,7 @@ int pinned_staging(size_t bytes, char** out) {
     return BSM_OK;
 }
 
-int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
+int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t s, NdCached& C) {
     const int64_t N = (int64_t)a->rows;
     // A's pattern to the host for the analysis
     char* stg = nullptr;
@@ -1049,7 +1083,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
                 "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
     const auto tl0 = host_now();
     NdLayout L;
-    nd_layout(P, L);
+    C.small_nt = small_nt;
+    nd_layout(P, small_nt, L);
     C.ms_layout = ms_since(tl0);
     C.leaf = leaf;
     C.nn = (int32_t)L.dev.size();
@@ -1065,6 +1100,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.n_flags = L.n_flags;
     C.vtot = L.vtot;
     C.n_tiles = L.tiles.size();
+    C.n_ztiles = L.ztiles.size();
     C.n_ext = L.ext.size();
     C.ms_graph = P.ms_graph;
     C.ms_order = P.ms_order;
@@ -1084,7 +1120,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     C.o_ftask = C.o_ext2 + al(L.ext2.size() * sizeof(int4));
     C.o_btask = C.o_ftask + al(L.ftasks.size() * sizeof(int2));
     C.o_perm = C.o_btask + al(L.btasks.size() * sizeof(int2));
-    const size_t total = C.o_perm + al((size_t)N * 8);
+    C.o_ztiles = C.o_perm + al((size_t)N * 8);
+    const size_t total = C.o_ztiles + al(L.ztiles.size() * sizeof(int4));
     const auto tp0 = host_now();
     char* hp = nullptr;
     BSM_TRY(pinned_staging(total, &hp));  // the pattern is no longer needed
@@ -1103,6 +1140,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
     put(C.o_ftask, L.ftasks.data(), L.ftasks.size() * sizeof(int2));
     put(C.o_btask, L.btasks.data(), L.btasks.size() * sizeof(int2));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
+    put(C.o_ztiles, L.ztiles.data(), L.ztiles.size() * sizeof(int4));
     C.ms_pack = ms_since(tp0);
     BSM_TRY(C.plan.alloc(total));
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
@@ -1114,9 +1152,10 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, hipStream_t s, NdCached& C) {
 size_t nd_pattern_rp_bytes(int64_t n) { return ((size_t)(n + 1) * sizeof(int64_t) + 255) / 256 * 256; }
 
 // the pattern's key (synchronous on s: a ~6M-element pass at C5, ~10 us)
-int nd_pattern_key(const bsm_csr* a, int64_t leaf, hipStream_t s, NdKey& key) {
+int nd_pattern_key(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t s, NdKey& key) {
     const int64_t n = (int64_t)a->rows, total = n + 1 + (int64_t)a->nnz;
     key.device = a->device;
+    key.small_nt = small_nt;
     key.n = n;
     key.leaf = leaf;
     key.nnz = a->nnz;
@@ -1258,24 +1297,28 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int64_t leaf = le ? atoll(le) : 192;  // C5 leaf sweep: 128 / 192 / 256 / 320 -> 11.9 / 11.4 / 12.3 / 12.5 ms
     const bool cache = !(ce && atoi(ce) == 0);
     const bool shared = cache && !(she && atoi(she) == 0);  // the cache across handles (BSM_ND_SHARED=0: off)
+    // fronts of at most this many tile rows factor as one task each (C5: most
+    // fronts of levels 0-4 have 2-4); BSM_ND_FRONT_NT=0: every front by tiles
+    const char* fne = getenv("BSM_ND_FRONT_NT");
+    const int32_t small_nt = fne ? atoi(fne) : 4;
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);
         auto c = std::static_pointer_cast<NdCached>(a->nd_plan);
-        if (c && c->leaf == leaf) pc = c;
+        if (c && c->leaf == leaf && c->small_nt == small_nt) pc = c;
     }
     NdKey key;
     if (pc) {
         stage_mark("nd_plan_cached", s);
     } else {
         if (shared) {
-            BSM_TRY(nd_pattern_key(a, leaf, s, key));
+            BSM_TRY(nd_pattern_key(a, leaf, small_nt, s, key));
             BSM_TRY(nd_cache_find(a, key, s, pc));
             stage_mark(pc ? "nd_plan_shared" : "nd_pattern_key", s);
         }
         if (!pc) {
             pc = std::make_shared<NdCached>();
-            BSM_TRY(nd_build_plan(a, leaf, s, *pc));
+            BSM_TRY(nd_build_plan(a, leaf, small_nt, s, *pc));
             if (shared) BSM_TRY(nd_cache_insert(a, key, pc, s));
         }
         if (cache) {
@@ -1298,6 +1341,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int32_t* d_owner = (const int32_t*)(pb + C.o_owner);
     const int32_t* d_lvl = (const int32_t*)(pb + C.o_lvl);
     const int4* d_tiles = (const int4*)(pb + C.o_tiles);
+    const int4* d_ztiles = (const int4*)(pb + C.o_ztiles);
     const int2* d_ext = (const int2*)(pb + C.o_ext);
     const int4* d_ext2 = (const int4*)(pb + C.o_ext2);
     const int2* d_ftask = (const int2*)(pb + C.o_ftask);
@@ -1347,8 +1391,8 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     int* d_tickets = d_flags + C.n_flags;
     int* d_status = d_tickets + C.n_levels;
     T* F = fr.as<T>();
-    if (C.n_tiles) {
-        nd_zero_tiles<T><<<(unsigned)C.n_tiles, 256, 0, s>>>(d_nodes, d_tiles, F);
+    if (C.n_ztiles) {
+        nd_zero_tiles<T><<<(unsigned)C.n_ztiles, 256, 0, s>>>(d_nodes, d_ztiles, F);
         BSM_HIP_TRY(hipGetLastError());
     }
     nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals), d_pinv,

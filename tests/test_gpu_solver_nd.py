@@ -278,7 +278,8 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
     assert _lib.nd_cache_info()["entries"] == 0
 
 
-@pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES"])
+@pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
+                                    "BSM_ND_FRONT_NT"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -297,7 +298,10 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
     * BSM_ND_BWD_TILES: the backward solve by pivot tiles (one workgroup per
       node, pivot tile and column; the front rows' products first, then each
       pivot tile's as its x arrives) instead of one workgroup per node and
-      column, which sums its rows in that same tile order.
+      column, which sums its rows in that same tile order;
+    * BSM_ND_FRONT_NT: fronts of at most 4 tile rows factored whole by one
+      workgroup, their tiles in column order, instead of one ticketed
+      workgroup per tile: every tile the same operations in the same order.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
