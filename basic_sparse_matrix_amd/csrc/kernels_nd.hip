@@ -775,9 +775,13 @@ struct NdLayout {
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
 };
 
-// small_nt: fronts of at most this many tile rows are one whole-front task
-// of nd_factor (0: every front by tiles)
-void nd_layout(const NdPlan& P, int32_t small_nt, NdLayout& L) {
+// lay: the layout's options. Bits 0-15: fronts of at most this many tile
+// rows are one whole-front task of nd_factor (0: every front by tiles); bit
+// 16: the per-slot extend lists too (BSM_ND_EXT_MERGE=0's A/B path; ~1M
+// entries at C5 that the default merged launches never read)
+void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
+    const int32_t small_nt = lay & 0xffff;
+    const bool per_slot = (lay >> 16) & 1;
     const int32_t nn = (int32_t)P.nodes.size();
     L.dev.resize((size_t)nn);
     int64_t st_total = 0;
@@ -808,33 +812,62 @@ void nd_layout(const NdPlan& P, int32_t small_nt, NdLayout& L) {
     }
     L.st.resize((size_t)st_total);
     L.ri.resize((size_t)st_total);
-    for (int32_t i = 0; i < nn; ++i) {
-        const NdNode& x = P.nodes[(size_t)i];
-        const NdDev& d = L.dev[(size_t)i];
-        for (int32_t a = 0; a < d.m; ++a) L.st[(size_t)(d.st_off + a)] = (int32_t)x.st[(size_t)a];
-        if (x.parent < 0) continue;
-        // a front row of the child is a pivot of the parent or one of its front rows
-        const NdNode& px = P.nodes[(size_t)x.parent];
-        const NdDev& pd = L.dev[(size_t)x.parent];
-        size_t j = 0;
-        for (int32_t a = 0; a < d.m; ++a) {
-            const int64_t q = x.st[(size_t)a];
-            if (q < px.end) {
-                L.ri[(size_t)(d.st_off + a)] = (int32_t)(q - px.start);
-            } else {
-                while (px.st[j] < q) ++j;
-                L.ri[(size_t)(d.st_off + a)] = pd.np_pad + (int32_t)j;
-            }
-        }
-    }
     L.pinv.resize((size_t)P.n);
     L.owner.resize((size_t)P.n);
-    for (int64_t v = 0; v < P.n; ++v) L.pinv[(size_t)v] = (int32_t)P.pinv[(size_t)v];
-    for (int32_t i = 0; i < nn; ++i)
-        for (int64_t q = P.nodes[(size_t)i].start; q < P.nodes[(size_t)i].end; ++q) L.owner[(size_t)q] = i;
+    // per node, disjoint ranges: on a few threads (the C5 plan's ~1M front
+    // rows and 1M columns)
+    auto per_node = [&](int32_t lo, int32_t hi) {
+        for (int32_t i = lo; i < hi; ++i) {
+            const NdNode& x = P.nodes[(size_t)i];
+            const NdDev& d = L.dev[(size_t)i];
+            for (int64_t q = x.start; q < x.end; ++q) {
+                L.owner[(size_t)q] = i;
+                L.pinv[(size_t)P.perm[(size_t)q]] = (int32_t)q;
+            }
+            for (int32_t a = 0; a < d.m; ++a) L.st[(size_t)(d.st_off + a)] = (int32_t)x.st[(size_t)a];
+            if (x.parent < 0) continue;
+            // a front row of the child is a pivot of the parent or one of its front rows
+            const NdNode& px = P.nodes[(size_t)x.parent];
+            const NdDev& pd = L.dev[(size_t)x.parent];
+            size_t j = 0;
+            for (int32_t a = 0; a < d.m; ++a) {
+                const int64_t q = x.st[(size_t)a];
+                if (q < px.end) {
+                    L.ri[(size_t)(d.st_off + a)] = (int32_t)(q - px.start);
+                } else {
+                    while (px.st[j] < q) ++j;
+                    L.ri[(size_t)(d.st_off + a)] = pd.np_pad + (int32_t)j;
+                }
+            }
+        }
+    };
+    {
+        const int nt = (int)std::min<int32_t>(8, std::max<int32_t>(1, nn / 1024));
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(per_node, (int32_t)((int64_t)nn * t / nt), (int32_t)((int64_t)nn * (t + 1) / nt));
+        per_node(0, (int32_t)((int64_t)nn / nt));
+        for (auto& th : pool) th.join();
+    }
     // per level: the nodes, the factor's tiles (K, node, I) and the extend tasks (slot, node, b)
     std::vector<std::vector<int32_t>> by_level((size_t)P.n_levels);
     for (int32_t i = 0; i < nn; ++i) by_level[(size_t)P.nodes[(size_t)i].level].push_back(i);
+    {  // the lists' sizes up front (no regrowth of ~1M-entry vectors)
+        size_t zt = 0, ft = 0, bt = 0, ex = 0;
+        for (const NdDev& d : L.dev) {
+            zt += (size_t)d.nt * (d.nt + 1) / 2;
+            ft += (size_t)d.nt;
+            bt += (size_t)d.npt;
+            ex += d.parent >= 0 ? (size_t)d.m : 0;
+        }
+        L.ztiles.reserve(zt);
+        L.tiles.reserve(zt);
+        L.ftasks.reserve(ft);
+        L.btasks.reserve(bt);
+        if (per_slot) L.ext.reserve(ex);
+        L.ext2.reserve(ex);
+        L.lvl_nodes.reserve((size_t)nn);
+    }
+    std::vector<char> used;  // the merge walk's marks, reused
     for (const auto& lv : by_level) {
         L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
         L.lvl_nodes.insert(L.lvl_nodes.end(), lv.begin(), lv.end());
@@ -864,6 +897,7 @@ void nd_layout(const NdPlan& P, int32_t small_nt, NdLayout& L) {
         for (int s = 0; s < 2; ++s) {
             L.ext_off.push_back((int64_t)L.ext.size());
             for (int32_t i : lv) {
+                if (!per_slot) break;
                 const NdNode& x = P.nodes[(size_t)i];
                 if (x.parent < 0 || x.slot != s) continue;
                 for (int32_t b = 0; b < L.dev[(size_t)i].m; ++b) L.ext.push_back(make_int2(i, b));
@@ -900,7 +934,7 @@ void nd_layout(const NdPlan& P, int32_t small_nt, NdLayout& L) {
             }
             const int32_t m1 = L.dev[(size_t)sib].m;
             const int32_t* r1 = L.ri.data() + L.dev[(size_t)sib].st_off;
-            std::vector<char> used((size_t)m1, 0);
+            used.assign((size_t)m1, 0);
             int32_t b1 = 0;
             for (int32_t b = 0; b < m0; ++b) {  // ri ascending on both sides: one merge walk
                 while (b1 < m1 && r1[b1] < r0[b]) ++b1;
@@ -1062,7 +1096,10 @@ int pinned_staging(size_t bytes, char** out) {
     return BSM_OK;
 }
 
-int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t s, NdCached& C) {
+// es > 0: the fronts (es-byte values) are allocated into C.fr on a helper
+// thread while the layout, the packing and the plan's upload run: a first
+// solve's 5 GB hipMalloc (C5) then costs no time of its own
+int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, hipStream_t s, NdCached& C) {
     const int64_t N = (int64_t)a->rows;
     // A's pattern to the host for the analysis
     char* stg = nullptr;
@@ -1081,6 +1118,24 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t 
     const int arc = nd_analyse(N, rp, cl, leaf, threads, P);
     BSM_REQUIRE(arc == 0, BSM_ERR_UNSUPPORTED,
                 "cholesky: rows must have strictly increasing columns (get_row_complete semantics)");
+    std::thread pre;
+    struct Join {
+        std::thread& t;
+        ~Join() {
+            if (t.joinable()) t.join();
+        }
+    } join_pre{pre};
+    if (es) {
+        int64_t f_elems = 0;  // nd_layout's sum of the fronts' f_pad^2
+        for (const auto& x : P.nodes) {
+            const int64_t np_pad = 64 * ((x.end - x.start + 63) / 64), ld = 64 * ((np_pad + (int64_t)x.st.size() + 63) / 64);
+            f_elems += ld * ld;
+        }
+        const int dev = a->device;
+        pre = std::thread([&C, f_elems, es, dev] {
+            if (hipSetDevice(dev) == hipSuccess) (void)C.fr.alloc((size_t)f_elems * es);  // nd_solve retries a failure
+        });
+    }
     const auto tl0 = host_now();
     NdLayout L;
     C.small_nt = small_nt;
@@ -1125,8 +1180,17 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t 
     const auto tp0 = host_now();
     char* hp = nullptr;
     BSM_TRY(pinned_staging(total, &hp));  // the pattern is no longer needed
+    // the arrays into the staging buffer in 1-MiB pieces on four threads
+    // (~40 MB at C5: one thread's memcpy into fresh pinned pages is ms)
+    struct Piece {
+        size_t o;
+        const char* p;
+        size_t b;
+    };
+    std::vector<Piece> pieces;
     auto put = [&](size_t o, const void* p, size_t b) {
-        if (b) memcpy(hp + o, p, b);
+        for (size_t c = 0; c < b; c += (1 << 20))
+            pieces.push_back({o + c, static_cast<const char*>(p) + c, std::min<size_t>(b - c, 1 << 20)});
     };
     put(C.o_dev, L.dev.data(), L.dev.size() * sizeof(NdDev));
     put(C.o_st, L.st.data(), L.st.size() * 4);
@@ -1141,6 +1205,16 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t 
     put(C.o_btask, L.btasks.data(), L.btasks.size() * sizeof(int2));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
     put(C.o_ztiles, L.ztiles.data(), L.ztiles.size() * sizeof(int4));
+    {
+        std::atomic<size_t> next{0};
+        auto copy = [&] {
+            for (size_t i; (i = next.fetch_add(1)) < pieces.size();) memcpy(hp + pieces[i].o, pieces[i].p, pieces[i].b);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < 4 && (size_t)t < pieces.size(); ++t) pool.emplace_back(copy);
+        copy();
+        for (auto& th : pool) th.join();
+    }
     C.ms_pack = ms_since(tp0);
     BSM_TRY(C.plan.alloc(total));
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
@@ -1300,7 +1374,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     // fronts of at most this many tile rows factor as one task each (C5: most
     // fronts of levels 0-4 have 2-4); BSM_ND_FRONT_NT=0: every front by tiles
     const char* fne = getenv("BSM_ND_FRONT_NT");
-    const int32_t small_nt = fne ? atoi(fne) : 4;
+    // BSM_ND_EXT_MERGE=0: one extend launch per child slot (A/B; same bits)
+    const char* eme = getenv("BSM_ND_EXT_MERGE");
+    const bool ext_merge = !(eme && atoi(eme) == 0);
+    // the layout's options (nd_layout's `lay`): part of the plan's keys
+    const int32_t small_nt = (fne ? atoi(fne) : 4) | (ext_merge ? 0 : 1 << 16);
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);
@@ -1318,7 +1396,9 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         }
         if (!pc) {
             pc = std::make_shared<NdCached>();
-            BSM_TRY(nd_build_plan(a, leaf, small_nt, s, *pc));
+            const char* ke0 = getenv("BSM_ND_KEEP");
+            const bool prealloc = cache && !(ke0 && atoi(ke0) == 0);  // the fronts will be this plan's own
+            BSM_TRY(nd_build_plan(a, leaf, small_nt, prealloc ? sizeof(T) : 0, s, *pc));
             if (shared) BSM_TRY(nd_cache_insert(a, key, pc, s));
         }
         if (cache) {
@@ -1346,9 +1426,6 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int4* d_ext2 = (const int4*)(pb + C.o_ext2);
     const int2* d_ftask = (const int2*)(pb + C.o_ftask);
     const int2* d_btask = (const int2*)(pb + C.o_btask);
-    // BSM_ND_EXT_MERGE=0: one extend launch per child slot (A/B; same bits)
-    const char* eme = getenv("BSM_ND_EXT_MERGE");
-    const bool ext_merge = !(eme && atoi(eme) == 0);
     const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
     // numeric storage: the plan's own buffers when this solve may hold them
     const char* ke = getenv("BSM_ND_KEEP");
