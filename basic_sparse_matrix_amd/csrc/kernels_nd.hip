@@ -979,10 +979,17 @@ struct NdCached {
     std::mutex num_mu;
     DBuf fr, dv, fl;
     std::atomic<size_t> kept_bytes{0};  // fr + dv + fl, written under num_mu
+    hipEvent_t fr_zeroed = nullptr;     // fr was just allocated and is being zeroed (nd_build_plan)
     // drop the kept numeric storage unless a solve holds it
+    void drop_zeroed() {  // fr no longer the freshly zeroed allocation (under num_mu)
+        if (fr_zeroed) (void)hipEventDestroy(fr_zeroed);
+        fr_zeroed = nullptr;
+    }
+    ~NdCached() { drop_zeroed(); }
     bool release_numeric() {
         std::unique_lock<std::mutex> l(num_mu, std::try_to_lock);
         if (!l.owns_lock()) return false;
+        drop_zeroed();
         fr.reset();
         dv.reset();
         fl.reset();
@@ -1010,10 +1017,12 @@ __device__ __forceinline__ uint64_t nd_mix64(uint64_t z) {  // SplitMix64's fina
 }
 
 // two sums (mod 2^64) of per-element hashes of (position, value): order-free
-// integer sums, so the key does not depend on the grid
+// integer sums, so the key does not depend on the grid; one pair of atomics
+// per workgroup (one per wave on 4096 workgroups contended for 0.4 ms)
 __global__ __launch_bounds__(256) void nd_pattern_hash(const int64_t* __restrict__ rp, int64_t n1,
                                                        const int32_t* __restrict__ col, int64_t nnz,
                                                        unsigned long long* __restrict__ h) {
+    __shared__ unsigned long long part[2][4];
     uint64_t s0 = 0, s1 = 0;
     const int64_t total = n1 + nnz;
     for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
@@ -1028,8 +1037,13 @@ __global__ __launch_bounds__(256) void nd_pattern_hash(const int64_t* __restrict
         s1 += (uint64_t)__shfl_xor((unsigned long long)s1, o);
     }
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&h[0], (unsigned long long)s0);
-        atomicAdd(&h[1], (unsigned long long)s1);
+        part[0][threadIdx.x >> 6] = s0;
+        part[1][threadIdx.x >> 6] = s1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned long long* p = part[threadIdx.x];
+        atomicAdd(&h[threadIdx.x], p[0] + p[1] + p[2] + p[3]);
     }
 }
 
@@ -1132,8 +1146,21 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             f_elems += ld * ld;
         }
         const int dev = a->device;
+        // ... and zeroed there on a stream of its own: a fresh allocation's
+        // first touch costs ~10 ms at C5 (5.2 GB), which then runs beside the
+        // host's layout and packing instead of inside the solve's first kernel
         pre = std::thread([&C, f_elems, es, dev] {
-            if (hipSetDevice(dev) == hipSuccess) (void)C.fr.alloc((size_t)f_elems * es);  // nd_solve retries a failure
+            if (hipSetDevice(dev) != hipSuccess || C.fr.alloc((size_t)f_elems * es) != BSM_OK) return;
+            hipStream_t z = nullptr;
+            hipEvent_t ev = nullptr;
+            if (hipStreamCreateWithFlags(&z, hipStreamNonBlocking) != hipSuccess) return;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+                hipMemsetAsync(C.fr.p, 0, C.fr.bytes, z) == hipSuccess && hipEventRecord(ev, z) == hipSuccess) {
+                C.fr_zeroed = ev;  // nd_solve waits for it and skips nd_zero_tiles once
+            } else if (ev) {
+                (void)hipEventDestroy(ev);
+            }
+            (void)hipStreamDestroy(z);  // released once its work is done
         });
     }
     const auto tl0 = host_now();
@@ -1236,7 +1263,7 @@ int nd_pattern_key(const bsm_csr* a, int64_t leaf, int32_t small_nt, hipStream_t
     DBuf hb;
     BSM_TRY(hb.alloc(16, s));
     BSM_HIP_TRY(hipMemsetAsync(hb.p, 0, 16, s));
-    nd_pattern_hash<<<(unsigned)std::min<int64_t>((total + 255) / 256, 4096), 256, 0, s>>>(
+    nd_pattern_hash<<<(unsigned)std::min<int64_t>((total + 255) / 256, 1024), 256, 0, s>>>(
         a->row_ptr, n + 1, a->col, (int64_t)a->nnz, hb.as<unsigned long long>());
     BSM_HIP_TRY(hipGetLastError());
     uint64_t h[2] = {0, 0};
@@ -1438,7 +1465,9 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const size_t fr_b = (size_t)C.f_elems * sizeof(T), dv_b = (size_t)std::max<int64_t>(C.dinv_elems, 1) * sizeof(T);
     const size_t nfl = (size_t)C.n_flags + (size_t)C.n_levels + 2;
     // a plan serves one dtype per handle; sizes match after the first solve
+    const void* fr_was = fr.p;
     BSM_TRY(nd_alloc_numeric(fr, fr_b, &C));
+    if (keep && fr.p != fr_was) C.drop_zeroed();  // reallocated: zeroed by nd_zero_tiles as usual
     BSM_TRY(nd_alloc_numeric(dv, dv_b, &C));
     BSM_TRY(nd_alloc_numeric(fl, nfl * sizeof(int), &C));
     if (keep) C.kept_bytes = fr.bytes + dv.bytes + fl.bytes;
@@ -1468,7 +1497,13 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     int* d_tickets = d_flags + C.n_flags;
     int* d_status = d_tickets + C.n_levels;
     T* F = fr.as<T>();
-    if (C.n_ztiles) {
+    if (keep && C.fr_zeroed) {  // the plan's first solve: fr is zeroed whole on another stream
+        const hipEvent_t ev = C.fr_zeroed;
+        C.fr_zeroed = nullptr;
+        const hipError_t we = hipStreamWaitEvent(s, ev, 0);
+        (void)hipEventDestroy(ev);
+        BSM_HIP_TRY(we);
+    } else if (C.n_ztiles) {
         nd_zero_tiles<T><<<(unsigned)C.n_ztiles, 256, 0, s>>>(d_nodes, d_ztiles, F);
         BSM_HIP_TRY(hipGetLastError());
     }

@@ -185,6 +185,12 @@ def main():
         if order == "nd":
             leaf = int(os.environ.get("BSM_ND_LEAF", "192"))
             model = nd_model(n, rp, ci, leaf, es)
+            # the process's first GPU work (runtime and device set-up, code
+            # objects) on a small system of another pattern, outside the clock:
+            # "cold" is the first solve of THIS pattern, not the process's first
+            wrp, wci, wv = orc.poisson2d(16)
+            solve(Csr.from_csr_arrays((256, 256), wrp, wci, wv.astype(dt)),
+                  Dense.from_columns([np.ones(256, dtype=dt)]), order="nd")
             # cold: the first solve of this pattern in the process, as the
             # reference's solve(a, b) is called (lib.rs:11, `a` by value): a new
             # handle (uploaded inside the clock), the host analysis, the plan
