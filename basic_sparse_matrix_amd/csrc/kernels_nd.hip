@@ -1247,6 +1247,10 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
     stage_mark("nd_upload", s);
+    if (pre.joinable()) {  // the fronts' allocation: the wait for it as a stage of its own
+        pre.join();
+        stage_mark("nd_fronts_alloc", s);
+    }
     return BSM_OK;
 }
 
@@ -1398,14 +1402,17 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int64_t leaf = le ? atoll(le) : 192;  // C5 leaf sweep: 128 / 192 / 256 / 320 -> 11.9 / 11.4 / 12.3 / 12.5 ms
     const bool cache = !(ce && atoi(ce) == 0);
     const bool shared = cache && !(she && atoi(she) == 0);  // the cache across handles (BSM_ND_SHARED=0: off)
-    // fronts of at most this many tile rows factor as one task each (C5: most
-    // fronts of levels 0-4 have 2-4); BSM_ND_FRONT_NT=0: every front by tiles
+    // BSM_ND_FRONT_NT=n: fronts of at most n tile rows factor as one task
+    // each (C5: most fronts of levels 0-4 have 2-4). Default 0, every front by
+    // tiles: measured at C5, n = 3 matches it and n = 4 / 5 are 0.25 / 0.5 ms
+    // slower (a middle level's 10-15 tiles in a row on one workgroup cost more
+    // than the tickets and flags they save; profiles/r06_b_*)
     const char* fne = getenv("BSM_ND_FRONT_NT");
     // BSM_ND_EXT_MERGE=0: one extend launch per child slot (A/B; same bits)
     const char* eme = getenv("BSM_ND_EXT_MERGE");
     const bool ext_merge = !(eme && atoi(eme) == 0);
     // the layout's options (nd_layout's `lay`): part of the plan's keys
-    const int32_t small_nt = (fne ? atoi(fne) : 4) | (ext_merge ? 0 : 1 << 16);
+    const int32_t small_nt = (fne ? atoi(fne) : 0) | (ext_merge ? 0 : 1 << 16);
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);

@@ -4,14 +4,15 @@ kernel-stats CSV (--kernel-trace --stats of scripts/solve_c5.py --orders nd)
 and the plan's work model in that run's JSON line (scripts/solve_c5.py's
 "model": true / padded flops of the fronts, bytes of L).
 
-Per solve (solves = calls of nd_scatter, one per solve):
+Per solve (solves: the line's nd_solves_in_process["full"], else the calls
+of nd_scatter, one per solve):
 * factor: nd_factor's time; true flops and 64-padded flops against the
   78.6 TF/s FP64 MFMA peak (MI355X_MICROARCH.md);
 * forward: nd_forward + nd_forward_tiles; backward: nd_backward +
   nd_backward_tiles; L's bytes (each entry read once) against 8 TB/s;
 * the fixed costs beside them (zero tiles, assemble, extend-add).
 
-usage: nd_roofline.py KERNEL_STATS.csv SOLVE_C5.jsonl [--dtype double]
+usage: nd_roofline.py KERNEL_STATS.csv SOLVE_C5.jsonl [--dtype double] [--solves N]
 """
 import argparse
 import csv
@@ -42,8 +43,10 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("jsonl")
     ap.add_argument("--dtype", default="double")
+    ap.add_argument("--solves", type=int, default=0,
+                    help="full-size solves in the profiled run (a line without nd_solves_in_process)")
     args = ap.parse_args()
-    model = None
+    model = nd_solves = None
     with open(args.jsonl) as f:
         for ln in f:
             ln = ln.strip()
@@ -51,9 +54,12 @@ def main():
                 d = json.loads(ln)
                 if d.get("config", {}).get("order") == "nd":
                     model = d["model"]
+                    nd_solves = d.get("nd_solves_in_process")
     assert model, "no nd line with a model in " + args.jsonl
     k = kernel_ns(args.csv, args.dtype)
-    solves = k.get("nd_scatter:calls", 0)
+    # the full-size solves of the run (solve_c5.py records them; its 16 x 16
+    # warm-up solve's kernels stay in the totals: ~1 % of one C5 solve)
+    solves = args.solves or (nd_solves or {}).get("full") or k.get("nd_scatter:calls", 0)
     assert solves > 0, "no nd_scatter calls in " + args.csv
     ms = lambda *names: sum(k.get(n, 0) for n in names) * 1e-6 / solves  # noqa: E731
     fac, fwd, bwd = ms("nd_factor"), ms("nd_forward", "nd_forward_tiles"), ms("nd_backward", "nd_backward_tiles")

@@ -181,7 +181,7 @@ def main():
     band_bytes = float(es) * n * (g + 1)
     _lib.stage_timing(True)
     for order in args.orders.split(","):
-        cold = by_value = model = None
+        cold = by_value = model = nd_solves = None
         if order == "nd":
             leaf = int(os.environ.get("BSM_ND_LEAF", "192"))
             model = nd_model(n, rp, ci, leaf, es)
@@ -191,6 +191,7 @@ def main():
             wrp, wci, wv = orc.poisson2d(16)
             solve(Csr.from_csr_arrays((256, 256), wrp, wci, wv.astype(dt)),
                   Dense.from_columns([np.ones(256, dtype=dt)]), order="nd")
+            nd_solves = {"small_warmup_16x16": 1, "full": 1 + max(args.reps, 1) + 1 + args.reps}
             # cold: the first solve of this pattern in the process, as the
             # reference's solve(a, b) is called (lib.rs:11, `a` by value): a new
             # handle (uploaded inside the clock), the host analysis, the plan
@@ -253,7 +254,7 @@ def main():
                 "primary": "cold: solve(a, b) takes a by value (lib.rs:11), so a drop-in caller's first solve of "
                            "a pattern pays the analysis; by_value: later calls with new handles of that pattern; "
                            "wall_ms: the same handle again",
-                "cold": cold, "by_value": by_value, "model": model,
+                "cold": cold, "by_value": by_value, "model": model, "nd_solves_in_process": nd_solves,
                 "factor": {"stage": "nd_factor (zero tiles + assemble are nd_assemble; the extend-adds run inside "
                                     "this stage, so its time bounds the factor kernels' from above)",
                            "ms": fms, "true_flops": model["true_flops"], "padded_flops": model["padded_flops"],

@@ -299,12 +299,15 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
       node, pivot tile and column; the front rows' products first, then each
       pivot tile's as its x arrives) instead of one workgroup per node and
       column, which sums its rows in that same tile order;
-    * BSM_ND_FRONT_NT: fronts of at most 4 tile rows factored whole by one
-      workgroup, their tiles in column order, instead of one ticketed
-      workgroup per tile: every tile the same operations in the same order.
+    * BSM_ND_FRONT_NT (off by default; 4 here): fronts of at most 4 tile rows
+      factored whole by one workgroup, their tiles in column order, instead
+      of one ticketed workgroup per tile: every tile the same operations in
+      the same order.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
+    if switch == "BSM_ND_FRONT_NT":  # off by default: on (4) against off
+        monkeypatch.setenv(switch, "4")
     g = 90
     n = g * g
     rp, ci, v = orc.poisson2d(g)
@@ -366,3 +369,42 @@ def test_c5_nd_poisson_1m_f64_properties(orc, golden_c5):
     assert rel_err(x[::golden_c5["x_stride"]], exact) < 1e-6
     assert rel_err(x, x_true) < 1e-6
     assert residual(rp, ci, v, x, b) < 1e-12
+
+
+def test_nd_plan_cache_concurrent_handles(orc):
+    """Four threads, each solving a new handle of one pattern three times
+    (ctypes releases the GIL, so the calls overlap): the library-wide cache's
+    lookups, insertions and the kept numeric storage (one solve holds it, a
+    concurrent one allocates its own) give every call the single-thread
+    bits."""
+    import threading
+
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.nd_cache_clear()
+    g = 48
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    b = orc.gen_x_cols(1016, n, 1)
+    ref = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0)).copy()
+    _lib.nd_cache_clear()
+    out, errs = [], []
+
+    def work():
+        try:
+            for _ in range(3):
+                x = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0)
+                out.append(np.asarray(x).copy())
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=work) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    assert len(out) == 12
+    for x in out:
+        assert np.array_equal(x.view(np.uint8), ref.view(np.uint8))
+    assert _lib.nd_cache_info()["entries"] == 1
