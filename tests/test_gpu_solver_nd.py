@@ -408,3 +408,26 @@ def test_nd_plan_cache_concurrent_handles(orc):
     for x in out:
         assert np.array_equal(x.view(np.uint8), ref.view(np.uint8))
     assert _lib.nd_cache_info()["entries"] == 1
+
+
+def test_nd_plan_shared_across_dtypes(orc):
+    """A plan serves both value types of one pattern (its numeric storage is
+    re-sized per dtype): f64, then f32, then f64 again on new handles, each
+    right for its own type, the f64 bits repeated."""
+    from basic_sparse_matrix_amd import _lib
+
+    _lib.nd_cache_clear()
+    g = 36
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    b64 = orc.gen_x_cols(1017, n, 1)
+    b32 = [c.astype(np.float32) for c in b64]
+    x0 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b64), order="nd").get_col(0)).copy()
+    x32 = solve(Csr.from_csr_arrays((n, n), rp, ci, v.astype(np.float32)), Dense.from_columns(b32), order="nd").get_col(0)
+    x1 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b64), order="nd").get_col(0)).copy()
+    info = _lib.nd_cache_info()
+    assert info["entries"] == 1 and info["hits"] >= 2
+    ex = orc.solve(n, rp, ci, v, b64, band=True)[0]
+    assert rel_err(x0, ex) < 1e-10
+    assert rel_err(x32, ex) < 2e-3
+    assert np.array_equal(x0.view(np.uint8), x1.view(np.uint8))
