@@ -113,11 +113,21 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 // it waits on nobody: these tasks follow the tiled fronts' tickets and fill
 // the CUs while those fronts' chains run, without a ticket and a flag
 // hand-off through L2 per tile.
-template <typename T>
+// STAMPS (BSM_ND_STAMPS=1, a diagnostic instantiation: the counters cost
+// SGPRs the product build cannot spare): per workgroup,
+// thread 0's shader-clock cycles in the flag waits, the products (loads,
+// LDS staging, MFMA), the diagonal factors, the sub-diagonal solves, the
+// update tiles' stores and the drains, and the tile counts of each kind,
+// added into stamps[0..11] at the end
+template <typename T, bool STAMPS = false>
 __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
                                                  int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
                                                  int* __restrict__ flags, int* __restrict__ ticket,
-                                                 int* __restrict__ status, int pad_skip) {
+                                                 int* __restrict__ status, int pad_skip,
+                                                 unsigned long long* __restrict__ stamps = nullptr) {
+    long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
+    long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
+    const long long c_start = STAMPS ? (long long)clock64() : 0;
     __shared__ T PT[64][TLD];
     __shared__ T QT[64][TLD];
     __shared__ T rd[64];
@@ -182,9 +192,12 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
         // (256, 2) keeps the VGPRs at 128; at 136 the occupancy query gave one
         // and the C5 factor took 8.5 instead of 5.7 ms)
         const int Jn = K < npt ? K : npt;
+        long long c0 = STAMPS ? (long long)clock64() : 0;
         for (int J = 0; J < Jn; ++J) {
+            const long long cw = STAMPS ? (long long)clock64() : 0;
             wait_flag(&fl[I * npt + J]);
             if (I != K) wait_flag(&fl[K * npt + J]);
+            if (STAMPS) c_wait += (long long)clock64() - cw;
             T va[16];
             load(va, I, J);
             store(PT, va);
@@ -195,6 +208,12 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             __syncthreads();
             mfma_tile<T, true>(PTl, I != K ? QTl : PTl, acc, w, lane);
             __syncthreads();
+        }
+        if (STAMPS) {
+            const long long c1 = (long long)clock64();
+            c_prod += c1 - c0;
+            n_prod += Jn;
+            c0 = c1;
         }
         if (K < npt && I == K) {
 #pragma unroll
@@ -245,9 +264,17 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
 #pragma unroll
                 for (int q = 0; q < 4; ++q) Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q] = acc[cb][q];
         }
+        long long c2 = 0;
+        if (STAMPS) {
+            c2 = (long long)clock64();
+            if (K < npt && I == K) c_diag += c2 - c0, ++n_diag;
+            else if (K < npt) c_trsm += c2 - c0, ++n_trsm;
+            else c_upd += c2 - c0, ++n_upd;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (K < npt && tid == 0) __hip_atomic_store(&fl[I * npt + K], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (STAMPS) c_drain += (long long)clock64() - c2, ++n_tiles;
         if (++I == ntf) {  // a whole front: the next tile in column order
             ++K;
             I = K;
@@ -257,6 +284,12 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
       if (tid == 0) tk = atomicAdd(ticket, 1);
       __syncthreads();
       t = __builtin_amdgcn_readfirstlane(tk);
+    }
+    if (STAMPS && tid == 0) {
+        c_total = (long long)clock64() - c_start;
+        const long long v[12] = {c_total, c_wait, c_prod, c_diag, c_trsm, c_upd, c_drain, n_tiles, n_prod, n_diag,
+                                 n_trsm, n_upd};
+        for (int i = 0; i < 12; ++i) atomicAdd(&stamps[i], (unsigned long long)v[i]);
     }
 }
 
@@ -1520,6 +1553,13 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     nd_pad_pivots<T><<<(unsigned)C.nn, 64, 0, s>>>(d_nodes, F);
     BSM_HIP_TRY(hipGetLastError());
     stage_mark("nd_assemble", s);
+    // BSM_ND_STAMPS=1: nd_factor's per-level cycle stamps, printed after the solve
+    const char* sde = getenv("BSM_ND_STAMPS");
+    DBuf stamps;
+    if (sde && atoi(sde) == 1) {
+        BSM_TRY(stamps.alloc((size_t)C.n_levels * 12 * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(stamps.p, 0, (size_t)C.n_levels * 12 * sizeof(unsigned long long), s));
+    }
     // BSM_ND_PAD_SKIP=0: diagonal tiles factor their padding panels too (A/B; same bits)
     const char* pse = getenv("BSM_ND_PAD_SKIP");
     const int pad_skip = !(pse && atoi(pse) == 0);
@@ -1527,8 +1567,13 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         const int64_t t0 = C.tiles_off[(size_t)lv], nt = C.tiles_off[(size_t)lv + 1] - t0;
         if (nt > 0) {
             const int64_t grid = std::min<int64_t>(nt, (int64_t)cus * per_cu);
-            nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                        d_tickets + lv, d_status, pad_skip);
+            if (stamps.p)
+                nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
+                                                                  d_tickets + lv, d_status, pad_skip,
+                                                                  stamps.as<unsigned long long>() + 12 * lv);
+            else
+                nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
+                                                            d_tickets + lv, d_status, pad_skip);
             BSM_HIP_TRY(hipGetLastError());
         }
         if (ext_merge) {
@@ -1607,6 +1652,20 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     BSM_HIP_TRY(hipStreamSynchronize(s));
     drain.armed = false;
     stage_mark("nd_copy_out", s);
+    if (stamps.p) {
+        std::vector<unsigned long long> h((size_t)C.n_levels * 12);
+        BSM_HIP_TRY(hipMemcpy(h.data(), stamps.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (int32_t lv = 0; lv < C.n_levels; ++lv) {
+            const unsigned long long* v = &h[(size_t)lv * 12];
+            const double nt = v[7] ? (double)v[7] : 1.0;
+            fprintf(stderr,
+                    "[bsm nd stamps] level %2d: %6llu tiles (prod %llu, diag %llu, trsm %llu, upd %llu); cycles per "
+                    "tile: wait %.0f, products %.0f, diag %.0f, trsm %.0f, update %.0f, drain %.0f; workgroup total "
+                    "%.0f per tile\n",
+                    lv, v[7], v[8], v[9], v[10], v[11], v[1] / nt, (v[2] - v[1]) / nt, v[3] / nt, v[4] / nt,
+                    v[5] / nt, v[6] / nt, v[0] / nt);
+        }
+    }
     BSM_REQUIRE(!(h & ST_TIMEOUT), BSM_ERR_HIP, "nd factor: tile hand-off timed out");
     BSM_REQUIRE(!(h & ST_NOT_PD), BSM_ERR_UNSUPPORTED,
                 "cholesky: matrix is not positive definite (a pivot is <= 0 or not finite)");
