@@ -1128,19 +1128,47 @@ size_t nd_cache_limit(const char* env, size_t dflt) {
 // The calling thread's page-locked staging buffer (grown on demand, kept for
 // the thread's later plans): the pattern's download and the plan's upload
 // are direct DMA (~30 MB each at C5) instead of pageable copies.
-int pinned_staging(size_t bytes, char** out) {
-    thread_local char* buf = nullptr;
-    thread_local size_t cap = 0;
-    if (cap < bytes) {
-        if (buf) (void)hipHostFree(buf);
-        buf = nullptr;
-        cap = 0;
-        const size_t want = std::max(bytes, cap * 2);
-        BSM_HIP_TRY(hipHostMalloc((void**)&buf, want, hipHostMallocDefault));
-        cap = want;
-    }
-    *out = buf;
+struct PinnedStage {
+    char* buf = nullptr;
+    size_t cap = 0;
+};
+PinnedStage& pinned_stage() {
+    thread_local PinnedStage st;
+    return st;
+}
+int pinned_grow(PinnedStage& st, size_t bytes) {
+    if (st.cap >= bytes) return BSM_OK;
+    if (st.buf) (void)hipHostFree(st.buf);
+    st.buf = nullptr;
+    st.cap = 0;
+    BSM_HIP_TRY(hipHostMalloc((void**)&st.buf, bytes, hipHostMallocDefault));
+    st.cap = bytes;
     return BSM_OK;
+}
+int pinned_staging(size_t bytes, char** out) {
+    PinnedStage& st = pinned_stage();
+    BSM_TRY(pinned_grow(st, bytes));
+    *out = st.buf;
+    return BSM_OK;
+}
+
+// An upper bound of nd_build_plan's packed plan bytes, from the analysis
+// alone (the same arrays as the layout; the merged extend tasks and the
+// factor's tasks are at most the child columns and the lower tiles)
+size_t nd_plan_bytes_bound(const NdPlan& P, int32_t lay) {
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    size_t sm = 0, zt = 0, ft = 0, bt = 0;
+    for (const auto& x : P.nodes) {
+        const int64_t npt = (x.end - x.start + 63) / 64, nt = (64 * npt + (int64_t)x.st.size() + 63) / 64;
+        sm += x.st.size();
+        zt += (size_t)(nt * (nt + 1) / 2);
+        ft += (size_t)nt;
+        bt += (size_t)npt;
+    }
+    const size_t nn = P.nodes.size(), n = (size_t)P.n;
+    return al(nn * sizeof(NdDev)) + 2 * al(sm * 4) + 2 * al(n * 4) + al(nn * 4) + al(zt * sizeof(int4)) +
+           al(((lay >> 16) & 1) ? sm * sizeof(int2) : 0) + al(sm * sizeof(int4)) + al(ft * sizeof(int2)) +
+           al(bt * sizeof(int2)) + al(n * 8) + al(zt * sizeof(int4));
 }
 
 // es > 0: the fronts (es-byte values) are allocated into C.fr on a helper
@@ -1172,6 +1200,27 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             if (t.joinable()) t.join();
         }
     } join_pre{pre};
+    // on the helper as well (the pattern in the staging buffer is no longer
+    // read): the plan's device buffer and the calling thread's page-locked
+    // staging buffer, both at an upper bound of the packed plan (~42 MB at
+    // C5), so the packing and the upload below allocate nothing
+    const size_t plan_bound = nd_plan_bytes_bound(P, small_nt);
+    PinnedStage* const stage = &pinned_stage();
+    {
+        const int dev0 = a->device;
+        pre = std::thread([&C, plan_bound, stage, dev0] {
+            if (hipSetDevice(dev0) != hipSuccess) return;
+            (void)C.plan.alloc(plan_bound);      // the main thread allocates again if this failed
+            (void)pinned_grow(*stage, plan_bound);  // likewise (pinned_staging)
+        });
+    }
+    std::thread pre_fronts;
+    struct JoinF {
+        std::thread& t;
+        ~JoinF() {
+            if (t.joinable()) t.join();
+        }
+    } join_fronts{pre_fronts};
     if (es) {
         int64_t f_elems = 0;  // nd_layout's sum of the fronts' f_pad^2
         for (const auto& x : P.nodes) {
@@ -1182,7 +1231,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         // ... and zeroed there on a stream of its own: a fresh allocation's
         // first touch costs ~10 ms at C5 (5.2 GB), which then runs beside the
         // host's layout and packing instead of inside the solve's first kernel
-        pre = std::thread([&C, f_elems, es, dev] {
+        pre_fronts = std::thread([&C, f_elems, es, dev] {
             if (hipSetDevice(dev) != hipSuccess || C.fr.alloc((size_t)f_elems * es) != BSM_OK) return;
             hipStream_t z = nullptr;
             hipEvent_t ev = nullptr;
@@ -1237,6 +1286,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     C.o_perm = C.o_btask + al(L.btasks.size() * sizeof(int2));
     C.o_ztiles = C.o_perm + al((size_t)N * 8);
     const size_t total = C.o_ztiles + al(L.ztiles.size() * sizeof(int4));
+    if (pre.joinable()) pre.join();  // the plan's buffers (device, page-locked staging)
     const auto tp0 = host_now();
     char* hp = nullptr;
     BSM_TRY(pinned_staging(total, &hp));  // the pattern is no longer needed
@@ -1276,12 +1326,12 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         for (auto& th : pool) th.join();
     }
     C.ms_pack = ms_since(tp0);
-    BSM_TRY(C.plan.alloc(total));
+    if (C.plan.bytes < total) BSM_TRY(C.plan.alloc(total));
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
     BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
     stage_mark("nd_upload", s);
-    if (pre.joinable()) {  // the fronts' allocation: the wait for it as a stage of its own
-        pre.join();
+    if (pre_fronts.joinable()) {  // the fronts' allocation: the wait for it as a stage of its own
+        pre_fronts.join();
         stage_mark("nd_fronts_alloc", s);
     }
     return BSM_OK;
