@@ -900,17 +900,23 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         L.ext2.reserve(ex);
         L.lvl_nodes.reserve((size_t)nn);
     }
-    std::vector<char> used;  // the merge walk's marks, reused
-    for (const auto& lv : by_level) {
-        L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
-        L.lvl_nodes.insert(L.lvl_nodes.end(), lv.begin(), lv.end());
-        L.tiles_off.push_back((int64_t)L.tiles.size());
+    // The levels' lists are independent: built on threads (the leaf level,
+    // the largest, sets the time), then concatenated in level order
+    struct LevelLists {
+        std::vector<int4> zt, tiles, ext2;
+        std::vector<int2> ext[2], ft, bt;
+    };
+    std::vector<LevelLists> per((size_t)P.n_levels);
+    auto build_level = [&](size_t li) {
+        const auto& lv = by_level[li];
+        LevelLists& o = per[li];
+        std::vector<char> used;  // the merge walk's marks, reused
         int32_t kmax = 0;
         for (int32_t i : lv) kmax = std::max(kmax, L.dev[(size_t)i].nt);
         // every front's lower tiles (nd_zero_tiles)
         for (int32_t i : lv)
             for (int32_t K = 0; K < L.dev[(size_t)i].nt; ++K)
-                for (int32_t I = K; I < L.dev[(size_t)i].nt; ++I) L.ztiles.push_back(make_int4(i, I, K, 0));
+                for (int32_t I = K; I < L.dev[(size_t)i].nt; ++I) o.zt.push_back(make_int4(i, I, K, 0));
         // tiled fronts, column K of every front: the diagonal tiles first,
         // then the tiles below (which wait for their diagonal tile's
         // inverse), so the waiting tiles' diagonals are well under way when
@@ -918,39 +924,33 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         auto small = [&](int32_t i) { return L.dev[(size_t)i].nt <= small_nt; };
         for (int32_t K = 0; K < kmax; ++K) {
             for (int32_t i : lv)
-                if (!small(i) && K < L.dev[(size_t)i].nt) L.tiles.push_back(make_int4(i, K, K, 0));
+                if (!small(i) && K < L.dev[(size_t)i].nt) o.tiles.push_back(make_int4(i, K, K, 0));
             for (int32_t i : lv) {
                 const NdDev& d = L.dev[(size_t)i];
                 if (small(i)) continue;
-                for (int32_t I = K + 1; I < d.nt; ++I) L.tiles.push_back(make_int4(i, I, K, 0));
+                for (int32_t I = K + 1; I < d.nt; ++I) o.tiles.push_back(make_int4(i, I, K, 0));
             }
         }
         for (int32_t i : lv)
-            if (small(i)) L.tiles.push_back(make_int4(i, 0, 0, 1));
-        for (int s = 0; s < 2; ++s) {
-            L.ext_off.push_back((int64_t)L.ext.size());
+            if (small(i)) o.tiles.push_back(make_int4(i, 0, 0, 1));
+        for (int s = 0; s < 2 && per_slot; ++s)
             for (int32_t i : lv) {
-                if (!per_slot) break;
                 const NdNode& x = P.nodes[(size_t)i];
                 if (x.parent < 0 || x.slot != s) continue;
-                for (int32_t b = 0; b < L.dev[(size_t)i].m; ++b) L.ext.push_back(make_int2(i, b));
+                for (int32_t b = 0; b < L.dev[(size_t)i].m; ++b) o.ext[s].push_back(make_int2(i, b));
             }
-        }
-        // both slots in one launch: a slot-0 child's columns, each paired with
-        // the slot-1 sibling's column landing on the same parent column when
-        // that sibling is on this level too, then the sibling's unpaired ones
-        L.ftask_off.push_back((int64_t)L.ftasks.size());
         for (int32_t I = 0; I < kmax; ++I)
             for (int32_t i : lv)
-                if (I < L.dev[(size_t)i].nt) L.ftasks.push_back(make_int2(i, I));
-        L.btask_off.push_back((int64_t)L.btasks.size());
+                if (I < L.dev[(size_t)i].nt) o.ft.push_back(make_int2(i, I));
         int32_t pmax = 0;
         for (int32_t i : lv) pmax = std::max(pmax, L.dev[(size_t)i].npt);
         for (int32_t d = 0; d < pmax; ++d)
             for (int32_t i : lv)
-                if (d < L.dev[(size_t)i].npt) L.btasks.push_back(make_int2(i, L.dev[(size_t)i].npt - 1 - d));
-        L.ext2_off.push_back((int64_t)L.ext2.size());
-        if (lv.empty()) continue;
+                if (d < L.dev[(size_t)i].npt) o.bt.push_back(make_int2(i, L.dev[(size_t)i].npt - 1 - d));
+        if (lv.empty()) return;
+        // both slots in one launch: a slot-0 child's columns, each paired with
+        // the slot-1 sibling's column landing on the same parent column when
+        // that sibling is on this level too, then the sibling's unpaired ones
         const int32_t level = P.nodes[(size_t)lv.front()].level;
         for (int32_t i : lv) {
             const NdNode& x = P.nodes[(size_t)i];
@@ -962,7 +962,7 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
             const int32_t m0 = L.dev[(size_t)i].m;
             const int32_t* r0 = L.ri.data() + L.dev[(size_t)i].st_off;
             if (!pair) {
-                for (int32_t b = 0; b < m0; ++b) L.ext2.push_back(make_int4(i, b, -1, -1));
+                for (int32_t b = 0; b < m0; ++b) o.ext2.push_back(make_int4(i, b, -1, -1));
                 continue;
             }
             const int32_t m1 = L.dev[(size_t)sib].m;
@@ -973,11 +973,41 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
                 while (b1 < m1 && r1[b1] < r0[b]) ++b1;
                 const bool hit = b1 < m1 && r1[b1] == r0[b];
                 if (hit) used[(size_t)b1] = 1;
-                L.ext2.push_back(make_int4(i, b, hit ? sib : -1, hit ? b1 : -1));
+                o.ext2.push_back(make_int4(i, b, hit ? sib : -1, hit ? b1 : -1));
             }
             for (int32_t b = 0; b < m1; ++b)
-                if (!used[(size_t)b]) L.ext2.push_back(make_int4(sib, b, -1, -1));
+                if (!used[(size_t)b]) o.ext2.push_back(make_int4(sib, b, -1, -1));
         }
+    };
+    {
+        std::atomic<size_t> next{0};
+        auto work = [&] {
+            for (size_t li; (li = next.fetch_add(1)) < per.size();) build_level(li);
+        };
+        std::vector<std::thread> pool;
+        const int nt = (int)std::min<size_t>(8, per.size());
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+    }
+    for (size_t li = 0; li < per.size(); ++li) {
+        const auto& lv = by_level[li];
+        const LevelLists& o = per[li];
+        L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
+        L.lvl_nodes.insert(L.lvl_nodes.end(), lv.begin(), lv.end());
+        L.tiles_off.push_back((int64_t)L.tiles.size());
+        L.ztiles.insert(L.ztiles.end(), o.zt.begin(), o.zt.end());
+        L.tiles.insert(L.tiles.end(), o.tiles.begin(), o.tiles.end());
+        for (int sl = 0; sl < 2; ++sl) {
+            L.ext_off.push_back((int64_t)L.ext.size());
+            L.ext.insert(L.ext.end(), o.ext[sl].begin(), o.ext[sl].end());
+        }
+        L.ftask_off.push_back((int64_t)L.ftasks.size());
+        L.ftasks.insert(L.ftasks.end(), o.ft.begin(), o.ft.end());
+        L.btask_off.push_back((int64_t)L.btasks.size());
+        L.btasks.insert(L.btasks.end(), o.bt.begin(), o.bt.end());
+        L.ext2_off.push_back((int64_t)L.ext2.size());
+        L.ext2.insert(L.ext2.end(), o.ext2.begin(), o.ext2.end());
     }
     L.lvl_off.push_back((int64_t)L.lvl_nodes.size());
     L.tiles_off.push_back((int64_t)L.tiles.size());
