@@ -811,7 +811,8 @@ struct NdLayout {
 // lay: the layout's options. Bits 0-15: fronts of at most this many tile
 // rows are one whole-front task of nd_factor (0: every front by tiles); bit
 // 16: the per-slot extend lists too (BSM_ND_EXT_MERGE=0's A/B path; ~1M
-// entries at C5 that the default merged launches never read)
+// entries at C5 that the default merged launches never read); bits 17-27:
+// the lag of the tiles below a diagonal, in fronts (0: none)
 void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
     const int32_t small_nt = lay & 0xffff;
     const bool per_slot = (lay >> 16) & 1;
@@ -921,14 +922,27 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         // then the tiles below (which wait for their diagonal tile's
         // inverse), so the waiting tiles' diagonals are well under way when
         // they are taken; then the small fronts, one task each
+        // With a lag (bits 17-27 of lay, in fronts), a front's tiles below the
+        // diagonal follow its diagonal tile by `lag` fronts' diagonals
+        // instead of all of them: at about the grid's size (512 workgroups)
+        // the diagonal is done when they are taken, and the level's other
+        // fronts are not held up behind the whole column of diagonals. 0: all
+        // of a column's diagonal tiles first (round 5). Either way a tile only
+        // waits on earlier tickets.
         auto small = [&](int32_t i) { return L.dev[(size_t)i].nt <= small_nt; };
+        const size_t lag_units = (size_t)((lay >> 17) & 0x7ff);
+        std::vector<int32_t> fr;
         for (int32_t K = 0; K < kmax; ++K) {
+            fr.clear();
             for (int32_t i : lv)
-                if (!small(i) && K < L.dev[(size_t)i].nt) o.tiles.push_back(make_int4(i, K, K, 0));
-            for (int32_t i : lv) {
-                const NdDev& d = L.dev[(size_t)i];
-                if (small(i)) continue;
-                for (int32_t I = K + 1; I < d.nt; ++I) o.tiles.push_back(make_int4(i, I, K, 0));
+                if (!small(i) && K < L.dev[(size_t)i].nt) fr.push_back(i);
+            const size_t nf = fr.size(), lag = lag_units ? lag_units : nf;
+            for (size_t idx = 0; idx < nf + lag; ++idx) {
+                if (idx < nf) o.tiles.push_back(make_int4(fr[idx], K, K, 0));
+                if (idx >= lag && idx - lag < nf) {
+                    const int32_t i = fr[idx - lag];
+                    for (int32_t I = K + 1; I < L.dev[(size_t)i].nt; ++I) o.tiles.push_back(make_int4(i, I, K, 0));
+                }
             }
         }
         for (int32_t i : lv)
@@ -1525,7 +1539,12 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const char* eme = getenv("BSM_ND_EXT_MERGE");
     const bool ext_merge = !(eme && atoi(eme) == 0);
     // the layout's options (nd_layout's `lay`): part of the plan's keys
-    const int32_t small_nt = (fne ? atoi(fne) : 0) | (ext_merge ? 0 : 1 << 16);
+    // BSM_ND_LAG=u: a front's tiles below the diagonal trail its diagonal
+    // tile by u fronts' diagonals (nd_layout; 0: all diagonals of a column
+    // first, the round-5 order)
+    const char* lge = getenv("BSM_ND_LAG");
+    const int32_t lag_units = std::min(0x7ff, std::max(0, lge ? atoi(lge) : 512));
+    const int32_t small_nt = (fne ? atoi(fne) : 0) | (ext_merge ? 0 : 1 << 16) | (lag_units << 17);
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);

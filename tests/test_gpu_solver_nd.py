@@ -279,7 +279,7 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
-                                    "BSM_ND_FRONT_NT"])
+                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -302,12 +302,18 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
     * BSM_ND_FRONT_NT (off by default; 4 here): fronts of at most 4 tile rows
       factored whole by one workgroup, their tiles in column order, instead
       of one ticketed workgroup per tile: every tile the same operations in
-      the same order.
+      the same order;
+    * BSM_ND_LAG (512 by default; 1 here, as this size's levels have fewer
+      fronts): a front's tiles below the diagonal taken right after the next
+      front's diagonal tile instead of after the column's last one: the same
+      tiles, only their tickets' order changes.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
     if switch == "BSM_ND_FRONT_NT":  # off by default: on (4) against off
         monkeypatch.setenv(switch, "4")
+    if switch == "BSM_ND_LAG":
+        monkeypatch.setenv(switch, "1")
     g = 90
     n = g * g
     rp, ci, v = orc.poisson2d(g)
