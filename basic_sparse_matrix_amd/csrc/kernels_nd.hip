@@ -12,8 +12,11 @@
 //                 hand-offs as in blk_chol). Pivot tiles: L and the inverse
 //                 diagonal tiles Dinv; trailing tiles: the update block
 //                 U = F22 - L21 L21^T left in place.
-//   nd_extend  -- U of each child added into its parent's front (children
-//                 slot 0, then slot 1: a fixed order, so the bits repeat).
+//   the extend-add -- U of each child added into its parent's front (the
+//                 lower-level child first, then slot 0: a fixed order, so
+//                 the bits repeat): by default inside the parent's nd_factor
+//                 tiles as they load (the "pull"); BSM_ND_PULL=0 runs
+//                 nd_extend2 (or nd_extend per slot) after each level.
 // The solves walk the same levels: forward bottom-up (a child's update
 // vector into its parent), backward top-down (the ancestors' x gathered).
 // Not bit-exact with the reference (another elimination order, FMA); within
@@ -41,7 +44,10 @@ struct NdDev {
     int64_t st_off;    // m front rows (st) and their places in the parent's front (ri)
     int64_t voff;      // f_pad solve-vector entries per right-hand column
     int64_t start;     // own columns [start, start + np)
-    int32_t ld, np, np_pad, m, npt, nt, parent, kid0, kid1, pad;
+    int32_t ld, np, np_pad, m, npt, nt, parent, kid0, kid1;
+    int32_t tb_off;     // (child) nt + 1 bounds of the parent's tile rows in ri: tb[t] = first a, ri[a] >= 64 t
+    int32_t pull_swap;  // (parent) kid1's update block is added before kid0's (kid1 on a lower level)
+    int32_t pad;
 };
 
 __device__ __forceinline__ int32_t lower_bound_i32(const int32_t* a, int32_t len, int64_t x) {
@@ -119,20 +125,24 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 // LDS staging, MFMA), the diagonal factors, the sub-diagonal solves, the
 // update tiles' stores and the drains, and the tile counts of each kind,
 // added into stamps[0..11] at the end
+constexpr int ND_NSTAMP = 18;  // per level: BSM_ND_STAMPS's counters
 template <typename T, bool STAMPS = false>
 __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
                                                  int64_t ntiles, T* __restrict__ F, T* __restrict__ Dinv,
                                                  int* __restrict__ flags, int* __restrict__ ticket,
                                                  int* __restrict__ status, int pad_skip,
+                                                 const int32_t* __restrict__ tb, const int32_t* __restrict__ ri,
                                                  unsigned long long* __restrict__ stamps = nullptr) {
     long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
     long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
+    long long c_pl[4] = {0, 0, 0, 0}, n_pull = 0;  // the pull's phases: tile + first child's loads, its adds, second, read-back
     const long long c_start = STAMPS ? (long long)clock64() : 0;
     __shared__ T PT[64][TLD];
     __shared__ T QT[64][TLD];
     __shared__ T rd[64];
     __shared__ T Di[4 * 256];
     __shared__ T Tb[3 * 256];
+    __shared__ int pcs[2][64];  // the pull: a child block's columns' places in the tile
     __shared__ int tk;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -180,19 +190,114 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                 X[e >> 6][e & 63] = v[u];
             }
         };
+        long long c0 = STAMPS ? (long long)clock64() : 0;
         T acc[4][4];
+        if (tb && (nd.kid0 >= 0 || nd.kid1 >= 0)) {
+            // The children's update blocks, pulled into this tile (tb: no
+            // nd_extend launches): the entries (a, b), a >= b, of child c
+            // with ri[a] in tile row I and ri[b] in tile column K, i.e. a in
+            // [tb[I], tb[I + 1]), b in [tb[K], tb[K + 1]) (ri ascending).
+            // The tile goes to LDS by coalesced columns; thread (lane, wave)
+            // takes the child's a = a0 + lane and b = b0 + 4 u + w, its
+            // row's place one load per lane and the columns' places through
+            // LDS (pcs). Every load is unconditional (indices clamped to
+            // the block, so they all go out together), and each child's 16
+            // additions read their LDS elements first and then write them
+            // (the block's places are distinct). The children's entries are
+            // added in the order nd_extend2 adds them (the lower level first,
+            // then slot 0): F + U_first + U_second, the same roundings, the
+            // same bits.
+            struct Blk {
+                const T* U;
+                const int32_t* rc;
+                int ld, a0, ra, b0, rbn;
+            } bk[2];
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
+            for (int h = 0; h < 2; ++h) {
+                const int c = h == nd.pull_swap ? nd.kid0 : nd.kid1;
+                bk[h].ra = 0;
+                if (c < 0) continue;
+                const NdDev& cd = nodes[c];
+                const int32_t* const tbc = tb + cd.tb_off;
+                bk[h].U = F + cd.foff + (int64_t)cd.np_pad * cd.ld + cd.np_pad;  // U[a][b] at U[b ld + a]
+                bk[h].rc = ri + cd.st_off;
+                bk[h].ld = cd.ld;
+                bk[h].a0 = tbc[I];
+                bk[h].ra = tbc[I + 1] - bk[h].a0;
+                bk[h].b0 = tbc[K];
+                bk[h].rbn = tbc[K + 1] - bk[h].b0;
+                if (bk[h].rbn <= 0) bk[h].ra = 0;
+            }
+            T v[16];
+            int pr[2] = {0, 0};
+            // the rows' places (per lane) and the columns' (into pcs, read
+            // back wave-uniform) of both children
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                acc[cb][q] = Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q];
-        // left-looking products, software-pipelined: the loads of block
-        // column J + 1 are in flight during column J's MFMAs
+            for (int h = 0; h < 2; ++h)
+                if (bk[h].ra > 0) {
+                    pr[h] = bk[h].rc[bk[h].a0 + min(lane, bk[h].ra - 1)] - 64 * I;
+                    if (tid < 64) pcs[h][tid] = bk[h].rc[bk[h].b0 + min(tid, bk[h].rbn - 1)] - 64 * K;
+                }
+            auto issue = [&](const Blk& k) {
+                const int a = k.a0 + min(lane, k.ra - 1);
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = k.U[(int64_t)(k.b0 + min(4 * u + w, k.rbn - 1)) * k.ld + a];
+            };
+            auto add = [&](const Blk& k, int h) {
+                T cur[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) cur[u] = PT[pr[h]][pcs[h][4 * u + w]];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int bl = 4 * u + w;
+                    if (lane < k.ra && bl < k.rbn && k.a0 + lane >= k.b0 + bl) PT[pr[h]][pcs[h][bl]] = cur[u] + v[u];
+                }
+            };
+            {
+                T fv[16];  // the tile by columns: element (lane, 4 u + w)
+#pragma unroll
+                for (int u = 0; u < 16; ++u) fv[u] = Fn[(int64_t)(64 * K + 4 * u + w) * ld + 64 * I + lane];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) PT[lane][4 * u + w] = fv[u];
+            }
+            if (bk[0].ra > 0) issue(bk[0]);
+            long long ps = 0;
+            auto pstamp = [&](int i) {
+                if (STAMPS) {
+                    const long long c = (long long)clock64();
+                    c_pl[i] += c - ps;
+                    ps = c;
+                }
+            };
+            if (STAMPS) ps = c0, ++n_pull;
+            __syncthreads();  // the staged tile
+            pstamp(0);
+            if (bk[0].ra > 0) add(bk[0], 0);
+            pstamp(1);
+            if (bk[1].ra > 0) {
+                issue(bk[1]);
+                __syncthreads();  // the first child's additions
+                add(bk[1], 1);
+            }
+            pstamp(2);
+            __syncthreads();
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[cb][q] = PT[rb + 4 * q][16 * cb + cm];
+            __syncthreads();  // PT is the products' staging next
+            pstamp(3);
+        } else {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[cb][q] = Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q];
+        }
         // left-looking products (two workgroups per CU: __launch_bounds__
         // (256, 2) keeps the VGPRs at 128; at 136 the occupancy query gave one
         // and the C5 factor took 8.5 instead of 5.7 ms)
         const int Jn = K < npt ? K : npt;
-        long long c0 = STAMPS ? (long long)clock64() : 0;
         for (int J = 0; J < Jn; ++J) {
             const long long cw = STAMPS ? (long long)clock64() : 0;
             wait_flag(&fl[I * npt + J]);
@@ -287,9 +392,10 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
     }
     if (STAMPS && tid == 0) {
         c_total = (long long)clock64() - c_start;
-        const long long v[12] = {c_total, c_wait, c_prod, c_diag, c_trsm, c_upd, c_drain, n_tiles, n_prod, n_diag,
-                                 n_trsm, n_upd};
-        for (int i = 0; i < 12; ++i) atomicAdd(&stamps[i], (unsigned long long)v[i]);
+        const long long v[ND_NSTAMP] = {c_total, c_wait, c_prod,  c_diag,  c_trsm,  c_upd,  c_drain, n_tiles,
+                                        n_prod,  n_diag, n_trsm,  n_upd,   c_pl[0], c_pl[1], c_pl[2], c_pl[3],
+                                        n_pull,  0};
+        for (int i = 0; i < ND_NSTAMP; ++i) atomicAdd(&stamps[i], (unsigned long long)v[i]);
     }
 }
 
@@ -795,6 +901,7 @@ inline unsigned nd_blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b)
 struct NdLayout {
     std::vector<NdDev> dev;
     std::vector<int32_t> st, ri, pinv, owner, lvl_nodes;
+    std::vector<int32_t> tb;   // per child: its rows' bounds per tile row of the parent (NdDev::tb_off)
     std::vector<int4> tiles;   // nd_factor's tasks: tiles of the tiled fronts, then the small fronts whole
     std::vector<int4> ztiles;  // every front's lower tiles (nd_zero_tiles)
     std::vector<int2> ext;
@@ -812,10 +919,13 @@ struct NdLayout {
 // rows are one whole-front task of nd_factor (0: every front by tiles); bit
 // 16: the per-slot extend lists too (BSM_ND_EXT_MERGE=0's A/B path; ~1M
 // entries at C5 that the default merged launches never read); bits 17-27:
-// the lag of the tiles below a diagonal, in fronts (0: none)
+// the lag of the tiles below a diagonal, in fronts (0: none); bit 28: the
+// extend-add by nd_extend2 / nd_extend launches (BSM_ND_PULL=0) instead of
+// inside nd_factor's tile loads (the extend task lists are only built then)
 void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
     const int32_t small_nt = lay & 0xffff;
     const bool per_slot = (lay >> 16) & 1;
+    const bool push = (lay >> 28) & 1;
     const int32_t nn = (int32_t)P.nodes.size();
     L.dev.resize((size_t)nn);
     int64_t st_total = 0;
@@ -832,6 +942,9 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         d.parent = x.parent;
         d.kid0 = x.kids[0];
         d.kid1 = x.kids[1];
+        d.tb_off = -1;
+        d.pull_swap = x.kids[0] >= 0 && x.kids[1] >= 0 &&
+                      P.nodes[(size_t)x.kids[1]].level < P.nodes[(size_t)x.kids[0]].level;
         d.pad = 0;
         d.foff = L.f_elems;
         L.f_elems += (int64_t)d.ld * d.ld;
@@ -844,6 +957,13 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         d.st_off = st_total;
         st_total += d.m;
     }
+    int64_t tb_total = 0;  // a child's bounds: its parent's nt + 1 (parents follow their children)
+    for (int32_t i = 0; i < nn; ++i)
+        if (L.dev[(size_t)i].parent >= 0) {
+            L.dev[(size_t)i].tb_off = (int32_t)tb_total;
+            tb_total += L.dev[(size_t)L.dev[(size_t)i].parent].nt + 1;
+        }
+    L.tb.resize((size_t)tb_total);
     L.st.resize((size_t)st_total);
     L.ri.resize((size_t)st_total);
     L.pinv.resize((size_t)P.n);
@@ -873,6 +993,12 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
                     L.ri[(size_t)(d.st_off + a)] = pd.np_pad + (int32_t)j;
                 }
             }
+            const int32_t* r = L.ri.data() + d.st_off;
+            int32_t* t = L.tb.data() + d.tb_off;
+            for (int32_t u = 0, a = 0; u <= pd.nt; ++u) {
+                while (a < d.m && r[a] < 64 * u) ++a;
+                t[u] = a;
+            }
         }
     };
     {
@@ -891,7 +1017,7 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
             zt += (size_t)d.nt * (d.nt + 1) / 2;
             ft += (size_t)d.nt;
             bt += (size_t)d.npt;
-            ex += d.parent >= 0 ? (size_t)d.m : 0;
+            ex += d.parent >= 0 && push ? (size_t)d.m : 0;
         }
         L.ztiles.reserve(zt);
         L.tiles.reserve(zt);
@@ -947,7 +1073,7 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         }
         for (int32_t i : lv)
             if (small(i)) o.tiles.push_back(make_int4(i, 0, 0, 1));
-        for (int s = 0; s < 2 && per_slot; ++s)
+        for (int s = 0; s < 2 && per_slot && push; ++s)
             for (int32_t i : lv) {
                 const NdNode& x = P.nodes[(size_t)i];
                 if (x.parent < 0 || x.slot != s) continue;
@@ -961,7 +1087,7 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         for (int32_t d = 0; d < pmax; ++d)
             for (int32_t i : lv)
                 if (d < L.dev[(size_t)i].npt) o.bt.push_back(make_int2(i, L.dev[(size_t)i].npt - 1 - d));
-        if (lv.empty()) return;
+        if (lv.empty() || !push) return;
         // both slots in one launch: a slot-0 child's columns, each paired with
         // the slot-1 sibling's column landing on the same parent column when
         // that sibling is on this level too, then the sibling's unpaired ones
@@ -1042,7 +1168,7 @@ struct NdCached {
     std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off, ftask_off, btask_off;
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
-           o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0;
+           o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0, o_tb = 0;
     size_t n_tiles = 0, n_ztiles = 0, n_ext = 0;
     int32_t small_nt = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
@@ -1210,9 +1336,12 @@ size_t nd_plan_bytes_bound(const NdPlan& P, int32_t lay) {
         bt += (size_t)npt;
     }
     const size_t nn = P.nodes.size(), n = (size_t)P.n;
+    const bool push = (lay >> 28) & 1;
+    // the children's tile bounds: at most two children of nt + 1 per node
     return al(nn * sizeof(NdDev)) + 2 * al(sm * 4) + 2 * al(n * 4) + al(nn * 4) + al(zt * sizeof(int4)) +
-           al(((lay >> 16) & 1) ? sm * sizeof(int2) : 0) + al(sm * sizeof(int4)) + al(ft * sizeof(int2)) +
-           al(bt * sizeof(int2)) + al(n * 8) + al(zt * sizeof(int4));
+           al(push && ((lay >> 16) & 1) ? sm * sizeof(int2) : 0) + al(push ? sm * sizeof(int4) : 0) +
+           al(ft * sizeof(int2)) + al(bt * sizeof(int2)) + al(n * 8) + al(zt * sizeof(int4)) +
+           al(2 * (ft + nn) * 4);
 }
 
 // es > 0: the fronts (es-byte values) are allocated into C.fr on a helper
@@ -1329,7 +1458,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     C.o_btask = C.o_ftask + al(L.ftasks.size() * sizeof(int2));
     C.o_perm = C.o_btask + al(L.btasks.size() * sizeof(int2));
     C.o_ztiles = C.o_perm + al((size_t)N * 8);
-    const size_t total = C.o_ztiles + al(L.ztiles.size() * sizeof(int4));
+    C.o_tb = C.o_ztiles + al(L.ztiles.size() * sizeof(int4));
+    const size_t total = C.o_tb + al(L.tb.size() * 4);
     if (pre.joinable()) pre.join();  // the plan's buffers (device, page-locked staging)
     const auto tp0 = host_now();
     char* hp = nullptr;
@@ -1359,6 +1489,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     put(C.o_btask, L.btasks.data(), L.btasks.size() * sizeof(int2));
     put(C.o_perm, P.perm.data(), (size_t)N * 8);
     put(C.o_ztiles, L.ztiles.data(), L.ztiles.size() * sizeof(int4));
+    put(C.o_tb, L.tb.data(), L.tb.size() * 4);
     {
         std::atomic<size_t> next{0};
         auto copy = [&] {
@@ -1544,7 +1675,13 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     // first, the round-5 order)
     const char* lge = getenv("BSM_ND_LAG");
     const int32_t lag_units = std::min(0x7ff, std::max(0, lge ? atoi(lge) : 512));
-    const int32_t small_nt = (fne ? atoi(fne) : 0) | (ext_merge ? 0 : 1 << 16) | (lag_units << 17);
+    // BSM_ND_PULL=0: the children's update blocks added by nd_extend2 /
+    // nd_extend launches after each level (round 5) instead of inside the
+    // parent's nd_factor tiles (same bits)
+    const char* pue = getenv("BSM_ND_PULL");
+    const bool pull = !(pue && atoi(pue) == 0);
+    const int32_t small_nt =
+        (fne ? atoi(fne) : 0) | (ext_merge ? 0 : 1 << 16) | (lag_units << 17) | (pull ? 0 : 1 << 28);
     std::shared_ptr<NdCached> pc;
     if (cache) {
         std::lock_guard<std::mutex> lk(a->plan_mu);
@@ -1593,6 +1730,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int2* d_ftask = (const int2*)(pb + C.o_ftask);
     const int2* d_btask = (const int2*)(pb + C.o_btask);
     const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
+    const int32_t* d_tb = pull ? (const int32_t*)(pb + C.o_tb) : nullptr;
     // numeric storage: the plan's own buffers when this solve may hold them
     const char* ke = getenv("BSM_ND_KEEP");
     std::unique_lock<std::mutex> num_lock(C.num_mu, std::defer_lock);
@@ -1656,8 +1794,8 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const char* sde = getenv("BSM_ND_STAMPS");
     DBuf stamps;
     if (sde && atoi(sde) == 1) {
-        BSM_TRY(stamps.alloc((size_t)C.n_levels * 12 * sizeof(unsigned long long)));
-        BSM_HIP_TRY(hipMemsetAsync(stamps.p, 0, (size_t)C.n_levels * 12 * sizeof(unsigned long long), s));
+        BSM_TRY(stamps.alloc((size_t)C.n_levels * ND_NSTAMP * sizeof(unsigned long long)));
+        BSM_HIP_TRY(hipMemsetAsync(stamps.p, 0, (size_t)C.n_levels * ND_NSTAMP * sizeof(unsigned long long), s));
     }
     // BSM_ND_PAD_SKIP=0: diagonal tiles factor their padding panels too (A/B; same bits)
     const char* pse = getenv("BSM_ND_PAD_SKIP");
@@ -1668,21 +1806,21 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             const int64_t grid = std::min<int64_t>(nt, (int64_t)cus * per_cu);
             if (stamps.p)
                 nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                                  d_tickets + lv, d_status, pad_skip,
-                                                                  stamps.as<unsigned long long>() + 12 * lv);
+                                                                  d_tickets + lv, d_status, pad_skip, d_tb, d_ri,
+                                                                  stamps.as<unsigned long long>() + ND_NSTAMP * lv);
             else
                 nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                            d_tickets + lv, d_status, pad_skip);
+                                                            d_tickets + lv, d_status, pad_skip, d_tb, d_ri);
             BSM_HIP_TRY(hipGetLastError());
         }
-        if (ext_merge) {
+        if (ext_merge && !pull) {
             const int64_t e0 = C.ext2_off[(size_t)lv], ne = C.ext2_off[(size_t)lv + 1] - e0;
             if (ne > 0) {
                 nd_extend2<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext2 + e0, ne, d_ri, F);
                 BSM_HIP_TRY(hipGetLastError());
             }
         }
-        for (int sl = 0; sl < 2 && !ext_merge; ++sl) {
+        for (int sl = 0; sl < 2 && !ext_merge && !pull; ++sl) {
             const int64_t e0 = C.ext_off[(size_t)(2 * lv + sl)], ne = C.ext_off[(size_t)(2 * lv + sl) + 1] - e0;
             if (ne <= 0) continue;
             nd_extend<T><<<nd_blocks(ne, 4), 256, 0, s>>>(d_nodes, d_ext + e0, ne, d_ri, F);
@@ -1752,10 +1890,10 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     drain.armed = false;
     stage_mark("nd_copy_out", s);
     if (stamps.p) {
-        std::vector<unsigned long long> h((size_t)C.n_levels * 12);
+        std::vector<unsigned long long> h((size_t)C.n_levels * ND_NSTAMP);
         BSM_HIP_TRY(hipMemcpy(h.data(), stamps.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         for (int32_t lv = 0; lv < C.n_levels; ++lv) {
-            const unsigned long long* v = &h[(size_t)lv * 12];
+            const unsigned long long* v = &h[(size_t)lv * ND_NSTAMP];
             const double nt = v[7] ? (double)v[7] : 1.0;
             fprintf(stderr,
                     "[bsm nd stamps] level %2d: %6llu tiles (prod %llu, diag %llu, trsm %llu, upd %llu); cycles per "
@@ -1763,6 +1901,12 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
                     "%.0f per tile\n",
                     lv, v[7], v[8], v[9], v[10], v[11], v[1] / nt, (v[2] - v[1]) / nt, v[3] / nt, v[4] / nt,
                     v[5] / nt, v[6] / nt, v[0] / nt);
+            if (v[16])
+                fprintf(stderr,
+                        "[bsm nd stamps] level %2d: pull into %llu tiles, cycles per pulling tile: tile and first "
+                        "child's loads %.0f, its additions %.0f, second child %.0f, read-back %.0f\n",
+                        lv, v[16], (double)v[12] / v[16], (double)v[13] / v[16], (double)v[14] / v[16],
+                        (double)v[15] / v[16]);
         }
     }
     BSM_REQUIRE(!(h & ST_TIMEOUT), BSM_ERR_HIP, "nd factor: tile hand-off timed out");

@@ -31,7 +31,9 @@ def kernel_ns(path, dtype):
             for short in ("nd_factor", "nd_forward_tiles", "nd_forward", "nd_backward_tiles", "nd_backward",
                           "nd_zero_tiles", "nd_assemble", "nd_extend2", "nd_extend", "nd_pad_pivots", "nd_gather",
                           "nd_scatter", "nd_pattern_hash", "nd_pattern_diff"):
-                if f"{short}<{dtype}>" in name or (short.startswith("nd_pattern") and f"{short}(" in name):
+                # nd_factor<double, false>: the product instantiation (STAMPS off)
+                if (f"{short}<{dtype}>" in name or f"{short}<{dtype}, false>" in name
+                        or (short.startswith("nd_pattern") and f"{short}(" in name)):
                     out[short] = out.get(short, 0) + int(row["TotalDurationNs"])
                     out[short + ":calls"] = out.get(short + ":calls", 0) + int(row["Calls"])
                     break

@@ -279,7 +279,7 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
-                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG"])
+                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -306,7 +306,11 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
     * BSM_ND_LAG (512 by default; 1 here, as this size's levels have fewer
       fronts): a front's tiles below the diagonal taken right after the next
       front's diagonal tile instead of after the column's last one: the same
-      tiles, only their tickets' order changes.
+      tiles, only their tickets' order changes;
+    * BSM_ND_PULL: the children's update blocks added inside the parent's
+      nd_factor tiles (staged in LDS, the lower-level child first, then
+      slot 0) instead of by nd_extend2 launches after each level: the same
+      adds in the same order.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
