@@ -47,8 +47,13 @@ struct NdDev {
     int32_t ld, np, np_pad, m, npt, nt, parent, kid0, kid1;
     int32_t tb_off;     // (child) nt + 1 bounds of the parent's tile rows in ri: tb[t] = first a, ri[a] >= 64 t
     int32_t pull_swap;  // (parent) kid1's update block is added before kid0's (kid1 on a lower level)
-    int32_t pad;
+    int32_t tile_off;   // the front's lower tiles' index base (nd_lower_idx) in the plan's per-tile flags
 };
+
+// (I, K), I >= K, among a front's nt (nt + 1) / 2 lower tiles, column by column
+__host__ __device__ inline int64_t nd_lower_idx(int32_t nt, int32_t I, int32_t K) {
+    return (int64_t)K * nt - (int64_t)K * (K - 1) / 2 + (I - K);
+}
 
 __device__ __forceinline__ int32_t lower_bound_i32(const int32_t* a, int32_t len, int64_t x) {
     int32_t lo = 0, hi = len;
@@ -83,13 +88,49 @@ __global__ __launch_bounds__(256) void nd_assemble(int64_t n, const int64_t* __r
     }
 }
 
+// The tiles A's entries land in (once per plan, from the pattern, with
+// nd_assemble's addressing): zf[tile_off + nd_lower_idx] = 1. The others
+// start from zero without being zeroed or read (the pulled extend-add: no
+// kernel writes them before their factor tile).
+__global__ __launch_bounds__(256) void nd_mark_tiles(int64_t n, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ col, const int32_t* __restrict__ pinv,
+                                                     const int32_t* __restrict__ owner,
+                                                     const NdDev* __restrict__ nodes, const int32_t* __restrict__ st,
+                                                     uint8_t* __restrict__ zf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t pi = pinv[i];
+    for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+        const int64_t j = col[e];
+        if (j > i) continue;
+        const int64_t pj = pinv[j];
+        const int64_t r = pi > pj ? pi : pj, c = pi > pj ? pj : pi;
+        const NdDev& nd = nodes[owner[c]];
+        const int64_t lc = c - nd.start;
+        const int64_t lr = r < nd.start + nd.np ? r - nd.start : nd.np_pad + lower_bound_i32(st + nd.st_off, nd.m, r);
+        zf[nd.tile_off + nd_lower_idx(nd.nt, (int32_t)(lr >> 6), (int32_t)(lc >> 6))] = 1;
+    }
+}
+// the factor's tasks of unmarked tiles: .w |= 2 (a whole-front task keeps its tiles' loads)
+__global__ __launch_bounds__(256) void nd_mark_tasks(int64_t ntasks, const NdDev* __restrict__ nodes,
+                                                     const uint8_t* __restrict__ zf, int4* __restrict__ tiles) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntasks) return;
+    const int4 tl = tiles[t];
+    if (tl.w != 0) return;
+    const NdDev& nd = nodes[tl.x];
+    if (!zf[nd.tile_off + nd_lower_idx(nd.nt, tl.y, tl.z)]) tiles[t].w = 2;
+}
+
 // zero the fronts' lower tiles (the only ones any kernel reads: every tile
-// of the factor's lists): 55 % of the bytes a memset of the whole squares writes
+// of the factor's lists): 55 % of the bytes a memset of the whole squares
+// writes; with zf, only the tiles A's entries land in (nd_mark_tiles)
 template <typename T>
 __global__ __launch_bounds__(256) void nd_zero_tiles(const NdDev* __restrict__ nodes, const int4* __restrict__ tiles,
-                                                     T* __restrict__ F) {
+                                                     T* __restrict__ F, const uint8_t* __restrict__ zf) {
     const int4 tl = tiles[blockIdx.x];
     const NdDev& nd = nodes[tl.x];
+    if (zf && !zf[nd.tile_off + nd_lower_idx(nd.nt, tl.y, tl.z)]) return;
     T* const t0 = F + nd.foff + (int64_t)64 * tl.z * nd.ld + 64 * tl.y;
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -132,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                                                  int* __restrict__ flags, int* __restrict__ ticket,
                                                  int* __restrict__ status, int pad_skip,
                                                  const int32_t* __restrict__ tb, const int32_t* __restrict__ ri,
-                                                 unsigned long long* __restrict__ stamps = nullptr) {
+                                                 int zskip, unsigned long long* __restrict__ stamps = nullptr) {
     long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
     long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
     long long c_pl[4] = {0, 0, 0, 0}, n_pull = 0;  // the pull's phases: tile + first child's loads, its adds, second, read-back
@@ -167,6 +208,9 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
       const int4 tl = tiles[t];
       const NdDev& nd = nodes[tl.x];
       const bool whole = tl.w == 1;
+      // zskip: a tile no A entry lands in starts from zero (tl.w == 2,
+      // nd_mark_tasks): it was neither zeroed nor written, and is not read
+      const bool fz = zskip && tl.w == 2;
       const int npt = nd.npt, ntf = nd.nt;
       const int cnt = whole ? ntf * (ntf + 1) / 2 : 1;
       int I = whole ? 0 : tl.y, K = whole ? 0 : tl.z;
@@ -256,7 +300,10 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             {
                 T fv[16];  // the tile by columns: element (lane, 4 u + w)
 #pragma unroll
-                for (int u = 0; u < 16; ++u) fv[u] = Fn[(int64_t)(64 * K + 4 * u + w) * ld + 64 * I + lane];
+                for (int u = 0; u < 16; ++u) fv[u] = (T)0;
+                if (!fz)
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) fv[u] = Fn[(int64_t)(64 * K + 4 * u + w) * ld + 64 * I + lane];
 #pragma unroll
                 for (int u = 0; u < 16; ++u) PT[lane][4 * u + w] = fv[u];
             }
@@ -287,6 +334,11 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                 for (int q = 0; q < 4; ++q) acc[cb][q] = PT[rb + 4 * q][16 * cb + cm];
             __syncthreads();  // PT is the products' staging next
             pstamp(3);
+        } else if (fz) {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[cb][q] = (T)0;
         } else {
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
@@ -912,7 +964,7 @@ struct NdLayout {
     std::vector<int64_t> ftask_off;                     // per level
     std::vector<int2> btasks;                           // nd_backward_tiles' (node, pivot tile), last tiles first
     std::vector<int64_t> btask_off;                     // per level
-    int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0;
+    int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, n_lower = 0;
 };
 
 // lay: the layout's options. Bits 0-15: fronts of at most this many tile
@@ -943,9 +995,10 @@ void nd_layout(const NdPlan& P, int32_t lay, NdLayout& L) {
         d.kid0 = x.kids[0];
         d.kid1 = x.kids[1];
         d.tb_off = -1;
+        d.tile_off = (int32_t)L.n_lower;
+        L.n_lower += (int64_t)d.nt * (d.nt + 1) / 2;
         d.pull_swap = x.kids[0] >= 0 && x.kids[1] >= 0 &&
                       P.nodes[(size_t)x.kids[1]].level < P.nodes[(size_t)x.kids[0]].level;
-        d.pad = 0;
         d.foff = L.f_elems;
         L.f_elems += (int64_t)d.ld * d.ld;
         d.dinv_off = L.dinv_elems;
@@ -1168,7 +1221,7 @@ struct NdCached {
     std::vector<int64_t> tiles_off, lvl_off, ext_off, ext2_off, ftask_off, btask_off;
     int64_t f_elems = 0, dinv_elems = 0, n_flags = 0, vtot = 0, max_front = 0;
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
-           o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0, o_tb = 0;
+           o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0, o_tb = 0, o_zf = 0;
     size_t n_tiles = 0, n_ztiles = 0, n_ext = 0;
     int32_t small_nt = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
@@ -1341,7 +1394,7 @@ size_t nd_plan_bytes_bound(const NdPlan& P, int32_t lay) {
     return al(nn * sizeof(NdDev)) + 2 * al(sm * 4) + 2 * al(n * 4) + al(nn * 4) + al(zt * sizeof(int4)) +
            al(push && ((lay >> 16) & 1) ? sm * sizeof(int2) : 0) + al(push ? sm * sizeof(int4) : 0) +
            al(ft * sizeof(int2)) + al(bt * sizeof(int2)) + al(n * 8) + al(zt * sizeof(int4)) +
-           al(2 * (ft + nn) * 4);
+           al(2 * (ft + nn) * 4) + al(zt);
 }
 
 // es > 0: the fronts (es-byte values) are allocated into C.fr on a helper
@@ -1401,11 +1454,17 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             f_elems += ld * ld;
         }
         const int dev = a->device;
-        // ... and zeroed there on a stream of its own: a fresh allocation's
-        // first touch costs ~10 ms at C5 (5.2 GB), which then runs beside the
-        // host's layout and packing instead of inside the solve's first kernel
-        pre_fronts = std::thread([&C, f_elems, es, dev] {
+        // BSM_ND_PREZERO=1: also zeroed whole there, on a stream of its own
+        // (round 6 before the marked tiles: a fresh allocation's first touch
+        // cost ~10 ms at C5 inside the solve's first kernel). Off by default:
+        // with the layout at ~6 ms the solve waited ~7 ms for that memset,
+        // while zeroing only the marked tiles in the solve takes ~3 ms
+        // (profiles/r06_m_*)
+        const char* pze = getenv("BSM_ND_PREZERO");
+        const bool prezero = pze && atoi(pze) == 1;
+        pre_fronts = std::thread([&C, f_elems, es, dev, prezero] {
             if (hipSetDevice(dev) != hipSuccess || C.fr.alloc((size_t)f_elems * es) != BSM_OK) return;
+            if (!prezero) return;
             hipStream_t z = nullptr;
             hipEvent_t ev = nullptr;
             if (hipStreamCreateWithFlags(&z, hipStreamNonBlocking) != hipSuccess) return;
@@ -1459,7 +1518,8 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     C.o_perm = C.o_btask + al(L.btasks.size() * sizeof(int2));
     C.o_ztiles = C.o_perm + al((size_t)N * 8);
     C.o_tb = C.o_ztiles + al(L.ztiles.size() * sizeof(int4));
-    const size_t total = C.o_tb + al(L.tb.size() * 4);
+    C.o_zf = C.o_tb + al(L.tb.size() * 4);
+    const size_t total = C.o_zf + al((size_t)L.n_lower);
     if (pre.joinable()) pre.join();  // the plan's buffers (device, page-locked staging)
     const auto tp0 = host_now();
     char* hp = nullptr;
@@ -1500,9 +1560,35 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         copy();
         for (auto& th : pool) th.join();
     }
+    // the per-tile marks: the pivot columns' diagonal tiles (their padding
+    // pivots' identity, nd_pad_pivots), then nd_mark_tiles on the device
+    memset(hp + C.o_zf, 0, (size_t)L.n_lower);
+    // (and every tile of a whole-front task: nd_factor reads those tiles as
+    // they are)
+    for (const NdDev& d : L.dev) {
+        if (d.nt <= (small_nt & 0xffff)) {
+            memset(hp + C.o_zf + d.tile_off, 1, (size_t)d.nt * (d.nt + 1) / 2);
+            continue;
+        }
+        for (int32_t K = 0; K < d.npt; ++K) hp[C.o_zf + d.tile_off + nd_lower_idx(d.nt, K, K)] = 1;
+    }
     C.ms_pack = ms_since(tp0);
     if (C.plan.bytes < total) BSM_TRY(C.plan.alloc(total));
     BSM_HIP_TRY(hipMemcpyAsync(C.plan.p, hp, total, hipMemcpyHostToDevice, s));
+    {
+        char* pb = C.plan.as<char>();
+        uint8_t* zf = (uint8_t*)(pb + C.o_zf);
+        nd_mark_tiles<<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, (const int32_t*)(pb + C.o_pinv),
+                                                        (const int32_t*)(pb + C.o_owner), (const NdDev*)(pb + C.o_dev),
+                                                        (const int32_t*)(pb + C.o_st), zf);
+        BSM_HIP_TRY(hipGetLastError());
+        if (C.n_tiles) {
+            nd_mark_tasks<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>((int64_t)C.n_tiles,
+                                                                             (const NdDev*)(pb + C.o_dev), zf,
+                                                                             (int4*)(pb + C.o_tiles));
+            BSM_HIP_TRY(hipGetLastError());
+        }
+    }
     BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
     stage_mark("nd_upload", s);
     if (pre_fronts.joinable()) {  // the fronts' allocation: the wait for it as a stage of its own
@@ -1731,6 +1817,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const int2* d_btask = (const int2*)(pb + C.o_btask);
     const int64_t* d_perm = (const int64_t*)(pb + C.o_perm);
     const int32_t* d_tb = pull ? (const int32_t*)(pb + C.o_tb) : nullptr;
+    // BSM_ND_ZSKIP=0: every lower tile zeroed and read (A/B; same bits). By
+    // default, with the pulled extend-add, only the tiles A's entries land in
+    const char* zse = getenv("BSM_ND_ZSKIP");
+    const int zskip = pull && !(zse && atoi(zse) == 0);
+    const uint8_t* d_zf = zskip ? (const uint8_t*)(pb + C.o_zf) : nullptr;
     // numeric storage: the plan's own buffers when this solve may hold them
     const char* ke = getenv("BSM_ND_KEEP");
     std::unique_lock<std::mutex> num_lock(C.num_mu, std::defer_lock);
@@ -1745,6 +1836,12 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const void* fr_was = fr.p;
     BSM_TRY(nd_alloc_numeric(fr, fr_b, &C));
     if (keep && fr.p != fr_was) C.drop_zeroed();  // reallocated: zeroed by nd_zero_tiles as usual
+    const char* poe = getenv("BSM_ND_POISON");  // tests: the fronts start as NaN (nothing may read unzeroed tiles)
+    if (poe && atoi(poe) == 1) {
+        if (C.fr_zeroed) hipStreamWaitEvent(s, C.fr_zeroed, 0);
+        C.drop_zeroed();
+        BSM_HIP_TRY(hipMemsetAsync(fr.p, 0xff, fr_b, s));
+    }
     BSM_TRY(nd_alloc_numeric(dv, dv_b, &C));
     BSM_TRY(nd_alloc_numeric(fl, nfl * sizeof(int), &C));
     if (keep) C.kept_bytes = fr.bytes + dv.bytes + fl.bytes;
@@ -1781,7 +1878,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         (void)hipEventDestroy(ev);
         BSM_HIP_TRY(we);
     } else if (C.n_ztiles) {
-        nd_zero_tiles<T><<<(unsigned)C.n_ztiles, 256, 0, s>>>(d_nodes, d_ztiles, F);
+        nd_zero_tiles<T><<<(unsigned)C.n_ztiles, 256, 0, s>>>(d_nodes, d_ztiles, F, d_zf);
         BSM_HIP_TRY(hipGetLastError());
     }
     nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals), d_pinv,
@@ -1807,10 +1904,10 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             if (stamps.p)
                 nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                                   d_tickets + lv, d_status, pad_skip, d_tb, d_ri,
-                                                                  stamps.as<unsigned long long>() + ND_NSTAMP * lv);
+                                                                  zskip, stamps.as<unsigned long long>() + ND_NSTAMP * lv);
             else
                 nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                            d_tickets + lv, d_status, pad_skip, d_tb, d_ri);
+                                                            d_tickets + lv, d_status, pad_skip, d_tb, d_ri, zskip);
             BSM_HIP_TRY(hipGetLastError());
         }
         if (ext_merge && !pull) {

@@ -279,7 +279,7 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
-                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL"])
+                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL", "BSM_ND_ZSKIP"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -310,7 +310,10 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
     * BSM_ND_PULL: the children's update blocks added inside the parent's
       nd_factor tiles (staged in LDS, the lower-level child first, then
       slot 0) instead of by nd_extend2 launches after each level: the same
-      adds in the same order.
+      adds in the same order;
+    * BSM_ND_ZSKIP: the tiles no entry of A lands in start from zero in
+      the factor, neither zeroed before nor read, instead of zeroed and
+      read: the same values.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
@@ -329,6 +332,34 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
     for j in range(2):
         a0, a1 = np.asarray(x_skip.get_col(j)), np.asarray(x_full.get_col(j))
         assert np.array_equal(a0.view(np.uint8), a1.view(np.uint8)), j
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("leaf", ["8", "100", "192"])
+def test_nd_poisoned_fronts_same_bits(orc, monkeypatch, dtype, leaf):
+    """With the fronts filled with NaN before the solve (BSM_ND_POISON=1),
+    the default path (only the tiles A's entries land in zeroed; the others
+    start from zero in the factor and are never read) gives the bits of the
+    path that zeroes and reads every tile: nothing reads a tile it did not
+    zero or write."""
+    monkeypatch.setenv("BSM_ND_LEAF", leaf)
+    g = 90
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    v = v.astype(dtype)
+    b = orc.gen_x_cols(1021, n, 2, dtype=dtype)
+    monkeypatch.setenv("BSM_ND_POISON", "1")
+    a = Csr.from_csr_arrays((n, n), rp, ci, v)
+    x_p = solve(a, Dense.from_columns(b), order="nd")
+    x_p2 = solve(a, Dense.from_columns(b), order="nd")  # the kept fronts, poisoned again
+    monkeypatch.setenv("BSM_ND_POISON", "0")
+    monkeypatch.setenv("BSM_ND_ZSKIP", "0")
+    x_z = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
+    for j in range(2):
+        a0, a1, a2 = (np.asarray(x.get_col(j)) for x in (x_p, x_p2, x_z))
+        assert np.all(np.isfinite(a0))
+        assert np.array_equal(a0.view(np.uint8), a2.view(np.uint8)), j
+        assert np.array_equal(a1.view(np.uint8), a2.view(np.uint8)), j
 
 
 def poisson3d(g):
