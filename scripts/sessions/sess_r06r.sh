@@ -1,0 +1,12 @@
+# round 6, session r: the host analysis with the child graphs extracted on
+# several threads at the top depths, against the build before it
+# (scripts/perf/nd_order_prev.cpp: the previous commit's nd_order.cpp),
+# alternating, on the box's CPUs; then the C5 nd line
+bash scripts/perf/build_nd_order_time.sh && \
+g++ -O3 -std=c++20 -pthread -Ibasic_sparse_matrix_amd/csrc scripts/perf/nd_order_time.cpp \
+    scripts/perf/nd_order_prev.cpp -o scripts/perf/bin/nd_order_time_prev && \
+bash scripts/gpu_session.sh r06r "env:BSM_ND_TRACE=2" \
+  "cmd:scripts/perf/bin/nd_order_time_prev 1000 192 16" "cmd:scripts/perf/bin/nd_order_time 1000 192 16" \
+  "cmd:scripts/perf/bin/nd_order_time_prev 1000 192 16" "cmd:scripts/perf/bin/nd_order_time 1000 192 16" \
+  "cmd:scripts/perf/bin/nd_order_time_prev 1000 192 16" "cmd:scripts/perf/bin/nd_order_time 1000 192 16" \
+  "unenv:BSM_ND_TRACE" "py:scripts/solve_c5.py --orders nd --reps 3 --no-cpu-baseline"
