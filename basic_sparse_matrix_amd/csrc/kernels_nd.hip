@@ -580,7 +580,12 @@ __global__ __launch_bounds__(256, 4) void nd_forward(const NdDev* __restrict__ n
             st_sc1(&v[64 * K + tid], y);
         }
         __syncthreads();
-        for (int r = 64 * (K + 1) + tid; r < fp; r += 256) {
+        // rows past f and the pivot padding rows are zero in L (and stay
+        // zero in v): skipped whole (the loads inside stay unconditional, so
+        // they go out together)
+        const int f = nd.np_pad + nd.m;
+        for (int r = 64 * (K + 1) + tid; r < f; r += 256) {
+            if (r >= nd.np && r < nd.np_pad) continue;
             // the row's 64 terms in two halves of 32 loads in flight: at 226
             // VGPRs (all 64 at once) two workgroups fit a CU, at <= 128 four
             // (the leaf level is latency bound: 7,699 fronts at C5); same
