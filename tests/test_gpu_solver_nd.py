@@ -362,6 +362,55 @@ def test_nd_poisoned_fronts_same_bits(orc, monkeypatch, dtype, leaf):
         assert np.array_equal(a1.view(np.uint8), a2.view(np.uint8)), j
 
 
+def _irregular_systems(orc, kind):
+    """(n, rp, ci, v) of a random SPD, a block-diagonal (separator-free
+    splits, pivot-free fronts) or a 3-D Laplacian system."""
+    if kind == "random":
+        rng = np.random.default_rng(11)
+        n = 400
+        a = np.zeros((n, n))
+        mask = rng.random((n, n)) < 0.015
+        a[mask] = rng.uniform(-1.0, 1.0, (n, n))[mask]
+        a = np.tril(a, -1)
+        a = a + a.T
+        a[np.arange(n), np.arange(n)] = np.abs(a).sum(axis=1) + 1.0
+        rp, ci, v = csr_arrays(a)
+        return n, rp, ci, v
+    if kind == "blocks":
+        import scipy.sparse as sp
+
+        g = 14
+        rp, ci, v = orc.poisson2d(g)
+        P = sp.csr_matrix((v, ci.astype(np.int64), rp.astype(np.int64)), shape=(g * g, g * g))
+        M = sp.block_diag([P, 2.0 * P, sp.identity(7) * 3.0], format="csr")
+        M.sort_indices()
+        return M.shape[0], M.indptr.astype(np.uint64), M.indices.astype(np.uint64), M.data.astype(np.float64)
+    rp, ci, v = poisson3d(11)
+    return 11 ** 3, rp.astype(np.uint64), ci, v
+
+
+@pytest.mark.parametrize("kind", ["random", "blocks", "poisson3d"])
+@pytest.mark.parametrize("leaf", ["4", "16", "64"])
+def test_nd_poisoned_fronts_irregular_trees(orc, monkeypatch, kind, leaf):
+    """Irregular separator trees (a random graph, disconnected blocks with
+    pivot-free fronts, a 3-D mesh) with the fronts NaN-poisoned: the pulled
+    extend-add and the zero-skip give the bits of the round-5 path (the
+    extend launches, every tile zeroed and read), and x solves the system."""
+    n, rp, ci, v = _irregular_systems(orc, kind)
+    monkeypatch.setenv("BSM_ND_LEAF", leaf)
+    b = orc.gen_x_cols(1031, n, 2)
+    monkeypatch.setenv("BSM_ND_POISON", "1")
+    x_p = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
+    monkeypatch.setenv("BSM_ND_POISON", "0")
+    monkeypatch.setenv("BSM_ND_PULL", "0")
+    x_r = solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd")
+    ex = orc.solve(n, rp, ci, v, b, band=kind == "poisson3d")
+    for j in range(2):
+        a0, a1 = np.asarray(x_p.get_col(j)), np.asarray(x_r.get_col(j))
+        assert np.array_equal(a0.view(np.uint8), a1.view(np.uint8)), j
+        assert rel_err(a0, ex[j]) < 1e-10
+
+
 def poisson3d(g):
     """7-point Laplacian on a g^3 grid (natural order, band g^2), diagonal 6.5."""
     n = g ** 3
