@@ -160,6 +160,13 @@ __global__ __launch_bounds__(64) void nd_pad_pivots(const NdDev* __restrict__ no
 // it waits on nobody: these tasks follow the tiled fronts' tickets and fill
 // the CUs while those fronts' chains run, without a ticket and a flag
 // hand-off through L2 per tile.
+// fV (the forward solve folded in, one right-hand side; BSM_ND_FOLD): the
+// diagonal tile (I, I) also forms w_I = b_I + the children's update-vector
+// entries landing in its rows - sum_{J < min(I, npt)} L_IJ y_J (the L_IJ are
+// the tiles its products stage anyway; y_J is published before the flags
+// its waits follow), then y_I = Linv_I w_I for a pivot tile or the update
+// vector u_I = w_I for a front-row tile, into fV (V's layout: the separate
+// forward's output), so no forward pass reads L again.
 // STAMPS (BSM_ND_STAMPS=1, a diagnostic instantiation: the counters cost
 // SGPRs the product build cannot spare): per workgroup,
 // thread 0's shader-clock cycles in the flag waits, the products (loads,
@@ -173,7 +180,8 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                                                  int* __restrict__ flags, int* __restrict__ ticket,
                                                  int* __restrict__ status, int pad_skip,
                                                  const int32_t* __restrict__ tb, const int32_t* __restrict__ ri,
-                                                 int zskip, unsigned long long* __restrict__ stamps = nullptr) {
+                                                 int zskip, T* __restrict__ fV, const T* __restrict__ fbp,
+                                                 unsigned long long* __restrict__ stamps = nullptr) {
     long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
     long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
     long long c_pl[4] = {0, 0, 0, 0}, n_pull = 0;  // the pull's phases: tile + first child's loads, its adds, second, read-back
@@ -184,6 +192,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
     __shared__ T Di[4 * 256];
     __shared__ T Tb[3 * 256];
     __shared__ int pcs[2][64];  // the pull: a child block's columns' places in the tile
+    __shared__ T fw[64], fyk[64], fpart[4][64];  // the folded forward solve (fV): w, y_J, partial sums
     __shared__ int tk;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -236,6 +245,9 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
         };
         long long c0 = STAMPS ? (long long)clock64() : 0;
         T acc[4][4];
+        // the folded forward solve on this diagonal tile: w = b (pivot rows)
+        const bool fold = fV && I == K;
+        if (fold && tid < 64) fw[tid] = 64 * K + tid < nd.np ? fbp[nd.start + 64 * K + tid] : (T)0;
         if (tb && (nd.kid0 >= 0 || nd.kid1 >= 0)) {
             // The children's update blocks, pulled into this tile (tb: no
             // nd_extend launches): the entries (a, b), a >= b, of child c
@@ -254,6 +266,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             struct Blk {
                 const T* U;
                 const int32_t* rc;
+                const T* u;  // the child's update vector (fold)
                 int ld, a0, ra, b0, rbn;
             } bk[2];
 #pragma unroll
@@ -265,6 +278,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                 const int32_t* const tbc = tb + cd.tb_off;
                 bk[h].U = F + cd.foff + (int64_t)cd.np_pad * cd.ld + cd.np_pad;  // U[a][b] at U[b ld + a]
                 bk[h].rc = ri + cd.st_off;
+                bk[h].u = fV ? fV + cd.voff + cd.np_pad : nullptr;
                 bk[h].ld = cd.ld;
                 bk[h].a0 = tbc[I];
                 bk[h].ra = tbc[I + 1] - bk[h].a0;
@@ -282,10 +296,12 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                     pr[h] = bk[h].rc[bk[h].a0 + min(lane, bk[h].ra - 1)] - 64 * I;
                     if (tid < 64) pcs[h][tid] = bk[h].rc[bk[h].b0 + min(tid, bk[h].rbn - 1)] - 64 * K;
                 }
+            T uv = (T)0;
             auto issue = [&](const Blk& k) {
                 const int a = k.a0 + min(lane, k.ra - 1);
 #pragma unroll
                 for (int u = 0; u < 16; ++u) v[u] = k.U[(int64_t)(k.b0 + min(4 * u + w, k.rbn - 1)) * k.ld + a];
+                if (fold && w == 0) uv = k.u[a];
             };
             auto add = [&](const Blk& k, int h) {
                 T cur[16];
@@ -296,6 +312,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                     const int bl = 4 * u + w;
                     if (lane < k.ra && bl < k.rbn && k.a0 + lane >= k.b0 + bl) PT[pr[h]][pcs[h][bl]] = cur[u] + v[u];
                 }
+                if (fold && w == 0 && lane < k.ra) fw[pr[h]] += uv;
             };
             {
                 T fv[16];  // the tile by columns: element (lane, 4 u + w)
@@ -350,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
         // (256, 2) keeps the VGPRs at 128; at 136 the occupancy query gave one
         // and the C5 factor took 8.5 instead of 5.7 ms)
         const int Jn = K < npt ? K : npt;
+        T fp = (T)0;  // fold: this thread's share of (L_IJ y_J)[lane], terms 16 w .. 16 w + 15
         for (int J = 0; J < Jn; ++J) {
             const long long cw = STAMPS ? (long long)clock64() : 0;
             wait_flag(&fl[I * npt + J]);
@@ -357,6 +375,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             if (STAMPS) c_wait += (long long)clock64() - cw;
             T va[16];
             load(va, I, J);
+            if (fold && tid < 64) fyk[tid] = ld_sc1(&fV[nd.voff + 64 * J + tid]);  // y_J (before (J, J)'s flag)
             store(PT, va);
             if (I != K) {
                 load(va, K, J);
@@ -364,6 +383,16 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             }
             __syncthreads();
             mfma_tile<T, true>(PTl, I != K ? QTl : PTl, acc, w, lane);
+            if (fold) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) fp = fma_t((T)PT[16 * w + t][lane], fyk[16 * w + t], fp);  // PT[t][r] = L[r][t]
+            }
+            __syncthreads();
+        }
+        if (fold) {  // w_I = b + children's entries - sum_J L_IJ y_J
+            fpart[w][lane] = fp;
+            __syncthreads();
+            if (tid < 64) fw[tid] = fw[tid] - ((fpart[0][tid] + fpart[1][tid]) + (fpart[2][tid] + fpart[3][tid]));
             __syncthreads();
         }
         if (STAMPS) {
@@ -391,6 +420,15 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                 st_sc1(&dk[e], (T)QT[q][l]);  // Dinv[q * 64 + l] = Linv[l][q]
                 const int r = e & 63, c = e >> 6;
                 Fn[(int64_t)(64 * K + c) * ld + 64 * K + r] = r >= c ? (T)PT[r][c] : (T)0;
+            }
+            if (fold) {  // y_K = Linv_K w_K (QT[q][l] = Linv[l][q]), published with the tile's flag
+                T y = (T)0;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) y = fma_t((T)QT[16 * w + j][lane], fw[16 * w + j], y);
+                fpart[w][lane] = y;
+                __syncthreads();
+                if (tid < 64)
+                    st_sc1(&fV[nd.voff + 64 * K + tid], (fpart[0][tid] + fpart[1][tid]) + (fpart[2][tid] + fpart[3][tid]));
             }
         } else if (K < npt) {
             wait_flag(&fl[K * npt + K]);
@@ -420,6 +458,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) Fn[(int64_t)(64 * K + 16 * cb + cm) * ld + 64 * I + rb + 4 * q] = acc[cb][q];
+            if (fold && tid < 64) st_sc1(&fV[nd.voff + 64 * K + tid], (T)fw[tid]);  // the update vector u_K
         }
         long long c2 = 0;
         if (STAMPS) {
@@ -1827,6 +1866,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const char* zse = getenv("BSM_ND_ZSKIP");
     const int zskip = pull && !(zse && atoi(zse) == 0);
     const uint8_t* d_zf = zskip ? (const uint8_t*)(pb + C.o_zf) : nullptr;
+    // BSM_ND_FOLD=0: the forward solve as its own pass over L after the
+    // factor. By default, with one right-hand side and the pull, the
+    // factor's diagonal tiles form y and the update vectors themselves
+    const char* foe = getenv("BSM_ND_FOLD");
+    const bool fold = k == 1 && pull && !(foe && atoi(foe) == 0);
     // numeric storage: the plan's own buffers when this solve may hold them
     const char* ke = getenv("BSM_ND_KEEP");
     std::unique_lock<std::mutex> num_lock(C.num_mu, std::defer_lock);
@@ -1899,6 +1943,14 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         BSM_TRY(stamps.alloc((size_t)C.n_levels * ND_NSTAMP * sizeof(unsigned long long)));
         BSM_HIP_TRY(hipMemsetAsync(stamps.p, 0, (size_t)C.n_levels * ND_NSTAMP * sizeof(unsigned long long), s));
     }
+    if (fold) {  // b into the new order before the factor; V's padding rows stay 0
+        nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
+                                                       bpb.as<T>());
+        BSM_HIP_TRY(hipGetLastError());
+        BSM_HIP_TRY(hipMemsetAsync(vb.p, 0, (size_t)std::max<int64_t>(C.vtot, 1) * sizeof(T), s));
+    }
+    T* const fV = fold ? vb.as<T>() : nullptr;
+    const T* const fbp = fold ? bpb.as<T>() : nullptr;
     // BSM_ND_PAD_SKIP=0: diagonal tiles factor their padding panels too (A/B; same bits)
     const char* pse = getenv("BSM_ND_PAD_SKIP");
     const int pad_skip = !(pse && atoi(pse) == 0);
@@ -1909,10 +1961,12 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             if (stamps.p)
                 nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                                   d_tickets + lv, d_status, pad_skip, d_tb, d_ri,
-                                                                  zskip, stamps.as<unsigned long long>() + ND_NSTAMP * lv);
+                                                                  zskip, fV, fbp,
+                                                                  stamps.as<unsigned long long>() + ND_NSTAMP * lv);
             else
                 nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
-                                                            d_tickets + lv, d_status, pad_skip, d_tb, d_ri, zskip);
+                                                            d_tickets + lv, d_status, pad_skip, d_tb, d_ri, zskip,
+                                                            fV, fbp);
             BSM_HIP_TRY(hipGetLastError());
         }
         if (ext_merge && !pull) {
@@ -1931,9 +1985,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     }
     stage_mark("nd_factor", s);
     if (k > 0) {
-        nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
-                                                       bpb.as<T>());
-        BSM_HIP_TRY(hipGetLastError());
+        if (!fold) {
+            nd_gather<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, (int64_t)k, d_perm, static_cast<const T*>(b_dev),
+                                                           bpb.as<T>());
+            BSM_HIP_TRY(hipGetLastError());
+        }
         // Levels with fewer (node, column) pairs than CUs run their solves by
         // tiles (nd_forward_tiles / nd_backward_tiles: a front's chain of pivot
         // tiles on many waves), the others one workgroup per pair (nd_forward /
@@ -1949,7 +2005,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         int* const d_ftk = d_xf + n_pf;
         int* const d_btk = d_ftk + C.n_levels;
         const int64_t fwd_grid = (int64_t)cus * fper, bwd_grid = (int64_t)cus * bper;
-        for (int32_t lv = 0; lv < C.n_levels; ++lv) {
+        for (int32_t lv = 0; lv < C.n_levels && !fold; ++lv) {
             const int64_t o = C.lvl_off[(size_t)lv], c = C.lvl_off[(size_t)lv + 1] - o;
             if (c <= 0) continue;
             if (by_tiles(fwd_mode, c * (int64_t)k)) {

@@ -8,7 +8,8 @@ Per solve (solves: the line's nd_solves_in_process["full"], else the calls
 of nd_scatter, one per solve):
 * factor: nd_factor's time; true flops and 64-padded flops against the
   78.6 TF/s FP64 MFMA peak (MI355X_MICROARCH.md);
-* forward: nd_forward + nd_forward_tiles; backward: nd_backward +
+* forward: nd_forward + nd_forward_tiles (none when the forward solve is
+  folded into nd_factor, one right-hand side); backward: nd_backward +
   nd_backward_tiles; L's bytes (each entry read once) against 8 TB/s;
 * the fixed costs beside them (zero tiles, assemble, extend-add).
 
@@ -74,9 +75,11 @@ def main():
                    "achieved_TFs_padded": round(model["padded_flops"] / fac * 1e-9, 3),
                    "frac_padded": round(model["padded_flops"] / fac * 1e-9 / F64_PEAK_TFS, 4),
                    "peak_TFs": F64_PEAK_TFS},
-        "forward": {"kernels": "nd_forward + nd_forward_tiles", "ms": round(fwd, 4),
-                    "achieved_GBs": round(model["l_bytes"] / fwd * 1e-6, 1),
-                    "frac": round(model["l_bytes"] / fwd * 1e-6 / HBM_PEAK_GBS, 4), "peak_GBs": HBM_PEAK_GBS},
+        "forward": ({"kernels": "nd_forward + nd_forward_tiles", "ms": round(fwd, 4),
+                     "achieved_GBs": round(model["l_bytes"] / fwd * 1e-6, 1),
+                     "frac": round(model["l_bytes"] / fwd * 1e-6 / HBM_PEAK_GBS, 4), "peak_GBs": HBM_PEAK_GBS}
+                    if fwd > 0 else
+                    {"kernels": "none: folded into nd_factor's diagonal tiles (BSM_ND_FOLD)", "ms": 0.0}),
         "backward": {"kernels": "nd_backward + nd_backward_tiles", "ms": round(bwd, 4),
                      "achieved_GBs": round(model["l_bytes"] / bwd * 1e-6, 1),
                      "frac": round(model["l_bytes"] / bwd * 1e-6 / HBM_PEAK_GBS, 4), "peak_GBs": HBM_PEAK_GBS},

@@ -411,6 +411,39 @@ def test_nd_poisoned_fronts_irregular_trees(orc, monkeypatch, kind, leaf):
         assert rel_err(a0, ex[j]) < 1e-10
 
 
+@pytest.mark.parametrize("kind", ["poisson2d", "random", "blocks", "poisson3d"])
+@pytest.mark.parametrize("leaf", ["4", "64", "192"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_nd_folded_forward(orc, monkeypatch, kind, leaf, dtype):
+    """One right-hand side: the forward solve folded into the factor's
+    diagonal tiles (BSM_ND_FOLD, default) against the separate forward pass
+    (BSM_ND_FOLD=0), with the fronts NaN-poisoned: another summation order,
+    so within rounding (f64 1e-12, f32 1e-4 relative), and against the
+    oracle; two fresh runs of the folded form give the same bits."""
+    if kind == "poisson2d":
+        g = 60
+        n = g * g
+        rp, ci, v = orc.poisson2d(g)
+    else:
+        n, rp, ci, v = _irregular_systems(orc, kind)
+    v = v.astype(dtype)
+    monkeypatch.setenv("BSM_ND_LEAF", leaf)
+    monkeypatch.setenv("BSM_ND_CACHE", "0")
+    b = orc.gen_x_cols(1041, n, 1, dtype=dtype)
+    monkeypatch.setenv("BSM_ND_POISON", "1")
+    x1 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0))
+    x2 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0))
+    monkeypatch.setenv("BSM_ND_FOLD", "0")
+    x0 = np.asarray(solve(Csr.from_csr_arrays((n, n), rp, ci, v), Dense.from_columns(b), order="nd").get_col(0))
+    assert np.all(np.isfinite(x1))
+    assert np.array_equal(x1.view(np.uint8), x2.view(np.uint8))
+    tol = 1e-12 if dtype == np.float64 else 1e-4
+    assert rel_err(x1, x0) < tol
+    if dtype == np.float64:
+        ex = orc.solve(n, rp, ci, v, b, band=kind in ("poisson2d", "poisson3d"))[0]
+        assert rel_err(x1, ex) < 1e-10
+
+
 def poisson3d(g):
     """7-point Laplacian on a g^3 grid (natural order, band g^2), diagonal 6.5."""
     n = g ** 3

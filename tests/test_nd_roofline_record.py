@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 
 
-@pytest.mark.parametrize("tag", ["r06_c", "r06_o"])
+@pytest.mark.parametrize("tag", ["r06_c", "r06_o", "r06_w"])
 def test_nd_roofline_reproducible(tag):
     csv_p = os.path.join(PROF, f"{tag}_c5_nd_kernel_stats.csv")
     jsonl_p = os.path.join(PROF, f"{tag}_solve_c5_nd_profiled.jsonl")
@@ -38,4 +38,7 @@ def test_nd_roofline_reproducible(tag):
     with open(jsonl_p) as f:
         line = [json.loads(x) for x in f if x.startswith("{")][-1]
     assert line["model"]["true_flops"] < 1e11 and line["factor"]["frac_true"] <= 1
-    assert line["forward"]["frac"] <= 1 and line["backward"]["frac"] <= 1
+    # the forward solve folded into the factor (one right-hand side) has no
+    # pass, hence no fraction, of its own
+    assert line["forward"].get("folded") or line["forward"]["frac"] <= 1
+    assert line["backward"]["frac"] <= 1
