@@ -122,6 +122,96 @@ __global__ __launch_bounds__(256) void nd_mark_tasks(int64_t ntasks, const NdDev
     if (!zf[nd.tile_off + nd_lower_idx(nd.nt, tl.y, tl.z)]) tiles[t].w = 2;
 }
 
+// A's entries by tile (once per plan, from the pattern, with nd_assemble's
+// addressing): aoff[g] .. aoff[g + 1] are tile g's entries in aent, each
+// (CSR index << 12) | (column << 6 | row) within the tile. A counting sort:
+// nd_aent_count, nd_scan_tiles, nd_aent_fill (the order within a tile is
+// the atomics', but the places are distinct, so the tile they form is not).
+__device__ __forceinline__ int64_t nd_aent_key(int64_t i, int64_t j, const int32_t* __restrict__ pinv,
+                                               const int32_t* __restrict__ owner, const NdDev* __restrict__ nodes,
+                                               const int32_t* __restrict__ st, int32_t* pos) {
+    const int64_t pi = pinv[i], pj = pinv[j];
+    const int64_t r = pi > pj ? pi : pj, c = pi > pj ? pj : pi;
+    const NdDev& nd = nodes[owner[c]];
+    const int64_t lc = c - nd.start;
+    const int64_t lr = r < nd.start + nd.np ? r - nd.start : nd.np_pad + lower_bound_i32(st + nd.st_off, nd.m, r);
+    *pos = (int32_t)((lr & 63) | ((lc & 63) << 6));
+    return nd.tile_off + nd_lower_idx(nd.nt, (int32_t)(lr >> 6), (int32_t)(lc >> 6));
+}
+__global__ __launch_bounds__(256) void nd_aent_count(int64_t n, const int64_t* __restrict__ rp,
+                                                     const int32_t* __restrict__ col, const int32_t* __restrict__ pinv,
+                                                     const int32_t* __restrict__ owner,
+                                                     const NdDev* __restrict__ nodes, const int32_t* __restrict__ st,
+                                                     int32_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+        if (col[e] > i) continue;
+        int32_t pos;
+        atomicAdd(&cnt[nd_aent_key(i, col[e], pinv, owner, nodes, st, &pos)], 1);
+    }
+}
+// cnt[0 .. m) -> its exclusive prefix sums in aoff[0 .. m], one workgroup
+__global__ __launch_bounds__(1024) void nd_scan_tiles(int64_t m, const int32_t* __restrict__ cnt,
+                                                      int32_t* __restrict__ aoff) {
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t lo = m * t / 1024, hi = m * (t + 1) / 1024;
+    int64_t sum = 0;
+    for (int64_t g = lo; g < hi; ++g) sum += cnt[g];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the chunk sums
+        const int64_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int64_t run = part[t] - sum;
+    for (int64_t g = lo; g < hi; ++g) {
+        aoff[g] = (int32_t)run;
+        run += cnt[g];
+    }
+    if (t == 1023) aoff[m] = (int32_t)part[1023];
+}
+__global__ __launch_bounds__(256) void nd_aent_fill(int64_t n, const int64_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col, const int32_t* __restrict__ pinv,
+                                                    const int32_t* __restrict__ owner, const NdDev* __restrict__ nodes,
+                                                    const int32_t* __restrict__ st, const int32_t* __restrict__ aoff,
+                                                    int32_t* __restrict__ cur, int64_t* __restrict__ aent) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+        if (col[e] > i) continue;
+        int32_t pos;
+        const int64_t g = nd_aent_key(i, col[e], pinv, owner, nodes, st, &pos);
+        const int32_t slot = atomicAdd(&cur[g], 1);
+        aent[aoff[g] + slot] = (e << 12) | pos;
+    }
+}
+// per factor task (not a whole front): its tile's entry range (offset, count)
+__global__ __launch_bounds__(256) void nd_task_ranges(int64_t ntasks, const int4* __restrict__ tiles,
+                                                      const NdDev* __restrict__ nodes, const int32_t* __restrict__ aoff,
+                                                      int2* __restrict__ tq) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntasks) return;
+    const int4 tl = tiles[t];
+    if (tl.w == 1) {
+        tq[t] = make_int2(0, 0);
+        return;
+    }
+    const NdDev& nd = nodes[tl.x];
+    const int64_t g = nd.tile_off + nd_lower_idx(nd.nt, tl.y, tl.z);
+    tq[t] = make_int2(aoff[g], aoff[g + 1] - aoff[g]);
+}
+// per solve: the entries' values in tile order (a contiguous read per tile)
+template <typename T>
+__global__ __launch_bounds__(256) void nd_aent_vals(int64_t na, const int64_t* __restrict__ aent,
+                                                    const T* __restrict__ val, T* __restrict__ av) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < na) av[q] = val[aent[q] >> 12];
+}
+
 // zero the fronts' lower tiles (the only ones any kernel reads: every tile
 // of the factor's lists): 55 % of the bytes a memset of the whole squares
 // writes; with zf, only the tiles A's entries land in (nd_mark_tiles)
@@ -181,6 +271,8 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                                                  int* __restrict__ status, int pad_skip,
                                                  const int32_t* __restrict__ tb, const int32_t* __restrict__ ri,
                                                  int zskip, T* __restrict__ fV, const T* __restrict__ fbp,
+                                                 const int64_t* __restrict__ aent, const T* __restrict__ av,
+                                                 const int32_t* __restrict__ aoff, const int2* __restrict__ tq,
                                                  unsigned long long* __restrict__ stamps = nullptr) {
     long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
     long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
@@ -248,7 +340,12 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
         // the folded forward solve on this diagonal tile: w = b (pivot rows)
         const bool fold = fV && I == K;
         if (fold && tid < 64) fw[tid] = 64 * K + tid < nd.np ? fbp[nd.start + 64 * K + tid] : (T)0;
-        if (tb && (nd.kid0 >= 0 || nd.kid1 >= 0)) {
+        const bool kids = tb && (nd.kid0 >= 0 || nd.kid1 >= 0);
+        if (kids || aent) {
+            // aent: the tile starts from A's entries in it (and the padding
+            // pivots' identity), staged in LDS from the plan's per-tile lists,
+            // instead of from F (no zeroing, no assembly, no read of F): the
+            // same values, written the same way.
             // The children's update blocks, pulled into this tile (tb: no
             // nd_extend launches): the entries (a, b), a >= b, of child c
             // with ri[a] in tile row I and ri[b] in tile column K, i.e. a in
@@ -273,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             for (int h = 0; h < 2; ++h) {
                 const int c = h == nd.pull_swap ? nd.kid0 : nd.kid1;
                 bk[h].ra = 0;
-                if (c < 0) continue;
+                if (c < 0 || !kids) continue;
                 const NdDev& cd = nodes[c];
                 const int32_t* const tbc = tb + cd.tb_off;
                 bk[h].U = F + cd.foff + (int64_t)cd.np_pad * cd.ld + cd.np_pad;  // U[a][b] at U[b ld + a]
@@ -314,7 +411,23 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                 }
                 if (fold && w == 0 && lane < k.ra) fw[pr[h]] += uv;
             };
-            {
+            if (aent) {
+                int2 rq;
+                if (whole) {
+                    const int64_t g = nd.tile_off + nd_lower_idx(ntf, I, K);
+                    rq = make_int2(aoff[g], aoff[g + 1] - aoff[g]);
+                } else {
+                    rq = tq[t];
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) PT[lane][4 * u + w] = (T)0;
+                __syncthreads();
+                for (int q = tid; q < rq.y; q += 256) {
+                    const int64_t x = aent[rq.x + q];
+                    PT[x & 63][(x >> 6) & 63] = av[rq.x + q];
+                }
+                if (I == K && K < npt && tid < 64 && 64 * K + tid >= nd.np) PT[tid][tid] = (T)1;
+            } else {
                 T fv[16];  // the tile by columns: element (lane, 4 u + w)
 #pragma unroll
                 for (int u = 0; u < 16; ++u) fv[u] = (T)0;
@@ -1267,6 +1380,8 @@ struct NdCached {
     size_t o_dev = 0, o_st = 0, o_ri = 0, o_pinv = 0, o_owner = 0, o_lvl = 0, o_tiles = 0, o_ext = 0, o_ext2 = 0,
            o_ftask = 0, o_btask = 0, o_perm = 0, o_ztiles = 0, o_tb = 0, o_zf = 0;
     size_t n_tiles = 0, n_ztiles = 0, n_ext = 0;
+    int64_t n_lower = 0, n_aent = 0;  // the fronts' lower tiles; A's lower entries
+    DBuf aoff, aent, tq;              // A's entries by tile (nd_aent_*), per task ranges
     int32_t small_nt = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
@@ -1540,6 +1655,7 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
     C.n_flags = L.n_flags;
     C.vtot = L.vtot;
     C.n_tiles = L.tiles.size();
+    C.n_lower = L.n_lower;
     C.n_ztiles = L.ztiles.size();
     C.n_ext = L.ext.size();
     C.ms_graph = P.ms_graph;
@@ -1633,7 +1749,36 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             BSM_HIP_TRY(hipGetLastError());
         }
     }
-    BSM_HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next plan
+    {  // A's entries by tile: count, scan, fill; the factor tasks' ranges
+        char* pb = C.plan.as<char>();
+        const int32_t* d_pinv = (const int32_t*)(pb + C.o_pinv);
+        const int32_t* d_owner = (const int32_t*)(pb + C.o_owner);
+        const NdDev* d_dev = (const NdDev*)(pb + C.o_dev);
+        const int32_t* d_st = (const int32_t*)(pb + C.o_st);
+        DBuf cnt;
+        BSM_TRY(cnt.alloc((size_t)std::max<int64_t>(2 * C.n_lower, 1) * sizeof(int32_t), s));
+        BSM_TRY(C.aoff.alloc((size_t)(C.n_lower + 1) * sizeof(int32_t)));
+        BSM_TRY(C.aent.alloc((size_t)std::max<uint64_t>(a->nnz, 1) * sizeof(int64_t)));
+        BSM_TRY(C.tq.alloc((size_t)std::max<size_t>(C.n_tiles, 1) * sizeof(int2)));
+        BSM_HIP_TRY(hipMemsetAsync(cnt.p, 0, (size_t)std::max<int64_t>(2 * C.n_lower, 1) * sizeof(int32_t), s));
+        int32_t* d_cnt = cnt.as<int32_t>();
+        nd_aent_count<<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, d_pinv, d_owner, d_dev, d_st, d_cnt);
+        BSM_HIP_TRY(hipGetLastError());
+        nd_scan_tiles<<<1, 1024, 0, s>>>(C.n_lower, d_cnt, C.aoff.as<int32_t>());
+        BSM_HIP_TRY(hipGetLastError());
+        nd_aent_fill<<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, d_pinv, d_owner, d_dev, d_st,
+                                                       C.aoff.as<int32_t>(), d_cnt + C.n_lower, C.aent.as<int64_t>());
+        BSM_HIP_TRY(hipGetLastError());
+        if (C.n_tiles) {
+            nd_task_ranges<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>(
+                (int64_t)C.n_tiles, (const int4*)(pb + C.o_tiles), d_dev, C.aoff.as<int32_t>(), C.tq.as<int2>());
+            BSM_HIP_TRY(hipGetLastError());
+        }
+        int32_t na = 0;
+        BSM_HIP_TRY(hipMemcpyAsync(&na, C.aoff.as<int32_t>() + C.n_lower, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        BSM_HIP_TRY(hipStreamSynchronize(s));  // also: the staging buffer is reused by the next plan
+        C.n_aent = na;
+    }
     stage_mark("nd_upload", s);
     if (pre_fronts.joinable()) {  // the fronts' allocation: the wait for it as a stage of its own
         pre_fronts.join();
@@ -1869,6 +2014,11 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     // BSM_ND_FOLD=0: the forward solve as its own pass over L after the
     // factor. By default, with one right-hand side and the pull, the
     // factor's diagonal tiles form y and the update vectors themselves
+    // BSM_ND_APULL=0: the fronts zeroed (the marked tiles) and A assembled
+    // into them before the factor. By default, with the pull, each factor
+    // tile stages its own A entries from the plan's per-tile lists
+    const char* ape = getenv("BSM_ND_APULL");
+    const bool apull = pull && !(ape && atoi(ape) == 0);
     const char* foe = getenv("BSM_ND_FOLD");
     const bool fold = k == 1 && pull && !(foe && atoi(foe) == 0);
     // numeric storage: the plan's own buffers when this solve may hold them
@@ -1907,7 +2057,8 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     BSM_REQUIRE(fper >= 1 && bper >= 1, BSM_ERR_UNSUPPORTED, "nd solve kernels do not fit a CU");
     const int64_t n_pf = (C.dinv_elems / 4096) * (int64_t)k;  // flags per pass: one per node, column, pivot tile
     const size_t n_tf = 2 * (size_t)n_pf + 2 * (size_t)C.n_levels;  // forward flags, backward flags, tickets
-    DBuf bpb, vb, tfl;  // from the thread's cache of temporaries (no hipFree per solve)
+    DBuf bpb, vb, tfl, avb;  // from the thread's cache of temporaries (no hipFree per solve)
+    if (apull) BSM_TRY(avb.alloc((size_t)std::max<int64_t>(C.n_aent, 1) * sizeof(T), s));
     if (k > 0) {
         BSM_TRY(bpb.alloc((size_t)N * k * sizeof(T), s));
         BSM_TRY(vb.alloc((size_t)std::max<int64_t>(C.vtot, 1) * k * sizeof(T), s));
@@ -1926,16 +2077,28 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
         const hipError_t we = hipStreamWaitEvent(s, ev, 0);
         (void)hipEventDestroy(ev);
         BSM_HIP_TRY(we);
-    } else if (C.n_ztiles) {
+    } else if (C.n_ztiles && !apull) {
         nd_zero_tiles<T><<<(unsigned)C.n_ztiles, 256, 0, s>>>(d_nodes, d_ztiles, F, d_zf);
         BSM_HIP_TRY(hipGetLastError());
     }
-    nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals), d_pinv,
-                                                     d_owner, d_nodes, d_st, F);
-    BSM_HIP_TRY(hipGetLastError());
-    nd_pad_pivots<T><<<(unsigned)C.nn, 64, 0, s>>>(d_nodes, F);
-    BSM_HIP_TRY(hipGetLastError());
+    if (apull) {  // A's values in the per-tile lists' order
+        if (C.n_aent > 0) {
+            nd_aent_vals<T><<<nd_blocks(C.n_aent, 256), 256, 0, s>>>(C.n_aent, C.aent.as<int64_t>(),
+                                                                    static_cast<const T*>(a->vals), avb.as<T>());
+            BSM_HIP_TRY(hipGetLastError());
+        }
+    } else {
+        nd_assemble<T><<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, static_cast<const T*>(a->vals),
+                                                         d_pinv, d_owner, d_nodes, d_st, F);
+        BSM_HIP_TRY(hipGetLastError());
+        nd_pad_pivots<T><<<(unsigned)C.nn, 64, 0, s>>>(d_nodes, F);
+        BSM_HIP_TRY(hipGetLastError());
+    }
     stage_mark("nd_assemble", s);
+    const int64_t* const d_aent = apull ? C.aent.as<int64_t>() : nullptr;
+    const T* const d_av = apull ? avb.as<T>() : nullptr;
+    const int32_t* const d_aoff = apull ? C.aoff.as<int32_t>() : nullptr;
+    const int2* const d_tq = apull ? C.tq.as<int2>() : nullptr;
     // BSM_ND_STAMPS=1: nd_factor's per-level cycle stamps, printed after the solve
     const char* sde = getenv("BSM_ND_STAMPS");
     DBuf stamps;
@@ -1961,12 +2124,12 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
             if (stamps.p)
                 nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                                   d_tickets + lv, d_status, pad_skip, d_tb, d_ri,
-                                                                  zskip, fV, fbp,
+                                                                  zskip, fV, fbp, d_aent, d_av, d_aoff, d_tq ? d_tq + t0 : nullptr,
                                                                   stamps.as<unsigned long long>() + ND_NSTAMP * lv);
             else
                 nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                             d_tickets + lv, d_status, pad_skip, d_tb, d_ri, zskip,
-                                                            fV, fbp);
+                                                            fV, fbp, d_aent, d_av, d_aoff, d_tq ? d_tq + t0 : nullptr);
             BSM_HIP_TRY(hipGetLastError());
         }
         if (ext_merge && !pull) {

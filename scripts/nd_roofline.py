@@ -31,7 +31,7 @@ def kernel_ns(path, dtype):
             name = row["Name"]
             for short in ("nd_factor", "nd_forward_tiles", "nd_forward", "nd_backward_tiles", "nd_backward",
                           "nd_zero_tiles", "nd_assemble", "nd_extend2", "nd_extend", "nd_pad_pivots", "nd_gather",
-                          "nd_scatter", "nd_pattern_hash", "nd_pattern_diff"):
+                          "nd_scatter", "nd_aent_vals", "nd_pattern_hash", "nd_pattern_diff"):
                 # nd_factor<double, false>: the product instantiation (STAMPS off)
                 if (f"{short}<{dtype}>" in name or f"{short}<{dtype}, false>" in name
                         or (short.startswith("nd_pattern") and f"{short}(" in name)):
@@ -84,7 +84,8 @@ def main():
                      "achieved_GBs": round(model["l_bytes"] / bwd * 1e-6, 1),
                      "frac": round(model["l_bytes"] / bwd * 1e-6 / HBM_PEAK_GBS, 4), "peak_GBs": HBM_PEAK_GBS},
         "fixed_ms_per_solve": {n: round(ms(n), 4) for n in ("nd_zero_tiles", "nd_assemble", "nd_pad_pivots",
-                                                            "nd_extend2", "nd_extend", "nd_gather", "nd_scatter")
+                                                            "nd_aent_vals", "nd_extend2", "nd_extend", "nd_gather",
+                                                            "nd_scatter")
                                if k.get(n)},
     }
     for part in ("factor", "forward", "backward"):

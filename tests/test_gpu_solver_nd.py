@@ -279,7 +279,8 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
-                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL", "BSM_ND_ZSKIP"])
+                                    "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL", "BSM_ND_ZSKIP",
+                                    "BSM_ND_APULL"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -313,7 +314,10 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
       adds in the same order;
     * BSM_ND_ZSKIP: the tiles no entry of A lands in start from zero in
       the factor, neither zeroed before nor read, instead of zeroed and
-      read: the same values.
+      read: the same values;
+    * BSM_ND_APULL: every factor tile stages its own entries of A (and the
+      padding pivots' 1) from the plan's per-tile lists, instead of the
+      fronts being zeroed and A assembled into them: the same values.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
