@@ -204,6 +204,41 @@ __global__ __launch_bounds__(256) void nd_task_ranges(int64_t ntasks, const int4
     const int64_t g = nd.tile_off + nd_lower_idx(nd.nt, tl.y, tl.z);
     tq[t] = make_int2(aoff[g], aoff[g + 1] - aoff[g]);
 }
+// per factor task (not a whole front): its children's blocks, first and
+// second in nd_extend2's order (NdPull::ra = 0: none), so the tile reads
+// them with its task instead of through node -> child -> bounds
+struct NdPull {
+    int64_t uoff;   // the child's update block U at F + uoff (U[a][b] at uoff + b ld + a)
+    int64_t uvoff;  // its update vector at V + uvoff (the folded forward solve)
+    int32_t rcoff, ld, a0, ra, b0, rbn;
+};
+__global__ __launch_bounds__(256) void nd_task_pull(int64_t ntasks, const int4* __restrict__ tiles,
+                                                    const NdDev* __restrict__ nodes, const int32_t* __restrict__ tb,
+                                                    NdPull* __restrict__ pd) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntasks) return;
+    const int4 tl = tiles[t];
+    const NdDev& nd = nodes[tl.x];
+    for (int h = 0; h < 2; ++h) {
+        NdPull o{0, 0, 0, 0, 0, 0, 0, 0};
+        const int c = h == nd.pull_swap ? nd.kid0 : nd.kid1;
+        if (c >= 0 && tl.w != 1) {
+            const NdDev& cd = nodes[c];
+            const int32_t* const tbc = tb + cd.tb_off;
+            o.uoff = cd.foff + (int64_t)cd.np_pad * cd.ld + cd.np_pad;
+            o.uvoff = cd.voff + cd.np_pad;
+            o.rcoff = (int32_t)cd.st_off;
+            o.ld = cd.ld;
+            o.a0 = tbc[tl.y];
+            o.ra = tbc[tl.y + 1] - o.a0;
+            o.b0 = tbc[tl.z];
+            o.rbn = tbc[tl.z + 1] - o.b0;
+            if (o.rbn <= 0) o.ra = 0;
+        }
+        pd[2 * t + h] = o;
+    }
+}
+
 // per solve: the entries' values in tile order (a contiguous read per tile)
 template <typename T>
 __global__ __launch_bounds__(256) void nd_aent_vals(int64_t na, const int64_t* __restrict__ aent,
@@ -273,6 +308,7 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
                                                  int zskip, T* __restrict__ fV, const T* __restrict__ fbp,
                                                  const int64_t* __restrict__ aent, const T* __restrict__ av,
                                                  const int32_t* __restrict__ aoff, const int2* __restrict__ tq,
+                                                 const NdPull* __restrict__ pdesc,
                                                  unsigned long long* __restrict__ stamps = nullptr) {
     long long c_wait = 0, c_prod = 0, c_diag = 0, c_trsm = 0, c_upd = 0, c_drain = 0;
     long long n_prod = 0, n_diag = 0, n_trsm = 0, n_upd = 0, c_total = 0, n_tiles = 0;
@@ -368,9 +404,22 @@ __global__ __launch_bounds__(256, 2) void nd_factor(const NdDev* __restrict__ no
             } bk[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int c = h == nd.pull_swap ? nd.kid0 : nd.kid1;
                 bk[h].ra = 0;
-                if (c < 0 || !kids) continue;
+                if (!kids) continue;
+                if (pdesc && !whole) {  // the task's own descriptors (nd_task_pull)
+                    const NdPull& o = pdesc[2 * t + h];
+                    bk[h].U = F + o.uoff;
+                    bk[h].rc = ri + o.rcoff;
+                    bk[h].u = fV ? fV + o.uvoff : nullptr;
+                    bk[h].ld = o.ld;
+                    bk[h].a0 = o.a0;
+                    bk[h].ra = o.ra;
+                    bk[h].b0 = o.b0;
+                    bk[h].rbn = o.rbn;
+                    continue;
+                }
+                const int c = h == nd.pull_swap ? nd.kid0 : nd.kid1;
+                if (c < 0) continue;
                 const NdDev& cd = nodes[c];
                 const int32_t* const tbc = tb + cd.tb_off;
                 bk[h].U = F + cd.foff + (int64_t)cd.np_pad * cd.ld + cd.np_pad;  // U[a][b] at U[b ld + a]
@@ -1382,6 +1431,7 @@ struct NdCached {
     size_t n_tiles = 0, n_ztiles = 0, n_ext = 0;
     int64_t n_lower = 0, n_aent = 0;  // the fronts' lower tiles; A's lower entries
     DBuf aoff, aent, tq;              // A's entries by tile (nd_aent_*), per task ranges
+    DBuf pdesc;                       // per task: its children's blocks (nd_task_pull)
     int32_t small_nt = 0;
     double ms_graph = 0, ms_order = 0, ms_symbolic = 0, ms_layout = 0, ms_pack = 0;
     DBuf plan;
@@ -1773,6 +1823,11 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             nd_task_ranges<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>(
                 (int64_t)C.n_tiles, (const int4*)(pb + C.o_tiles), d_dev, C.aoff.as<int32_t>(), C.tq.as<int2>());
             BSM_HIP_TRY(hipGetLastError());
+            BSM_TRY(C.pdesc.alloc(C.n_tiles * 2 * sizeof(NdPull)));
+            nd_task_pull<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>(
+                (int64_t)C.n_tiles, (const int4*)(pb + C.o_tiles), d_dev, (const int32_t*)(pb + C.o_tb),
+                C.pdesc.as<NdPull>());
+            BSM_HIP_TRY(hipGetLastError());
         }
         int32_t na = 0;
         BSM_HIP_TRY(hipMemcpyAsync(&na, C.aoff.as<int32_t>() + C.n_lower, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -2099,6 +2154,10 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     const T* const d_av = apull ? avb.as<T>() : nullptr;
     const int32_t* const d_aoff = apull ? C.aoff.as<int32_t>() : nullptr;
     const int2* const d_tq = apull ? C.tq.as<int2>() : nullptr;
+    // BSM_ND_PDESC=0: the pull finds its children's blocks through the
+    // node, the child and the bounds (A/B; same bits)
+    const char* pde = getenv("BSM_ND_PDESC");
+    const NdPull* const d_pd = pull && C.pdesc.p && !(pde && atoi(pde) == 0) ? C.pdesc.as<NdPull>() : nullptr;
     // BSM_ND_STAMPS=1: nd_factor's per-level cycle stamps, printed after the solve
     const char* sde = getenv("BSM_ND_STAMPS");
     DBuf stamps;
@@ -2125,11 +2184,13 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
                 nd_factor<T, true><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                                   d_tickets + lv, d_status, pad_skip, d_tb, d_ri,
                                                                   zskip, fV, fbp, d_aent, d_av, d_aoff, d_tq ? d_tq + t0 : nullptr,
+                                                                  d_pd ? d_pd + 2 * t0 : nullptr,
                                                                   stamps.as<unsigned long long>() + ND_NSTAMP * lv);
             else
                 nd_factor<T><<<(unsigned)grid, 256, 0, s>>>(d_nodes, d_tiles + t0, nt, F, dv.as<T>(), d_flags,
                                                             d_tickets + lv, d_status, pad_skip, d_tb, d_ri, zskip,
-                                                            fV, fbp, d_aent, d_av, d_aoff, d_tq ? d_tq + t0 : nullptr);
+                                                            fV, fbp, d_aent, d_av, d_aoff, d_tq ? d_tq + t0 : nullptr,
+                                                            d_pd ? d_pd + 2 * t0 : nullptr);
             BSM_HIP_TRY(hipGetLastError());
         }
         if (ext_merge && !pull) {

@@ -280,7 +280,7 @@ def test_nd_plan_cache_bounded(orc, monkeypatch):
 
 @pytest.mark.parametrize("switch", ["BSM_ND_PAD_SKIP", "BSM_ND_EXT_MERGE", "BSM_ND_FWD_TILES", "BSM_ND_BWD_TILES",
                                     "BSM_ND_FRONT_NT", "BSM_ND_LAG", "BSM_ND_PULL", "BSM_ND_ZSKIP",
-                                    "BSM_ND_APULL"])
+                                    "BSM_ND_APULL", "BSM_ND_PDESC"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("leaf", ["8", "100", "192"])
 def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
@@ -317,7 +317,10 @@ def test_nd_shortcuts_same_bits(orc, monkeypatch, switch, dtype, leaf):
       read: the same values;
     * BSM_ND_APULL: every factor tile stages its own entries of A (and the
       padding pivots' 1) from the plan's per-tile lists, instead of the
-      fronts being zeroed and A assembled into them: the same values.
+      fronts being zeroed and A assembled into them: the same values;
+    * BSM_ND_PDESC: the pull reads its children's blocks from per-task
+      descriptors built once per plan, instead of through the node, the
+      child and the bounds: the same blocks.
     (At this size every level has fewer fronts than CUs, so the default runs
     the tile kernels on every level.)"""
     monkeypatch.setenv("BSM_ND_LEAF", leaf)
