@@ -1657,11 +1657,19 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         }
     } join_fronts{pre_fronts};
     if (es) {
-        int64_t f_elems = 0;  // nd_layout's sum of the fronts' f_pad^2
+        int64_t f_elems = 0, dinv_elems = 0, n_flags = 0;  // nd_layout's sums (fronts, inverse tiles, flags)
         for (const auto& x : P.nodes) {
-            const int64_t np_pad = 64 * ((x.end - x.start + 63) / 64), ld = 64 * ((np_pad + (int64_t)x.st.size() + 63) / 64);
+            const int64_t npt = (x.end - x.start + 63) / 64, np_pad = 64 * npt;
+            const int64_t nt = (np_pad + (int64_t)x.st.size() + 63) / 64, ld = 64 * nt;
             f_elems += ld * ld;
+            dinv_elems += npt * 4096;
+            n_flags += nt * npt;
         }
+        // the inverse diagonal tiles and the flags too, at the sizes nd_solve
+        // asks for (a fresh hipMalloc of ~0.8 GB took ms inside the first
+        // solve when the box had just freed memory)
+        const size_t dv_bytes = (size_t)std::max<int64_t>(dinv_elems, 1) * es;
+        const size_t fl_bytes = ((size_t)n_flags + (size_t)P.n_levels + 2) * sizeof(int);
         const int dev = a->device;
         // BSM_ND_PREZERO=1: also zeroed whole there, on a stream of its own
         // (round 6 before the marked tiles: a fresh allocation's first touch
@@ -1671,8 +1679,10 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         // (profiles/r06_m_*)
         const char* pze = getenv("BSM_ND_PREZERO");
         const bool prezero = pze && atoi(pze) == 1;
-        pre_fronts = std::thread([&C, f_elems, es, dev, prezero] {
+        pre_fronts = std::thread([&C, f_elems, es, dev, prezero, dv_bytes, fl_bytes] {
             if (hipSetDevice(dev) != hipSuccess || C.fr.alloc((size_t)f_elems * es) != BSM_OK) return;
+            (void)C.dv.alloc(dv_bytes);  // nd_solve allocates again if this failed
+            (void)C.fl.alloc(fl_bytes);
             if (!prezero) return;
             hipStream_t z = nullptr;
             hipEvent_t ev = nullptr;

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 
 
-@pytest.mark.parametrize("tag", ["r06_c", "r06_o", "r06_w", "r06_x"])
+@pytest.mark.parametrize("tag", ["r06_c", "r06_o", "r06_w", "r06_x", "r06_z"])
 def test_nd_roofline_reproducible(tag):
     csv_p = os.path.join(PROF, f"{tag}_c5_nd_kernel_stats.csv")
     jsonl_p = os.path.join(PROF, f"{tag}_solve_c5_nd_profiled.jsonl")
