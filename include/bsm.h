@@ -197,7 +197,12 @@ int bsm_solve_blocked(const bsm_csr* a, uint64_t k, uint64_t n, const void* cons
  * plans' kept storage and retries. bsm_nd_cache_clear releases every cached
  * plan not also held by a live handle (bsm_csr_free releases the handle's).
  * Env BSM_ND_CACHE=0: no plan kept anywhere; BSM_ND_SHARED=0: per handle only;
- * BSM_ND_KEEP=0: numeric storage freed after every solve. */
+ * BSM_ND_KEEP=0: numeric storage freed after every solve. A plan also holds
+ * A's lower entries sorted by front tile (8 bytes each) and two small
+ * per-task arrays. With one right-hand side (k == 1) the forward solve is
+ * formed inside the factor (another summation order than k > 1, within
+ * rounding; BSM_ND_FOLD=0 turns it off). The factor's other switches
+ * (README.md's table) change no bits. */
 int bsm_solve_nd(const bsm_csr* a, uint64_t k, uint64_t n, const void* const* b_cols,
                  void* const* x_cols);
 /* The cross-handle plan cache of bsm_solve_nd: drop every entry, or read its
