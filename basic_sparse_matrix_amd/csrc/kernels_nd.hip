@@ -1815,11 +1815,18 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
         const int32_t* d_owner = (const int32_t*)(pb + C.o_owner);
         const NdDev* d_dev = (const NdDev*)(pb + C.o_dev);
         const int32_t* d_st = (const int32_t*)(pb + C.o_st);
+        // every buffer first: an error return after a launch would free
+        // buffers queued kernels still write (and the guard drains the stream)
         DBuf cnt;
         BSM_TRY(cnt.alloc((size_t)std::max<int64_t>(2 * C.n_lower, 1) * sizeof(int32_t), s));
         BSM_TRY(C.aoff.alloc((size_t)(C.n_lower + 1) * sizeof(int32_t)));
         BSM_TRY(C.aent.alloc((size_t)std::max<uint64_t>(a->nnz, 1) * sizeof(int64_t)));
         BSM_TRY(C.tq.alloc((size_t)std::max<size_t>(C.n_tiles, 1) * sizeof(int2)));
+        BSM_TRY(C.pdesc.alloc((size_t)std::max<size_t>(C.n_tiles, 1) * 2 * sizeof(NdPull)));
+        struct Drain {
+            hipStream_t s;
+            ~Drain() { (void)hipStreamSynchronize(s); }
+        } drain{s};
         BSM_HIP_TRY(hipMemsetAsync(cnt.p, 0, (size_t)std::max<int64_t>(2 * C.n_lower, 1) * sizeof(int32_t), s));
         int32_t* d_cnt = cnt.as<int32_t>();
         nd_aent_count<<<nd_blocks(N, 256), 256, 0, s>>>(N, a->row_ptr, a->col, d_pinv, d_owner, d_dev, d_st, d_cnt);
@@ -1833,7 +1840,6 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             nd_task_ranges<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>(
                 (int64_t)C.n_tiles, (const int4*)(pb + C.o_tiles), d_dev, C.aoff.as<int32_t>(), C.tq.as<int2>());
             BSM_HIP_TRY(hipGetLastError());
-            BSM_TRY(C.pdesc.alloc(C.n_tiles * 2 * sizeof(NdPull)));
             nd_task_pull<<<nd_blocks((int64_t)C.n_tiles, 256), 256, 0, s>>>(
                 (int64_t)C.n_tiles, (const int4*)(pb + C.o_tiles), d_dev, (const int32_t*)(pb + C.o_tb),
                 C.pdesc.as<NdPull>());
