@@ -1809,7 +1809,10 @@ int nd_build_plan(const bsm_csr* a, int64_t leaf, int32_t small_nt, size_t es, h
             BSM_HIP_TRY(hipGetLastError());
         }
     }
-    {  // A's entries by tile: count, scan, fill; the factor tasks' ranges
+    // A's entries by tile: count, scan, fill; the factor tasks' ranges (the
+    // offsets are 32-bit: a pattern with 2^31 or more lower entries keeps
+    // the zeroing and the assembly instead, BSM_ND_APULL=0's path)
+    if (a->nnz < ((uint64_t)1 << 31)) {
         char* pb = C.plan.as<char>();
         const int32_t* d_pinv = (const int32_t*)(pb + C.o_pinv);
         const int32_t* d_owner = (const int32_t*)(pb + C.o_owner);
@@ -2089,7 +2092,7 @@ int nd_solve(const bsm_csr* a, uint64_t k, uint64_t n, const void* b_dev, void* 
     // into them before the factor. By default, with the pull, each factor
     // tile stages its own A entries from the plan's per-tile lists
     const char* ape = getenv("BSM_ND_APULL");
-    const bool apull = pull && !(ape && atoi(ape) == 0);
+    const bool apull = pull && C.aent.p && !(ape && atoi(ape) == 0);
     const char* foe = getenv("BSM_ND_FOLD");
     const bool fold = k == 1 && pull && !(foe && atoi(foe) == 0);
     // numeric storage: the plan's own buffers when this solve may hold them
