@@ -979,14 +979,22 @@ __global__ __launch_bounds__(256) void nd_backward(const NdDev* __restrict__ nod
         // the pivot tiles' x arrive)
         const T* lc = Fn + (int64_t)(64 * K + 16 * wv) * ld;
         const int rlo = 64 * (K + 1);
+        // a zero row of L (past f, or a pivot padding row) has w = 0 exactly:
+        // its loads go to a real row's address instead (the same cache lines
+        // for every such lane, so no HBM bytes), unconditionally (they still
+        // go out together), and the term stays 0 (an accumulator that starts
+        // at +0 never becomes -0): the same sums, the same bits
+        const int f = nd.np_pad + nd.m;
+        auto row = [&](int rr) { return rr >= f ? f - 1 : (rr >= nd.np && rr < nd.np_pad ? nd.np - 1 : rr); };
         int r = fp - 64 + lane;
         for (; r - 64 >= rlo; r -= 128) {
             const T w0 = ld_sc1(&w[r]), w1 = ld_sc1(&w[r - 64]);
+            const int q0 = row(r), q1 = row(r - 64);
             T l0[16], l1[16];
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
-                l0[c] = lc[(int64_t)c * ld + r];
-                l1[c] = lc[(int64_t)c * ld + r - 64];
+                l0[c] = lc[(int64_t)c * ld + q0];
+                l1[c] = lc[(int64_t)c * ld + q1];
             }
 #pragma unroll
             for (int c = 0; c < 16; ++c) acc[c] = fma_t(l1[c], w1, fma_t(l0[c], w0, acc[c]));
