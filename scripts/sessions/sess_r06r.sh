@@ -1,4 +1,6 @@
 # round 6, session r: the host analysis with the child graphs extracted on
+# (To rerun: the A/B side is not committed; recreate scripts/perf/nd_order_prev.cpp
+# first with git show <commit before the session>:basic_sparse_matrix_amd/csrc/nd_order.cpp.)
 # several threads at the top depths, against the build before it
 # (scripts/perf/nd_order_prev.cpp: the previous commit's nd_order.cpp),
 # alternating, on the box's CPUs. To rerun: the A/B side is not committed;
