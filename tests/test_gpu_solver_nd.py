@@ -451,6 +451,25 @@ def test_nd_folded_forward(orc, monkeypatch, kind, leaf, dtype):
         assert rel_err(x1, ex) < 1e-10
 
 
+def test_nd_one_and_several_right_hand_sides_agree(orc, monkeypatch):
+    """k = 1 takes the folded forward solve, k = 3 the separate pass: every
+    column of a three-column solve agrees with its one-column solve within
+    rounding (and both with the oracle)."""
+    monkeypatch.setenv("BSM_ND_LEAF", "64")
+    g = 50
+    n = g * g
+    rp, ci, v = orc.poisson2d(g)
+    b = orc.gen_x_cols(1051, n, 3)
+    A = Csr.from_csr_arrays((n, n), rp, ci, v)
+    x3 = solve(A, Dense.from_columns(b), order="nd")
+    ex = orc.solve(n, rp, ci, v, b, band=True)
+    for j in range(3):
+        x1 = np.asarray(solve(A, Dense.from_columns([b[j]]), order="nd").get_col(0))
+        xj = np.asarray(x3.get_col(j))
+        assert rel_err(x1, xj) < 1e-12
+        assert rel_err(x1, ex[j]) < 1e-10
+
+
 def poisson3d(g):
     """7-point Laplacian on a g^3 grid (natural order, band g^2), diagonal 6.5."""
     n = g ** 3
